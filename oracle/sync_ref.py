@@ -1,0 +1,173 @@
+"""ORACLE -- test infrastructure only.
+
+CPU restatement of the sync-selection half of the hot path, over an sqlite3 `sync` table with the reference's
+columns (dispersydatabase.py:53-64).  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import it.  Pinned against tests/golden/sync_vectors.json (outputs of the reference's own methods, lifted from
+community.py by tests/golden/gen_sync_golden.py).
+
+Restated functions (reference file:line):
+  respond_lists        community.py:2746-2811 (_get_packets_for_bloomfilters) + :2555-2567 (byte-limited loop)
+  select_and_fix       community.py:881-903
+  select_range         community.py:839-879
+  claim_largest        community.py:763-837
+  claim_modulo         community.py:908-933
+"""
+import math
+
+MAX_GT = 2 ** 63 - 1
+
+
+def syncable(metas):
+    """Metas synced by bloom filters: SyncDistribution with priority > 32 (community.py:767, :2790-2794)."""
+    return [m for m in metas if m["priority"] > 32]
+
+
+def ordered_metas(metas):
+    """Priority DESC, stable over declaration order (community.py:2790-2794)."""
+    return sorted(syncable(metas), key=lambda m: m["priority"], reverse=True)
+
+
+def meta_time_low(meta, time_low, global_time, include_inactive):
+    """community.py:2800-2808: with include_inactive=False, GlobalTimePruning metas only offer active packets."""
+    if include_inactive or not meta.get("pruning"):
+        return time_low
+    inactive = meta["pruning"][0]
+    return min(max(time_low, global_time - inactive + 1), MAX_GT)
+
+
+_ORDER = {"ASC": "global_time ASC", "DESC": "global_time DESC", "RANDOM": "RANDOM()"}
+
+
+def selected_rows(conn, metas, time_low, time_high, offset, modulo, global_time, include_inactive):
+    """[(id, packet)] in the order the reference's UNION ALL query yields them."""
+    out = []
+    for meta in ordered_metas(metas):
+        lo = meta_time_low(meta, time_low, global_time, include_inactive)
+        sql = ("SELECT id, packet FROM sync WHERE meta_message = ? AND undone = 0 AND global_time BETWEEN ? AND ? "
+               "AND (global_time + ?) % ? = 0 ORDER BY " + _ORDER[meta["direction"]])
+        out.extend((i, bytes(p)) for i, p in conn.execute(sql, (meta["id"], lo, time_high, offset, modulo)))
+    return out
+
+
+def respond_lists(conn, metas, request, bloom, global_time, byte_limit, include_inactive=False):
+    """Row ids the responder sends for one claim, in send order.
+
+    request: (time_low, time_high, offset, modulo) with time_high already resolved (0 -> global_time) and clamped.
+    bloom: an object with not_filter(iterator of tuples) (OracleBloom).
+    """
+    time_low, time_high, offset, modulo = request
+    rows = selected_rows(conn, metas, time_low, time_high, offset, modulo, global_time, include_inactive)
+    sent = []
+    budget = byte_limit
+    for packet, rid in bloom.not_filter((p, i) for i, p in rows):
+        sent.append(rid)
+        budget -= len(packet)
+        if budget <= 0:
+            break
+    return sent
+
+
+# ---------------------------------------------------------------------------------------------- claim side
+def _ids(metas):
+    return ", ".join(str(m["id"]) for m in syncable(metas))
+
+
+def select_and_fix(conn, metas, global_time, to_select, higher=True):
+    cmp, order = (">", "ASC") if higher else ("<", "DESC")
+    data = [(g, bytes(p)) for g, p in conn.execute(
+        "SELECT global_time, packet FROM sync WHERE meta_message IN (%s) AND undone = 0 AND global_time %s ? "
+        "ORDER BY global_time %s LIMIT ?" % (_ids(metas), cmp, order), (global_time, to_select + 1))]
+    fixed = len(data) > to_select
+    if fixed:
+        # the last global time may be only partially selected: drop that whole group
+        cut = data[-1][0]
+        data.pop()
+        while data and data[-1][0] == cut:
+            data.pop()
+    if not higher:
+        data.reverse()
+    return data, fixed
+
+
+def select_range(conn, metas, global_time, to_select, higher, own_global_time, acceptable):
+    data, fixed = select_and_fix(conn, metas, global_time, to_select, higher)
+    lowerfixed = higherfixed = True
+    if len(data) < to_select:
+        remain = to_select - len(data)
+        if remain > 25:
+            if higher:
+                more, lowerfixed = select_and_fix(conn, metas, global_time + 1, remain, False)
+                data = more + data
+            else:
+                more, higherfixed = select_and_fix(conn, metas, global_time - 1, remain, True)
+                data = data + more
+    rng = [data[0][0], data[-1][0], len(data)]  # IndexError on empty data, as community.py:857
+    if higher:
+        rng[0] = min(rng[0], global_time + 1)
+        if not fixed:
+            rng[1] = acceptable
+        if not lowerfixed:
+            rng[0] = 1
+    else:
+        rng[1] = max(rng[1], global_time - 1)
+        if not fixed:
+            rng[0] = 1
+        if not higherfixed:
+            rng[1] = acceptable
+    return rng, data
+
+
+def claim_largest(conn, metas, bits, error_rate, global_time, acceptable, nrsync, draws, bloom_cls):
+    """Returns ((time_low, time_high, modulo, offset, bloom), nrsync_after)."""
+    if not syncable(metas):
+        return (1, acceptable, 1, 0, bloom_cls.from_m_f(8, 0.1, b"\x00")), nrsync
+    bloom = bloom_cls.from_m_f(bits, error_rate, bytes([int(draws.random() * 256)]))
+    from oracle.bloom_ref import capacity_for
+    capacity = capacity_for(bloom.m, error_rate)
+    gt = max(1, global_time)
+    pivot = gt - int(draws.expovariate(1.0 / (gt / 2.0)))
+    if pivot < 1:
+        pivot = int(draws.random() * gt)
+    if pivot > 1 and nrsync >= capacity:
+        right, rdata = select_range(conn, metas, pivot - 1, capacity, True, gt, acceptable)
+        if right[2] == capacity:
+            left, ldata = select_range(conn, metas, pivot + 1, capacity, False, gt, acceptable)
+            if (left[1] or gt) - left[0] > (right[1] or gt) - right[0]:
+                rng, data = left, ldata
+            else:
+                rng, data = right, rdata
+        else:
+            rng, data = right, rdata
+    else:
+        rng = [1, acceptable]
+        data, fixed = select_and_fix(conn, metas, 0, capacity, True)
+        if data and fixed:
+            rng[1] = data[-1][0]
+            nrsync = capacity + 1
+    if data:
+        bloom.add_keys(p for _, p in data)
+        return (min(rng[0], acceptable), min(rng[1], acceptable), 1, 0, bloom), nrsync
+    return (1, acceptable, 1, 0, bloom_cls.from_m_f(8, 0.1, b"\x00")), nrsync
+
+
+def claim_modulo(conn, metas, bits, error_rate, acceptable, draws, bloom_cls):
+    """Returns ((1, acceptable, modulo, offset, bloom), nrsync_after)."""
+    if not syncable(metas):
+        return (1, acceptable, 1, 0, bloom_cls.from_m_f(8, 0.1, b"\x00")), 0
+    bloom = bloom_cls.from_m_f(bits, error_rate, bytes([int(draws.random() * 256)]))
+    from oracle.bloom_ref import capacity_for
+    capacity = capacity_for(bloom.m, error_rate)
+    ids = _ids(metas)
+    nrsync = conn.execute("SELECT count(*) FROM sync WHERE meta_message IN (%s) AND undone = 0" % ids).fetchone()[0]
+    modulo = int(math.ceil(nrsync / float(capacity)))
+    if modulo > 1:
+        offset = draws.randint(0, modulo - 1)
+        packets = [bytes(p) for p, in conn.execute(
+            "SELECT packet FROM sync WHERE meta_message IN (%s) AND undone = 0 AND (global_time + ?) %% ? = 0" % ids,
+            (offset, modulo))]
+    else:
+        offset, modulo = 0, 1
+        packets = [bytes(p) for p, in conn.execute(
+            "SELECT packet FROM sync WHERE meta_message IN (%s) AND undone = 0" % ids)]
+    bloom.add_keys(packets)
+    return (1, acceptable, modulo, offset, bloom), nrsync
