@@ -1,0 +1,779 @@
+// dsy_capi.hip -- the extern "C" boundary (include/dsybloom.h): contexts, workspaces, validation that mirrors
+// the reference's asserts, staging of host buffers, and orchestration of the responder windows.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "dsy_kernels.h"
+
+using namespace dsy;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                              \
+    do {                                                                                           \
+        hipError_t _e = (expr);                                                                    \
+        if (_e != hipSuccess) return fail(DSY_EHIP, "%s failed: %s", #expr, hipGetErrorString(_e)); \
+    } while (0)
+
+struct DevBuf {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+};
+
+enum TimerClass { kTimePairTest = 0, kTimeBuild = 1, kTimeSelect = 2, kTimeCompact = 3, kTimeClasses = 4 };
+
+struct PendingTimer {
+    int cls;
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct dsy_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    std::map<std::string, DevBuf> ws;
+    uint32_t max_grid = 2048;
+    bool timing = false;
+    std::vector<PendingTimer> pending;
+    std::vector<hipEvent_t> event_pool;
+    double time_ms[kTimeClasses] = {0, 0, 0, 0};
+    uint64_t launches[kTimeClasses] = {0, 0, 0, 0};
+    uint64_t blocks[kTimeClasses] = {0, 0, 0, 0};
+    uint64_t bytes[kTimeClasses] = {0, 0, 0, 0};
+    void* pinned = nullptr;  // small pinned staging for flags/counters
+};
+
+struct dsy_store {
+    dsy_ctx* ctx = nullptr;
+    uint64_t n = 0, n_live = 0, blob_len = 0, min_len = 0;
+    const uint8_t* d_blob = nullptr;
+    const uint64_t* d_offsets = nullptr;
+    const uint64_t* d_live_gt = nullptr;
+    const uint64_t* d_live_row = nullptr;
+    std::vector<void*> owned;
+    std::unordered_map<uint32_t, std::pair<uint64_t, uint64_t>> segs;
+};
+
+namespace {
+
+// grow-only named workspace buffer
+int ws_get(dsy_ctx* c, const char* name, size_t bytes, void** out) {
+    DevBuf& b = c->ws[name];
+    if (b.bytes < bytes) {
+        if (b.ptr) hipFree(b.ptr);
+        b.ptr = nullptr;
+        b.bytes = 0;
+        size_t want = std::max<size_t>(bytes + bytes / 4, 256);
+        if (hipMalloc(&b.ptr, want) != hipSuccess) {
+            b.ptr = nullptr;
+            return fail(DSY_ENOMEM, "hipMalloc(%zu) for workspace '%s' failed", want, name);
+        }
+        b.bytes = want;
+    }
+    *out = b.ptr;
+    return DSY_OK;
+}
+
+hipEvent_t take_event(dsy_ctx* c) {
+    if (!c->event_pool.empty()) {
+        hipEvent_t e = c->event_pool.back();
+        c->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    hipEventCreate(&e);
+    return e;
+}
+
+void timer_begin(dsy_ctx* c, PendingTimer* t, int cls) {
+    t->cls = cls;
+    t->a = t->b = nullptr;
+    if (!c->timing) return;
+    t->a = take_event(c);
+    t->b = take_event(c);
+    hipEventRecord(t->a, c->stream);
+}
+
+void timer_end(dsy_ctx* c, PendingTimer* t) {
+    if (!t->a) return;
+    hipEventRecord(t->b, c->stream);
+    c->pending.push_back(*t);
+}
+
+// fold completed timers (call after a stream synchronisation)
+void timers_collect(dsy_ctx* c) {
+    for (auto& t : c->pending) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) {
+            c->time_ms[t.cls] += ms;
+            c->launches[t.cls] += 1;
+        }
+        c->event_pool.push_back(t.a);
+        c->event_pool.push_back(t.b);
+    }
+    c->pending.clear();
+}
+
+int check_family(uint64_t m, uint32_t k, int32_t* kind, uint32_t* chunk) {
+    // bloomfilter.py:125-156
+    if (m == 0 || m % 8 != 0) return fail(DSY_EINVAL, "size must be a positive multiple of eight (%llu)", (unsigned long long)m);
+    if (k == 0 || k > m) return fail(DSY_EINVAL, "0 < k <= m violated (k=%u, m=%llu)", k, (unsigned long long)m);
+    uint32_t c = m >= (1ull << 31) ? 8 : (m >= (1ull << 15) ? 4 : 2);
+    uint64_t bits = (uint64_t)c * k * 8;
+    if (bits > 512) return fail(DSY_EINVAL, "Combining multiple hashfunctions is not implemented, cannot create a hash for %llu bits", (unsigned long long)bits);
+    int32_t kd = bits > 384 ? DSY_SHA512 : bits > 256 ? DSY_SHA384 : bits > 160 ? DSY_SHA256 : bits > 128 ? DSY_SHA1 : DSY_MD5;
+    *kind = kd;
+    *chunk = c;
+    return DSY_OK;
+}
+
+int check_params(const dsy_bloom_params* p) {
+    if (!p) return fail(DSY_EINVAL, "params is NULL");
+    int32_t kind;
+    uint32_t chunk;
+    int rc = check_family(p->m_bits, p->k, &kind, &chunk);
+    if (rc) return rc;
+    if (kind != p->hash_kind || chunk != p->chunk_bytes)
+        return fail(DSY_EINVAL, "hash_kind/chunk (%d/%u) disagree with bloomfilter.py for m=%llu k=%u (%d/%u)", p->hash_kind,
+                    p->chunk_bytes, (unsigned long long)p->m_bits, p->k, kind, chunk);
+    if (p->prefix_len > 255) return fail(DSY_EINVAL, "prefix too long (%u)", p->prefix_len);
+    return DSY_OK;
+}
+
+uint64_t filter_words(uint64_t m) { return (m + 31) / 32; }
+
+int upload_params(dsy_ctx* c, const dsy_bloom_params* p, DevParams** out) {
+    DevParams hp{};
+    hp.m_bits = p->m_bits;
+    hp.k = p->k;
+    hp.prefix_len = p->prefix_len;
+    std::memcpy(hp.prefix, p->prefix, p->prefix_len);
+    void* d;
+    int rc = ws_get(c, "params", sizeof(DevParams), &d);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(d, &hp, sizeof hp, hipMemcpyHostToDevice, c->stream));
+    *out = (DevParams*)d;
+    return DSY_OK;
+}
+
+int check_offsets(const uint64_t* offsets, uint64_t n, uint64_t blob_len) {
+    if (!offsets) return fail(DSY_EINVAL, "offsets is NULL");
+    for (uint64_t i = 0; i < n; ++i) {
+        if (offsets[i + 1] < offsets[i]) return fail(DSY_EINVAL, "offsets not monotone at %llu", (unsigned long long)i);
+        if (offsets[i + 1] - offsets[i] > 0xffffffffull) return fail(DSY_EINVAL, "key %llu longer than 4 GiB", (unsigned long long)i);
+    }
+    if (offsets[n] > blob_len) return fail(DSY_EINVAL, "offsets[n]=%llu beyond blob_len=%llu", (unsigned long long)offsets[n], (unsigned long long)blob_len);
+    return DSY_OK;
+}
+
+// stage a packed key set (blob + offsets) into the workspace, with the read guard after the blob
+int stage_keys(dsy_ctx* c, const uint8_t* blob, uint64_t blob_len, const uint64_t* offsets, uint64_t n,
+               uint8_t** d_blob, uint64_t** d_off) {
+    int rc = check_offsets(offsets, n, blob_len);
+    if (rc) return rc;
+    void *b, *o;
+    if ((rc = ws_get(c, "keys_blob", blob_len + DSY_BLOB_GUARD, &b))) return rc;
+    if ((rc = ws_get(c, "keys_off", (n + 1) * 8, &o))) return rc;
+    if (blob_len) HIP_TRY(hipMemcpyAsync(b, blob, blob_len, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync((uint8_t*)b + blob_len, 0, DSY_BLOB_GUARD, c->stream));
+    HIP_TRY(hipMemcpyAsync(o, offsets, (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    *d_blob = (uint8_t*)b;
+    *d_off = (uint64_t*)o;
+    return DSY_OK;
+}
+
+int run_bloom(dsy_ctx* c, BloomOp op, const dsy_bloom_params* p, const uint8_t* d_blob, const uint64_t* d_off,
+              const uint64_t* d_rows, uint64_t n, uint32_t* d_filter, uint8_t* d_present, uint64_t* d_idx) {
+    DevParams* dp;
+    int rc = upload_params(c, p, &dp);
+    if (rc) return rc;
+    if (n == 0) return DSY_OK;
+    BloomLaunch L{};
+    L.op = op;
+    L.kind = p->hash_kind;
+    L.chunk = p->chunk_bytes;
+    L.prm = dp;
+    L.blob = d_blob;
+    L.offsets = d_off;
+    L.rows = d_rows;
+    L.n = n;
+    L.filter = d_filter;
+    L.nwords = (uint32_t)filter_words(p->m_bits);
+    L.use_lds = (uint64_t)L.nwords * 4 <= 64 * 1024;
+    L.present = d_present;
+    L.indices = d_idx;
+    L.max_grid = c->max_grid;
+    L.stream = c->stream;
+    PendingTimer t;
+    timer_begin(c, &t, kTimeBuild);
+    HIP_TRY(launch_bloom(L));
+    timer_end(c, &t);
+    return DSY_OK;
+}
+
+struct Guard {
+    dsy_ctx* c;
+    explicit Guard(dsy_ctx* c) : c(c) { c->mu.lock(); hipSetDevice(c->device); }
+    ~Guard() { c->mu.unlock(); }
+};
+
+}  // namespace
+
+extern "C" {
+
+int dsy_abi_version(void) { return DSY_ABI_VERSION; }
+const char* dsy_last_error(void) { return g_err.c_str(); }
+uint64_t dsy_filter_words(uint64_t m_bits) { return filter_words(m_bits); }
+
+int dsy_hash_family(uint64_t m_bits, uint32_t k, int32_t* out_kind, uint32_t* out_chunk) {
+    int32_t kind;
+    uint32_t chunk;
+    int rc = check_family(m_bits, k, &kind, &chunk);
+    if (rc) return rc;
+    if (out_kind) *out_kind = kind;
+    if (out_chunk) *out_chunk = chunk;
+    return DSY_OK;
+}
+
+int dsy_ctx_create(int device, dsy_ctx** out) {
+    if (!out) return fail(DSY_EINVAL, "out is NULL");
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(DSY_EINVAL, "device %d out of range (%d devices)", device, ndev);
+    HIP_TRY(hipSetDevice(device));
+    dsy_ctx* c = new dsy_ctx();
+    c->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return fail(DSY_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
+    }
+    int cus = 256;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    c->max_grid = (uint32_t)std::max(cus, 1) * 8;
+    hipHostMalloc(&c->pinned, 4096, hipHostMallocDefault);
+    *out = c;
+    return DSY_OK;
+}
+
+int dsy_ctx_destroy(dsy_ctx* c) {
+    if (!c) return DSY_OK;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        hipSetDevice(c->device);
+        hipStreamSynchronize(c->stream);
+        timers_collect(c);
+        for (auto& kv : c->ws) if (kv.second.ptr) hipFree(kv.second.ptr);
+        for (auto e : c->event_pool) hipEventDestroy(e);
+        if (c->pinned) hipHostFree(c->pinned);
+        hipStreamDestroy(c->stream);
+    }
+    delete c;
+    return DSY_OK;
+}
+
+int dsy_ctx_synchronize(dsy_ctx* c) {
+    if (!c) return fail(DSY_EINVAL, "ctx is NULL");
+    Guard g(c);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    timers_collect(c);
+    return DSY_OK;
+}
+
+void* dsy_ctx_stream(dsy_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int dsy_ctx_set_timing(dsy_ctx* c, int enable) {
+    if (!c) return fail(DSY_EINVAL, "ctx is NULL");
+    Guard g(c);
+    c->timing = enable != 0;
+    return DSY_OK;
+}
+
+int dsy_ctx_kernel_time(dsy_ctx* c, int which, double* out_ms, uint64_t* out_launches, uint64_t* out_blocks,
+                        uint64_t* out_bytes) {
+    if (!c || which < 0 || which >= kTimeClasses) return fail(DSY_EINVAL, "bad ctx or timer class");
+    Guard g(c);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    timers_collect(c);
+    if (out_ms) *out_ms = c->time_ms[which];
+    if (out_launches) *out_launches = c->launches[which];
+    if (out_blocks) *out_blocks = c->blocks[which];
+    if (out_bytes) *out_bytes = c->bytes[which];
+    return DSY_OK;
+}
+
+int dsy_ctx_reset_timing(dsy_ctx* c) {
+    if (!c) return fail(DSY_EINVAL, "ctx is NULL");
+    Guard g(c);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    timers_collect(c);
+    for (int i = 0; i < kTimeClasses; ++i) c->time_ms[i] = 0, c->launches[i] = 0, c->blocks[i] = 0, c->bytes[i] = 0;
+    return DSY_OK;
+}
+
+// ------------------------------------------------------------------------------------------ bloom ops
+int dsy_bloom_add(dsy_ctx* c, const dsy_bloom_params* p, const uint8_t* blob, uint64_t blob_len,
+                  const uint64_t* offsets, uint64_t n, uint8_t* filter_inout) {
+    if (!c || !filter_inout) return fail(DSY_EINVAL, "NULL ctx or filter");
+    int rc = check_params(p);
+    if (rc) return rc;
+    Guard g(c);
+    uint8_t* db;
+    uint64_t* dof;
+    if ((rc = stage_keys(c, blob, blob_len, offsets, n, &db, &dof))) return rc;
+    const uint64_t nbytes = p->m_bits / 8, words = filter_words(p->m_bits);
+    void* df;
+    if ((rc = ws_get(c, "filter", words * 4, &df))) return rc;
+    HIP_TRY(hipMemsetAsync(df, 0, words * 4, c->stream));
+    HIP_TRY(hipMemcpyAsync(df, filter_inout, nbytes, hipMemcpyHostToDevice, c->stream));
+    if ((rc = run_bloom(c, BloomOp::Add, p, db, dof, nullptr, n, (uint32_t*)df, nullptr, nullptr))) return rc;
+    HIP_TRY(hipMemcpyAsync(filter_inout, df, nbytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    timers_collect(c);
+    return DSY_OK;
+}
+
+int dsy_bloom_test(dsy_ctx* c, const dsy_bloom_params* p, const uint8_t* blob, uint64_t blob_len,
+                   const uint64_t* offsets, uint64_t n, const uint8_t* filter, uint8_t* out_present) {
+    if (!c || !filter || (!out_present && n)) return fail(DSY_EINVAL, "NULL ctx, filter or output");
+    int rc = check_params(p);
+    if (rc) return rc;
+    Guard g(c);
+    uint8_t* db;
+    uint64_t* dof;
+    if ((rc = stage_keys(c, blob, blob_len, offsets, n, &db, &dof))) return rc;
+    const uint64_t nbytes = p->m_bits / 8, words = filter_words(p->m_bits);
+    void *df, *dp;
+    if ((rc = ws_get(c, "filter", words * 4, &df))) return rc;
+    if ((rc = ws_get(c, "present", n + 1, &dp))) return rc;
+    HIP_TRY(hipMemsetAsync(df, 0, words * 4, c->stream));
+    HIP_TRY(hipMemcpyAsync(df, filter, nbytes, hipMemcpyHostToDevice, c->stream));
+    if ((rc = run_bloom(c, BloomOp::Test, p, db, dof, nullptr, n, (uint32_t*)df, (uint8_t*)dp, nullptr))) return rc;
+    if (n) HIP_TRY(hipMemcpyAsync(out_present, dp, n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    timers_collect(c);
+    return DSY_OK;
+}
+
+int dsy_bloom_indices(dsy_ctx* c, const dsy_bloom_params* p, const uint8_t* blob, uint64_t blob_len,
+                      const uint64_t* offsets, uint64_t n, uint64_t* out_idx) {
+    if (!c || (!out_idx && n)) return fail(DSY_EINVAL, "NULL ctx or output");
+    int rc = check_params(p);
+    if (rc) return rc;
+    Guard g(c);
+    uint8_t* db;
+    uint64_t* dof;
+    if ((rc = stage_keys(c, blob, blob_len, offsets, n, &db, &dof))) return rc;
+    void* di;
+    if ((rc = ws_get(c, "indices", (n * p->k + 1) * 8, &di))) return rc;
+    if ((rc = run_bloom(c, BloomOp::Indices, p, db, dof, nullptr, n, nullptr, nullptr, (uint64_t*)di))) return rc;
+    if (n) HIP_TRY(hipMemcpyAsync(out_idx, di, n * p->k * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    timers_collect(c);
+    return DSY_OK;
+}
+
+int dsy_bloom_add_dev(dsy_ctx* c, const dsy_bloom_params* p, const uint8_t* d_blob, const uint64_t* d_offsets,
+                      uint64_t n, uint32_t* d_filter) {
+    if (!c || !d_filter) return fail(DSY_EINVAL, "NULL ctx or filter");
+    int rc = check_params(p);
+    if (rc) return rc;
+    Guard g(c);
+    return run_bloom(c, BloomOp::Add, p, d_blob, d_offsets, nullptr, n, d_filter, nullptr, nullptr);
+}
+
+int dsy_bloom_test_dev(dsy_ctx* c, const dsy_bloom_params* p, const uint8_t* d_blob, const uint64_t* d_offsets,
+                       uint64_t n, const uint32_t* d_filter, uint8_t* d_present) {
+    if (!c || !d_filter) return fail(DSY_EINVAL, "NULL ctx or filter");
+    int rc = check_params(p);
+    if (rc) return rc;
+    Guard g(c);
+    return run_bloom(c, BloomOp::Test, p, d_blob, d_offsets, nullptr, n, (uint32_t*)d_filter, d_present, nullptr);
+}
+
+// ------------------------------------------------------------------------------------------------ store
+static int store_index(dsy_store* s, const uint64_t* offsets, const uint64_t* gt, const uint32_t* meta,
+                       const uint8_t* undone, std::vector<uint64_t>* live_gt, std::vector<uint64_t>* live_row,
+                       bool* identity) {
+    // Build the live index (undone == 0) and the per-meta segments; check the (meta, global_time) order the
+    // export promises (the sync_meta_message_undone_global_time_index order, dispersydatabase.py:63).
+    const uint64_t n = s->n;
+    *identity = true;
+    uint64_t minlen = ~0ull;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (i && (meta[i] < meta[i - 1] || (meta[i] == meta[i - 1] && gt[i] < gt[i - 1])))
+            return fail(DSY_EUNSORTED, "store rows not sorted by (meta, global_time) at row %llu", (unsigned long long)i);
+        minlen = std::min(minlen, offsets[i + 1] - offsets[i]);
+        if (undone && undone[i]) *identity = false;
+    }
+    s->min_len = n ? minlen : 0;
+    if (!*identity) {
+        live_gt->reserve(n);
+        live_row->reserve(n);
+    }
+    uint64_t li = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (undone && undone[i]) continue;
+        auto it = s->segs.find(meta[i]);
+        if (it == s->segs.end()) s->segs[meta[i]] = {li, li + 1};
+        else it->second.second = li + 1;
+        if (!*identity) {
+            live_gt->push_back(gt[i]);
+            live_row->push_back(i);
+        }
+        ++li;
+    }
+    s->n_live = li;
+    return DSY_OK;
+}
+
+static int store_finish(dsy_ctx* c, dsy_store* s, const uint64_t* h_gt_or_null, const uint64_t* d_gt,
+                        std::vector<uint64_t>& live_gt, std::vector<uint64_t>& live_row, bool identity) {
+    if (identity) {
+        if (d_gt) {
+            s->d_live_gt = d_gt;
+        } else {
+            void* p;
+            if (hipMalloc(&p, std::max<uint64_t>(s->n, 1) * 8) != hipSuccess) return fail(DSY_ENOMEM, "store gt alloc");
+            s->owned.push_back(p);
+            if (s->n) HIP_TRY(hipMemcpyAsync(p, h_gt_or_null, s->n * 8, hipMemcpyHostToDevice, c->stream));
+            s->d_live_gt = (uint64_t*)p;
+        }
+        s->d_live_row = nullptr;
+    } else {
+        void *pg, *pr;
+        if (hipMalloc(&pg, std::max<uint64_t>(s->n_live, 1) * 8) != hipSuccess) return fail(DSY_ENOMEM, "store live alloc");
+        s->owned.push_back(pg);
+        if (hipMalloc(&pr, std::max<uint64_t>(s->n_live, 1) * 8) != hipSuccess) return fail(DSY_ENOMEM, "store live alloc");
+        s->owned.push_back(pr);
+        if (s->n_live) {
+            HIP_TRY(hipMemcpyAsync(pg, live_gt.data(), s->n_live * 8, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(hipMemcpyAsync(pr, live_row.data(), s->n_live * 8, hipMemcpyHostToDevice, c->stream));
+        }
+        s->d_live_gt = (uint64_t*)pg;
+        s->d_live_row = (uint64_t*)pr;
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return DSY_OK;
+}
+
+int dsy_store_upload(dsy_ctx* c, const uint8_t* blob, uint64_t blob_len, const uint64_t* offsets, uint64_t n,
+                     const uint64_t* global_time, const uint32_t* meta, const uint8_t* undone, dsy_store** out) {
+    if (!c || !out || !offsets || (n && (!global_time || !meta))) return fail(DSY_EINVAL, "NULL argument");
+    int rc = check_offsets(offsets, n, blob_len);
+    if (rc) return rc;
+    Guard g(c);
+    dsy_store* s = new dsy_store();
+    s->ctx = c;
+    s->n = n;
+    s->blob_len = blob_len;
+    std::vector<uint64_t> lg, lr;
+    bool identity;
+    if ((rc = store_index(s, offsets, global_time, meta, undone, &lg, &lr, &identity))) { delete s; return rc; }
+    void *pb, *po;
+    if (hipMalloc(&pb, blob_len + DSY_BLOB_GUARD) != hipSuccess) { delete s; return fail(DSY_ENOMEM, "store blob alloc (%llu B)", (unsigned long long)blob_len); }
+    s->owned.push_back(pb);
+    if (hipMalloc(&po, (n + 1) * 8) != hipSuccess) { dsy_store_free(s); return fail(DSY_ENOMEM, "store offsets alloc"); }
+    s->owned.push_back(po);
+    if (blob_len) HIP_TRY(hipMemcpyAsync(pb, blob, blob_len, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync((uint8_t*)pb + blob_len, 0, DSY_BLOB_GUARD, c->stream));
+    HIP_TRY(hipMemcpyAsync(po, offsets, (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    s->d_blob = (uint8_t*)pb;
+    s->d_offsets = (uint64_t*)po;
+    if ((rc = store_finish(c, s, global_time, nullptr, lg, lr, identity))) { dsy_store_free(s); return rc; }
+    *out = s;
+    return DSY_OK;
+}
+
+int dsy_store_attach(dsy_ctx* c, const uint8_t* d_blob, uint64_t blob_len, const uint64_t* d_offsets, uint64_t n,
+                     const uint64_t* d_global_time, const uint32_t* d_meta, const uint8_t* d_undone, dsy_store** out) {
+    if (!c || !out || !d_offsets || (n && (!d_global_time || !d_meta || !d_blob))) return fail(DSY_EINVAL, "NULL argument");
+    Guard g(c);
+    std::vector<uint64_t> off(n + 1), gt(n);
+    std::vector<uint32_t> meta(n);
+    std::vector<uint8_t> und;
+    HIP_TRY(hipMemcpy(off.data(), d_offsets, (n + 1) * 8, hipMemcpyDeviceToHost));
+    if (n) {
+        HIP_TRY(hipMemcpy(gt.data(), d_global_time, n * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(meta.data(), d_meta, n * 4, hipMemcpyDeviceToHost));
+        if (d_undone) {
+            und.resize(n);
+            HIP_TRY(hipMemcpy(und.data(), d_undone, n, hipMemcpyDeviceToHost));
+        }
+    }
+    int rc = check_offsets(off.data(), n, blob_len);
+    if (rc) return rc;
+    dsy_store* s = new dsy_store();
+    s->ctx = c;
+    s->n = n;
+    s->blob_len = blob_len;
+    s->d_blob = d_blob;
+    s->d_offsets = d_offsets;
+    std::vector<uint64_t> lg, lr;
+    bool identity;
+    if ((rc = store_index(s, off.data(), gt.data(), meta.data(), d_undone ? und.data() : nullptr, &lg, &lr, &identity))) {
+        delete s;
+        return rc;
+    }
+    if ((rc = store_finish(c, s, nullptr, d_global_time, lg, lr, identity))) { dsy_store_free(s); return rc; }
+    *out = s;
+    return DSY_OK;
+}
+
+int dsy_store_free(dsy_store* s) {
+    if (!s) return DSY_OK;
+    if (s->ctx) {
+        std::lock_guard<std::mutex> lk(s->ctx->mu);
+        hipSetDevice(s->ctx->device);
+        hipStreamSynchronize(s->ctx->stream);
+        for (void* p : s->owned) hipFree(p);
+    }
+    delete s;
+    return DSY_OK;
+}
+
+uint64_t dsy_store_rows(const dsy_store* s) { return s ? s->n : 0; }
+
+int dsy_bloom_add_rows(dsy_ctx* c, const dsy_bloom_params* p, const dsy_store* s, const uint64_t* rows, uint64_t n,
+                       uint8_t* filter_inout) {
+    if (!c || !s || !filter_inout || (n && !rows)) return fail(DSY_EINVAL, "NULL argument");
+    int rc = check_params(p);
+    if (rc) return rc;
+    for (uint64_t i = 0; i < n; ++i)
+        if (rows[i] >= s->n) return fail(DSY_EINVAL, "row %llu out of range (%llu rows)", (unsigned long long)rows[i], (unsigned long long)s->n);
+    Guard g(c);
+    const uint64_t nbytes = p->m_bits / 8, words = filter_words(p->m_bits);
+    void *df, *dr;
+    if ((rc = ws_get(c, "filter", words * 4, &df))) return rc;
+    if ((rc = ws_get(c, "rows", (n + 1) * 8, &dr))) return rc;
+    HIP_TRY(hipMemsetAsync(df, 0, words * 4, c->stream));
+    HIP_TRY(hipMemcpyAsync(df, filter_inout, nbytes, hipMemcpyHostToDevice, c->stream));
+    if (n) HIP_TRY(hipMemcpyAsync(dr, rows, n * 8, hipMemcpyHostToDevice, c->stream));
+    if ((rc = run_bloom(c, BloomOp::Add, p, s->d_blob, s->d_offsets, (uint64_t*)dr, n, (uint32_t*)df, nullptr, nullptr)))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(filter_inout, df, nbytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    timers_collect(c);
+    return DSY_OK;
+}
+
+// -------------------------------------------------------------------------------------------- responder
+static const uint64_t kWindow = 4096;
+
+static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, uint32_t R, const uint8_t* d_filters,
+                        uint64_t filters_len, const dsy_meta* metas, uint32_t J, uint64_t responder_gt,
+                        int include_inactive, int64_t byte_limit, uint64_t seed, uint64_t** d_packed,
+                        uint64_t** d_packed_off, uint64_t* total_pairs) {
+    // ---- validate claims (payload.py:89-101, conversion.py:772-789) and their filters
+    std::map<std::pair<int, uint32_t>, std::vector<uint32_t>> families;
+    for (uint32_t r = 0; r < R; ++r) {
+        const dsy_request& q = reqs[r];
+        if (q.modulo == 0 || q.offset >= q.modulo)
+            return fail(DSY_EINVAL, "claim %u: need 0 <= offset < modulo (offset=%u modulo=%u)", r, q.offset, q.modulo);
+        int32_t kind;
+        uint32_t chunk;
+        int rc = check_family(q.m_bits, q.k, &kind, &chunk);
+        if (rc) return rc;
+        if (kind != q.hash_kind || chunk != q.chunk_bytes) return fail(DSY_EINVAL, "claim %u: hash family mismatch", r);
+        if (q.prefix_len > 255) return fail(DSY_EINVAL, "claim %u: prefix too long", r);
+        if (q.filter_offset % 4) return fail(DSY_EINVAL, "claim %u: filter_offset must be a multiple of 4", r);
+        if (filters_len && q.filter_offset + filter_words(q.m_bits) * 4 > filters_len)
+            return fail(DSY_EINVAL, "claim %u: filter beyond the filters buffer", r);
+        families[{kind, chunk}].push_back(r);
+    }
+    std::vector<SegMeta> sm(J);
+    for (uint32_t j = 0; j < J; ++j) {
+        if (metas[j].direction < DSY_ASC || metas[j].direction > DSY_RANDOM)
+            return fail(DSY_EINVAL, "meta %u: unknown synchronization direction %d", j, metas[j].direction);
+        auto it = s->segs.find(metas[j].meta_id);
+        sm[j].seg_a = it == s->segs.end() ? 0 : it->second.first;
+        sm[j].seg_b = it == s->segs.end() ? 0 : it->second.second;
+        sm[j].dir = (uint32_t)metas[j].direction;
+        sm[j].has_pruning = metas[j].has_pruning;
+        sm[j].inactive = metas[j].inactive_threshold;
+    }
+    const uint64_t W = kWindow;
+    int rc;
+    void *d_reqs, *d_metas, *d_plans, *d_state, *d_upper, *d_pairs, *d_miss, *d_flags, *d_total, *d_lists;
+    if ((rc = ws_get(c, "reqs", std::max<size_t>(R, 1) * sizeof(dsy_request), &d_reqs))) return rc;
+    if ((rc = ws_get(c, "metas", std::max<size_t>(J, 1) * sizeof(SegMeta), &d_metas))) return rc;
+    if ((rc = ws_get(c, "plans", std::max<size_t>((size_t)R * J, 1) * sizeof(Plan), &d_plans))) return rc;
+    if ((rc = ws_get(c, "state", std::max<size_t>(R, 1) * sizeof(ReqState), &d_state))) return rc;
+    if ((rc = ws_get(c, "upper", std::max<size_t>(R, 1) * 8, &d_upper))) return rc;
+    if ((rc = ws_get(c, "pairs", std::max<size_t>((size_t)R * W, 1) * 8, &d_pairs))) return rc;
+    if ((rc = ws_get(c, "miss", std::max<size_t>((size_t)R * W, 1), &d_miss))) return rc;
+    if ((rc = ws_get(c, "flags", 64, &d_flags))) return rc;
+    if ((rc = ws_get(c, "total", 64, &d_total))) return rc;
+    if ((rc = ws_get(c, "lists", std::max<size_t>(R, 1) * 4, &d_lists))) return rc;
+
+    if (R) HIP_TRY(hipMemcpyAsync(d_reqs, reqs, (size_t)R * sizeof(dsy_request), hipMemcpyHostToDevice, c->stream));
+    if (J) HIP_TRY(hipMemcpyAsync(d_metas, sm.data(), (size_t)J * sizeof(SegMeta), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(d_upper, 0, std::max<size_t>(R, 1) * 8, c->stream));
+    HIP_TRY(hipMemsetAsync(d_total, 0, 64, c->stream));
+    std::vector<uint32_t> lists;
+    std::vector<std::pair<std::pair<int, uint32_t>, std::pair<size_t, size_t>>> fam_ranges;
+    for (auto& kv : families) {
+        fam_ranges.push_back({kv.first, {lists.size(), kv.second.size()}});
+        lists.insert(lists.end(), kv.second.begin(), kv.second.end());
+    }
+    if (!lists.empty())
+        HIP_TRY(hipMemcpyAsync(d_lists, lists.data(), lists.size() * 4, hipMemcpyHostToDevice, c->stream));
+
+    RespondLaunch L{};
+    L.st.blob = s->d_blob;
+    L.st.offsets = s->d_offsets;
+    L.st.live_gt = s->d_live_gt;
+    L.st.live_row = s->d_live_row;
+    L.st.n_live = s->n_live;
+    L.reqs = (const dsy_request*)d_reqs;
+    L.metas = (const SegMeta*)d_metas;
+    L.R = R;
+    L.J = J;
+    L.filters = d_filters;
+    L.responder_gt = responder_gt;
+    L.include_inactive = include_inactive;
+    L.byte_limit = byte_limit;
+    L.seed = seed;
+    L.window = W;
+    L.plans = (Plan*)d_plans;
+    L.state = (ReqState*)d_state;
+    L.upper = (uint64_t*)d_upper;
+    L.pair_row = (uint64_t*)d_pairs;
+    L.miss = (uint8_t*)d_miss;
+    L.flags = (uint32_t*)d_flags;
+    L.total_pairs = (uint64_t*)d_total;
+    L.total_blocks = (uint64_t*)d_total + 1;
+    L.stream = c->stream;
+
+    PendingTimer t;
+    timer_begin(c, &t, kTimeSelect);
+    HIP_TRY(launch_plan(L));
+    timer_end(c, &t);
+    // ---- per-claim output capacity: every emitted packet but the last costs >= min_len bytes of budget
+    std::vector<uint64_t> upper(R);
+    if (R) HIP_TRY(hipMemcpyAsync(upper.data(), d_upper, (size_t)R * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    std::vector<ReqState> st(R);
+    uint64_t cap_total = 0;
+    for (uint32_t r = 0; r < R; ++r) {
+        uint64_t cap = upper[r];
+        if (byte_limit <= 0) cap = std::min<uint64_t>(cap, 1);
+        else if (s->min_len > 0) cap = std::min<uint64_t>(cap, (uint64_t)byte_limit / s->min_len + 2);
+        st[r] = ReqState{};
+        st[r].cap = cap;
+        st[r].out_base = cap_total;
+        st[r].done = upper[r] == 0;
+        cap_total += cap;
+    }
+    void* d_out;
+    if ((rc = ws_get(c, "out", std::max<uint64_t>(cap_total, 1) * 8, &d_out))) return rc;
+    L.out = (uint64_t*)d_out;
+    if (R) HIP_TRY(hipMemcpyAsync(d_state, st.data(), (size_t)R * sizeof(ReqState), hipMemcpyHostToDevice, c->stream));
+
+    uint32_t* h_flags = (uint32_t*)c->pinned;
+    for (int window = 0;; ++window) {
+        HIP_TRY(hipMemsetAsync(d_flags, 0, 64, c->stream));
+        timer_begin(c, &t, kTimeSelect);
+        HIP_TRY(launch_fill(L));
+        timer_end(c, &t);
+        for (auto& fr : fam_ranges) {
+            timer_begin(c, &t, kTimePairTest);
+            HIP_TRY(launch_pair_test_list(L, fr.first.first, fr.first.second, (const uint32_t*)d_lists + fr.second.first,
+                                          (uint32_t)fr.second.second));
+            timer_end(c, &t);
+        }
+        timer_begin(c, &t, kTimeCompact);
+        HIP_TRY(launch_compact(L));
+        timer_end(c, &t);
+        HIP_TRY(hipMemcpyAsync(h_flags, d_flags, 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (!h_flags[0]) break;
+    }
+    void *d_packed_v, *d_packed_off_v;
+    if ((rc = ws_get(c, "packed", std::max<uint64_t>(cap_total, 1) * 8, &d_packed_v))) return rc;
+    if ((rc = ws_get(c, "packed_off", ((size_t)R + 1) * 8, &d_packed_off_v))) return rc;
+    HIP_TRY(launch_pack(L, (uint64_t*)d_packed_v, (uint64_t*)d_packed_off_v, nullptr));
+    uint64_t* h_tot = (uint64_t*)c->pinned + 8;
+    HIP_TRY(hipMemcpyAsync(h_tot, d_total, 24, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    // capacity overflow can only come from a wrong min_len bound; report it loudly
+    std::vector<ReqState> fin(R);
+    if (R) {
+        HIP_TRY(hipMemcpy(fin.data(), d_state, (size_t)R * sizeof(ReqState), hipMemcpyDeviceToHost));
+        for (uint32_t r = 0; r < R; ++r)
+            if (fin[r].overflow) return fail(DSY_ECAPACITY, "internal: claim %u overflowed its output capacity", r);
+    }
+    timers_collect(c);
+    c->blocks[kTimePairTest] += h_tot[1];
+    c->bytes[kTimePairTest] += h_tot[2];
+    *total_pairs = h_tot[0];
+    *d_packed = (uint64_t*)d_packed_v;
+    *d_packed_off = (uint64_t*)d_packed_off_v;
+    return DSY_OK;
+}
+
+int dsy_sync_respond(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, uint32_t R, const uint8_t* filters,
+                     uint64_t filters_len, const dsy_meta* metas, uint32_t nmeta, uint64_t responder_global_time,
+                     int include_inactive, int64_t byte_limit, uint64_t random_seed, uint64_t* out_idx,
+                     uint64_t out_cap, uint64_t* out_req_offsets) {
+    if (!c || !s || (R && (!reqs || !filters)) || (nmeta && !metas) || !out_req_offsets)
+        return fail(DSY_EINVAL, "NULL argument");
+    Guard g(c);
+    void* d_f;
+    int rc;
+    if ((rc = ws_get(c, "filters", filters_len + 64, &d_f))) return rc;
+    if (filters_len) HIP_TRY(hipMemcpyAsync(d_f, filters, filters_len, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync((uint8_t*)d_f + filters_len, 0, 64, c->stream));
+    uint64_t *d_packed, *d_off, pairs;
+    if ((rc = respond_core(c, s, reqs, R, (const uint8_t*)d_f, filters_len + 64, metas, nmeta, responder_global_time,
+                           include_inactive, byte_limit, random_seed, &d_packed, &d_off, &pairs)))
+        return rc;
+    HIP_TRY(hipMemcpy(out_req_offsets, d_off, ((size_t)R + 1) * 8, hipMemcpyDeviceToHost));
+    const uint64_t total = out_req_offsets[R];
+    if (total > out_cap) return fail(DSY_ECAPACITY, "out_cap %llu < %llu rows", (unsigned long long)out_cap, (unsigned long long)total);
+    if (total) HIP_TRY(hipMemcpy(out_idx, d_packed, total * 8, hipMemcpyDeviceToHost));
+    return DSY_OK;
+}
+
+int dsy_sync_respond_dev(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, uint32_t R,
+                         const uint8_t* d_filters, const dsy_meta* metas, uint32_t nmeta,
+                         uint64_t responder_global_time, int include_inactive, int64_t byte_limit,
+                         uint64_t random_seed, const uint64_t** d_out_idx, const uint64_t** d_out_offsets,
+                         uint64_t* out_total_pairs) {
+    if (!c || !s || (R && (!reqs || !d_filters)) || (nmeta && !metas)) return fail(DSY_EINVAL, "NULL argument");
+    Guard g(c);
+    uint64_t *d_packed, *d_off, pairs = 0;
+    int rc = respond_core(c, s, reqs, R, d_filters, 0, metas, nmeta, responder_global_time, include_inactive,
+                          byte_limit, random_seed, &d_packed, &d_off, &pairs);
+    if (rc) return rc;
+    if (d_out_idx) *d_out_idx = d_packed;
+    if (d_out_offsets) *d_out_offsets = d_off;
+    if (out_total_pairs) *out_total_pairs = pairs;
+    return DSY_OK;
+}
+
+}  // extern "C"

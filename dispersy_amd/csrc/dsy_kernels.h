@@ -1,0 +1,115 @@
+// dsy_kernels.h -- launch descriptors shared by the C-ABI (dsy_capi.hip) and the kernel translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dsybloom.h"
+#include "dsy_message.h"
+
+namespace dsy {
+
+// Device copy of one filter's hashing parameters (the prefix must live in device memory: lanes index it).
+struct DevParams {
+    uint64_t m_bits;
+    uint32_t k;
+    uint32_t prefix_len;
+    uint8_t prefix[256];
+};
+
+enum class BloomOp { Add, Test, Indices };
+
+struct BloomLaunch {
+    BloomOp op;
+    int kind;
+    uint32_t chunk;
+    const DevParams* prm;
+    const uint8_t* blob;
+    const uint64_t* offsets;
+    const uint64_t* rows;  // optional indirection (add by store row)
+    uint64_t n;
+    uint32_t* filter;
+    uint32_t nwords;
+    int use_lds;
+    uint8_t* present;
+    uint64_t* indices;
+    uint32_t max_grid;
+    hipStream_t stream;
+};
+
+hipError_t launch_bloom(const BloomLaunch& L);
+
+// ------------------------------------------------------------------------------------------ responder
+// Store view the responder kernels read.  `live` rows are the rows with undone == 0, in index order.
+struct StoreView {
+    const uint8_t* blob;
+    const uint64_t* offsets;  // [n_rows + 1] over ALL rows
+    const uint64_t* live_gt;  // [n_live] global_time of live row i
+    const uint64_t* live_row; // [n_live] store row of live row i (nullptr: identity)
+    uint64_t n_live;
+};
+
+// Per (claim, meta) selection plan.
+struct Plan {
+    uint64_t a, b;     // live-row span [a, b) with lo' <= gt <= hi, inside the meta's segment
+    uint64_t g0;       // first candidate global_time (enumerate mode)
+    uint64_t ncand;    // size of the candidate space
+    uint32_t mode;     // 0: scan live rows a..b   1: enumerate global times g0 + i*modulo
+    uint32_t dir;      // DSY_ASC / DSY_DESC / DSY_RANDOM
+    uint64_t perm_key; // RANDOM: permutation key
+    uint32_t perm_bits;// RANDOM: Feistel half-width
+    uint32_t _pad;
+};
+
+// Per-claim window state.
+struct ReqState {
+    uint32_t meta;     // current meta index
+    uint32_t done;     // 1 once the byte limit is reached or every candidate was visited
+    uint64_t cand;     // next candidate (iteration order) within the current meta
+    uint64_t sub;      // rows of that candidate already emitted
+    uint64_t n_window; // pairs placed in the current window
+    uint64_t emitted;  // packets sent so far
+    int64_t spent;     // bytes sent so far
+    uint64_t cap;      // output capacity of this claim
+    uint64_t out_base; // where this claim's output starts
+    uint32_t exhausted;// every candidate of every meta visited
+    uint32_t overflow; // output capacity exceeded (host retries with a larger capacity)
+};
+
+struct SegMeta {          // one syncable meta in serving order, resolved against the store
+    uint64_t seg_a, seg_b; // live-row segment of this meta id
+    uint32_t dir;
+    uint32_t has_pruning;
+    uint64_t inactive;
+};
+
+struct RespondLaunch {
+    StoreView st;
+    const dsy_request* reqs;  // device [R]
+    const SegMeta* metas;     // device [J]
+    uint32_t R, J;
+    const uint8_t* filters;   // device
+    uint64_t responder_gt;
+    int include_inactive;
+    int64_t byte_limit;
+    uint64_t seed;
+    uint64_t window;          // W pairs per claim per window
+    Plan* plans;              // device [R*J]
+    ReqState* state;          // device [R]
+    uint64_t* upper;          // device [R]: upper bound of selected rows per claim
+    uint64_t* pair_row;       // device [R*W]
+    uint8_t* miss;            // device [R*W]
+    uint64_t* out;            // device [sum cap]
+    uint32_t* flags;          // device [4]: [0] any claim still active
+    uint64_t* total_pairs;    // device [1]
+    uint64_t* total_blocks;   // device [2]: compression blocks, packet bytes hashed (nullable)
+    hipStream_t stream;
+};
+
+hipError_t launch_plan(const RespondLaunch& L);
+hipError_t launch_fill(const RespondLaunch& L);
+// hash + test the window's pairs of the listed claims, all of one (hash kind, chunk) family
+hipError_t launch_pair_test_list(const RespondLaunch& L, int kind, uint32_t chunk, const uint32_t* d_list, uint32_t n);
+hipError_t launch_compact(const RespondLaunch& L);
+hipError_t launch_pack(const RespondLaunch& L, uint64_t* packed, uint64_t* packed_offsets, uint64_t* d_scan_tmp);
+
+}  // namespace dsy

@@ -1,0 +1,413 @@
+// dsy_sync_kernels.hip -- the batched responder (community.py:2746-2811 + :2555-2567) on gfx950.
+//
+// Work is windowed per claim, mirroring the reference's lazy cursor + lazy not_filter: each window selects at
+// most W (claim, packet) pairs per claim in send order, hashes and tests them, and emits missing packets until
+// the claim's byte budget is spent.  A claim whose budget is spent after its first window never selects more,
+// exactly as the reference stops pulling rows from SQLite.
+//
+//   k_plan        one lane per (claim, meta): binary-search the live-row span of [time_low', time_high] in the
+//                 meta's global_time-sorted segment; choose scan (every row) or enumerate (every global time
+//                 g = g0 + i*modulo, each found by binary search) by which touches fewer bytes.
+//   k_fill        one 256-lane workgroup per claim: the next <= W rows in send order (ASC / DESC / Feistel-
+//                 permuted RANDOM), block prefix-sum placement, resumable (meta, candidate, sub-row) cursor.
+//   k_pair_test   one lane per pair, a wave per 64 pairs of one claim (filter/prefix/m/k wave-uniform): digest
+//                 of prefix || packet, k probes -> missing flag.
+//   k_compact     one wave per claim: ballot + prefix-sum compaction of missing pairs in send order with the
+//                 byte-limit rule of community.py:2559-2567 (the crossing packet is sent).
+//   k_pack        exclusive scan of per-claim counts and a copy into the packed output.
+#include "dsy_kernels.h"
+
+namespace dsy {
+
+static constexpr uint64_t kMaxGt = 0x7fffffffffffffffull;  // 2^63 - 1 (community.py:2547-2548, :2806)
+
+__device__ __forceinline__ uint64_t lower_bound_gt(const uint64_t* gt, uint64_t a, uint64_t b, uint64_t v) {
+    while (a < b) {
+        const uint64_t mid = a + ((b - a) >> 1);
+        if (gt[mid] < v) a = mid + 1; else b = mid;
+    }
+    return a;
+}
+
+__device__ __forceinline__ uint64_t upper_bound_gt(const uint64_t* gt, uint64_t a, uint64_t b, uint64_t v) {
+    while (a < b) {
+        const uint64_t mid = a + ((b - a) >> 1);
+        if (gt[mid] <= v) a = mid + 1; else b = mid;
+    }
+    return a;
+}
+
+__device__ __forceinline__ uint32_t mix32(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+    return (uint32_t)x;
+}
+
+// Bijection of [0, n) by a 4-round Feistel network on 2*bits bits with cycle walking (RANDOM direction).
+__device__ __forceinline__ uint64_t permute(uint64_t x, uint64_t n, uint32_t bits, uint64_t key) {
+    const uint64_t mask = (1ull << bits) - 1;
+    do {
+        uint64_t l = x >> bits, r = x & mask;
+#pragma unroll
+        for (int round = 0; round < 4; ++round) {
+            const uint64_t f = mix32(r ^ (key + 0x9e3779b97f4a7c15ull * (round + 1))) & mask;
+            const uint64_t t = l ^ f;
+            l = r;
+            r = t;
+        }
+        x = (l << bits) | r;
+    } while (x >= n);
+    return x;
+}
+
+__global__ void k_plan(RespondLaunch L) {
+    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= L.R * L.J) return;
+    const uint32_t r = idx / L.J, j = idx % L.J;
+    const dsy_request& q = L.reqs[r];
+    const SegMeta& mt = L.metas[j];
+    uint64_t lo = q.time_low, hi = q.time_high;
+    if (!L.include_inactive && mt.has_pruning) {
+        // time_low' = min(max(time_low, global_time - inactive + 1), 2^63-1)   (community.py:2806)
+        if (L.responder_gt + 1 > mt.inactive) {
+            const uint64_t act = L.responder_gt + 1 - mt.inactive;
+            if (act > lo) lo = act;
+        }
+        if (lo > kMaxGt) lo = kMaxGt;
+    }
+    Plan p{};
+    p.dir = mt.dir;
+    p.a = p.b = mt.seg_a;
+    if (lo <= hi && mt.seg_a < mt.seg_b) {
+        p.a = lower_bound_gt(L.st.live_gt, mt.seg_a, mt.seg_b, lo);
+        p.b = upper_bound_gt(L.st.live_gt, p.a, mt.seg_b, hi);
+    }
+    const uint64_t span = p.b - p.a;
+    const uint64_t mod = q.modulo;
+    p.mode = 0;
+    p.ncand = span;
+    if (mod > 1 && span > 0) {
+        const uint64_t rem = (lo + q.offset) % mod;
+        const uint64_t g0 = rem ? lo + (mod - rem) : lo;
+        const uint64_t nenum = g0 > hi ? 0 : (hi - g0) / mod + 1;
+        uint32_t lg = 1;
+        while ((1ull << lg) < span && lg < 63) ++lg;
+        // enumerate when ~2*log2(span) random 64-byte probes per global time beat streaming 8 bytes per row
+        if (nenum * (uint64_t)(2 * lg + 2) * 8 < span) {
+            p.mode = 1;
+            p.g0 = g0;
+            p.ncand = nenum;
+        }
+    }
+    if (p.dir == DSY_RANDOM && p.ncand > 1) {
+        uint32_t bits = 1;
+        while ((1ull << (2 * bits)) < p.ncand) ++bits;
+        p.perm_bits = bits;
+        p.perm_key = (uint64_t)mix32(L.seed ^ ((uint64_t)r << 32) ^ j) << 32 | mix32(L.seed * 31 + r * 131 + j);
+    }
+    L.plans[idx] = p;
+    atomicAdd((unsigned long long*)&L.upper[r], (unsigned long long)span);
+}
+
+// ------------------------------------------------------------------------------------------- k_fill
+static constexpr int kFillThreads = 256;
+
+__device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* lds, uint64_t* total) {
+    // lds: kFillThreads + 1 words.  Simple Hillis-Steele over LDS (one per window step; not the hot loop).
+    const int t = threadIdx.x;
+    lds[t] = v;
+    __syncthreads();
+    for (int d = 1; d < kFillThreads; d <<= 1) {
+        const uint64_t add = t >= d ? lds[t - d] : 0;
+        __syncthreads();
+        lds[t] += add;
+        __syncthreads();
+    }
+    const uint64_t incl = lds[t];
+    *total = lds[kFillThreads - 1];
+    __syncthreads();
+    return incl - v;
+}
+
+__global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
+    __shared__ uint64_t scan[kFillThreads + 1];
+    __shared__ uint32_t first_cross;
+    const uint32_t r = blockIdx.x;
+    ReqState* S = &L.state[r];
+    if (S->done) {
+        if (threadIdx.x == 0) S->n_window = 0;
+        return;
+    }
+    const dsy_request& q = L.reqs[r];
+    const uint64_t W = L.window;
+    uint64_t* out = L.pair_row + (uint64_t)r * W;
+    uint32_t j = S->meta;
+    uint64_t c = S->cand, s = S->sub, filled = 0;
+    const uint64_t mod = q.modulo, off = q.offset;
+    while (j < L.J && filled < W) {
+        const Plan p = L.plans[(uint64_t)r * L.J + j];
+        if (c >= p.ncand) { ++j; c = 0; s = 0; continue; }
+        const uint64_t ci = c + threadIdx.x;
+        const bool valid = ci < p.ncand;
+        uint64_t x = 0, y = 0;  // live-row range of this candidate
+        if (valid) {
+            uint64_t cand = ci;
+            if (p.dir == DSY_DESC) cand = p.ncand - 1 - ci;
+            else if (p.dir == DSY_RANDOM && p.ncand > 1) cand = permute(ci, p.ncand, p.perm_bits, p.perm_key);
+            if (p.mode == 0) {
+                x = p.a + cand;
+                const bool match = mod <= 1 || ((L.st.live_gt[x] + off) % mod) == 0;
+                y = match ? x + 1 : x;
+            } else {
+                const uint64_t g = p.g0 + cand * mod;
+                x = lower_bound_gt(L.st.live_gt, p.a, p.b, g);
+                y = upper_bound_gt(L.st.live_gt, x, p.b, g);
+            }
+        }
+        uint64_t cnt = y - x;
+        const uint64_t skip = (threadIdx.x == 0) ? s : 0;
+        cnt = cnt > skip ? cnt - skip : 0;
+        uint64_t total;
+        const uint64_t pos = block_exclusive_scan(cnt, scan, &total);
+        // emit rows of this candidate that still fit in the window
+        for (uint64_t e = 0; e < cnt; ++e) {
+            const uint64_t dst = filled + pos + e;
+            if (dst >= W) break;
+            const uint64_t lr = (p.dir == DSY_DESC) ? (y - 1 - skip - e) : (x + skip + e);
+            out[dst] = L.st.live_row ? L.st.live_row[lr] : lr;
+        }
+        const uint64_t batch = (p.ncand - c) < (uint64_t)kFillThreads ? (p.ncand - c) : (uint64_t)kFillThreads;
+        if (filled + total <= W) {
+            filled += total;
+            c += batch;
+            s = 0;
+        } else {
+            if (threadIdx.x == 0) first_cross = 0xffffffffu;
+            __syncthreads();
+            if (valid && filled + pos + cnt > W) atomicMin(&first_cross, threadIdx.x);
+            __syncthreads();
+            const uint32_t t = first_cross;
+            // broadcast the crossing candidate's position through LDS
+            if (threadIdx.x == t) scan[kFillThreads] = W - filled - pos + skip;
+            __syncthreads();
+            s = scan[kFillThreads];
+            c = c + t;
+            filled = W;
+            __syncthreads();
+        }
+    }
+    if (threadIdx.x == 0) {
+        S->meta = j;
+        S->cand = c;
+        S->sub = s;
+        S->n_window = filled;
+        if (j >= L.J) S->exhausted = 1;
+    }
+}
+
+// -------------------------------------------------------------------------------------- k_pair_test
+template <class H, int CHUNK>
+__global__ void __launch_bounds__(256) k_pair_test(RespondLaunch L, const uint32_t* __restrict__ req_list,
+                                                   uint32_t n_list) {
+    const uint64_t W = L.window;
+    const uint64_t waves_per_req = W / 64;
+    const uint64_t total_waves = (uint64_t)n_list * waves_per_req;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t wave0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t wv = wave0; wv < total_waves; wv += wstride) {
+        const uint32_t r = req_list[wv / waves_per_req];
+        const uint64_t t = (wv % waves_per_req) * 64 + lane;
+        const uint64_t n = L.state[r].n_window;
+        if ((wv % waves_per_req) * 64 >= n) continue;  // whole wave past this claim's window (wave-uniform)
+        if (t >= n) continue;
+        const dsy_request& q = L.reqs[r];
+        const uint64_t row = L.pair_row[(uint64_t)r * W + t];
+        const uint64_t a = L.st.offsets[row], e = L.st.offsets[row + 1];
+        KeyView kv{L.st.blob + a, (uint32_t)(e - a), q.prefix, q.prefix_len};
+        H st;
+        hash_key<H>(kv, st);
+        const uint32_t* filt = (const uint32_t*)(L.filters + q.filter_offset);
+        const uint64_t m = q.m_bits;
+        uint32_t ok = 1;
+#pragma unroll
+        for (int jj = 0; jj < ChunkLimit<H, CHUNK>::kmax; ++jj) {
+            if (jj < (int)q.k) {
+                const uint64_t pos = bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, jj), m);
+                ok &= (filt[pos >> 5] >> (pos & 31)) & 1u;
+            }
+        }
+        L.miss[(uint64_t)r * W + t] = (uint8_t)(ok ^ 1u);
+        if (L.total_blocks) {  // algorithmic work of this wave: compression blocks and packet bytes
+            unsigned long long nb = n_blocks(kv.plen + kv.len, H::block_bytes, H::len_bytes), by = kv.len;
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) {
+                nb += __shfl_xor(nb, d, 64);
+                by += __shfl_xor(by, d, 64);
+            }
+            if (lane == __builtin_ffsll(__ballot(1)) - 1) {
+                atomicAdd((unsigned long long*)&L.total_blocks[0], nb);
+                atomicAdd((unsigned long long*)&L.total_blocks[1], by);
+            }
+        }
+    }
+}
+
+template <class H, int CHUNK>
+static hipError_t pair_test_family(const RespondLaunch& L, const uint32_t* list, uint32_t n_list) {
+    const uint64_t waves = (uint64_t)n_list * (L.window / 64);
+    uint64_t blocks = (waves + 3) / 4;
+    if (blocks > 256 * 16) blocks = 256 * 16;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL((k_pair_test<H, CHUNK>), dim3((uint32_t)blocks), dim3(256), 0, L.stream, L, list, n_list);
+    return hipGetLastError();
+}
+
+template <class H>
+static hipError_t pair_test_chunk(const RespondLaunch& L, uint32_t chunk, const uint32_t* list, uint32_t n) {
+    switch (chunk) {
+        case 2: return pair_test_family<H, 2>(L, list, n);
+        case 4: return pair_test_family<H, 4>(L, list, n);
+        default: return pair_test_family<H, 8>(L, list, n);
+    }
+}
+
+hipError_t launch_pair_test_list(const RespondLaunch& L, int kind, uint32_t chunk, const uint32_t* list, uint32_t n) {
+    switch (kind) {
+        case DSY_MD5: return pair_test_chunk<Md5>(L, chunk, list, n);
+        case DSY_SHA1: return chunk == 2 ? pair_test_family<Sha1, 2>(L, list, n) : pair_test_family<Sha1, 4>(L, list, n);
+        case DSY_SHA256: return pair_test_chunk<Sha256>(L, chunk, list, n);
+        case DSY_SHA384: return pair_test_chunk<Sha384>(L, chunk, list, n);
+        default: return pair_test_chunk<Sha512>(L, chunk, list, n);
+    }
+}
+
+// ----------------------------------------------------------------------------------------- k_compact
+__device__ __forceinline__ int64_t wave_inclusive_scan(int64_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int64_t o = __shfl_up(v, d, 64);
+        if (lane >= d) v += o;
+    }
+    return v;
+}
+
+__global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
+    const uint32_t r = blockIdx.x;
+    ReqState* S = &L.state[r];
+    if (S->done) return;
+    const uint64_t W = L.window;
+    const uint64_t n = S->n_window;
+    const uint32_t lane = threadIdx.x;
+    uint64_t emitted = S->emitted;
+    int64_t spent = S->spent;
+    uint32_t done = 0, overflow = S->overflow;
+    const int64_t limit = L.byte_limit;
+    for (uint64_t t0 = 0; t0 < n && !done; t0 += 64) {
+        const uint64_t t = t0 + lane;
+        const bool valid = t < n;
+        const bool miss = valid && L.miss[(uint64_t)r * W + t];
+        uint64_t row = 0;
+        int64_t len = 0;
+        if (miss) {
+            row = L.pair_row[(uint64_t)r * W + t];
+            len = (int64_t)(L.st.offsets[row + 1] - L.st.offsets[row]);
+        }
+        const int64_t incl = wave_inclusive_scan(len);
+        const int64_t excl = incl - len;
+        const uint64_t mmask = __ballot(miss);
+        const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+        const uint32_t rank = __popcll(mmask & lt);
+        // send while the budget before this packet is positive; the first packet is always sent
+        const bool inc = miss && ((emitted + rank == 0) || (spent + excl < limit));
+        const uint64_t imask = __ballot(inc);
+        const uint32_t nin = __popcll(imask);
+        if (inc) {
+            const uint64_t slot = emitted + rank;
+            if (slot < S->cap) L.out[S->out_base + slot] = row;
+            else overflow = 1;
+        }
+        // bytes of the included prefix = inclusive scan at the last included lane
+        int64_t sum_in = 0;
+        if (nin) {
+            const int last = 63 - __builtin_clzll(imask);
+            sum_in = __shfl(incl, last, 64);
+        }
+        emitted += nin;
+        spent += sum_in;
+        if (emitted > 0 && spent >= limit) done = 1;
+    }
+    overflow = __any(overflow) ? 1u : 0u;
+    if (lane == 0) {
+        S->emitted = emitted;
+        S->spent = spent;
+        S->overflow = overflow;
+        if (done || S->exhausted) S->done = 1;
+        else L.flags[0] = 1;
+        atomicAdd((unsigned long long*)L.total_pairs, (unsigned long long)n);
+    }
+}
+
+// -------------------------------------------------------------------------------------------- k_pack
+__global__ void __launch_bounds__(1024) k_scan_counts(RespondLaunch L, uint64_t* packed_offsets) {
+    // single workgroup: exclusive scan of state[r].emitted over R claims
+    __shared__ uint64_t part[1024];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (L.R + 1023) / 1024;
+    uint64_t sum = 0;
+    for (uint32_t i = 0; i < per; ++i) {
+        const uint32_t r = t * per + i;
+        if (r < L.R) sum += L.state[r].emitted;
+    }
+    part[t] = sum;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const uint64_t add = t >= (uint32_t)d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += add;
+        __syncthreads();
+    }
+    uint64_t run = part[t] - sum;
+    for (uint32_t i = 0; i < per; ++i) {
+        const uint32_t r = t * per + i;
+        if (r < L.R) {
+            packed_offsets[r] = run;
+            run += L.state[r].emitted;
+        }
+    }
+    if (t == 1023) packed_offsets[L.R] = part[1023];
+}
+
+__global__ void __launch_bounds__(256) k_copy_out(RespondLaunch L, const uint64_t* packed_offsets, uint64_t* packed) {
+    const uint32_t r = blockIdx.x;
+    const ReqState& S = L.state[r];
+    const uint64_t n = S.emitted < S.cap ? S.emitted : S.cap;
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) packed[packed_offsets[r] + i] = L.out[S.out_base + i];
+}
+
+hipError_t launch_plan(const RespondLaunch& L) {
+    const uint32_t n = L.R * L.J;
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_plan, dim3((n + 255) / 256), dim3(256), 0, L.stream, L);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill(const RespondLaunch& L) {
+    if (!L.R) return hipSuccess;
+    hipLaunchKernelGGL(k_fill, dim3(L.R), dim3(kFillThreads), 0, L.stream, L);
+    return hipGetLastError();
+}
+
+hipError_t launch_compact(const RespondLaunch& L) {
+    if (!L.R) return hipSuccess;
+    hipLaunchKernelGGL(k_compact, dim3(L.R), dim3(64), 0, L.stream, L);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack(const RespondLaunch& L, uint64_t* packed, uint64_t* packed_offsets, uint64_t*) {
+    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, L.stream, L, packed_offsets);
+    if (L.R) hipLaunchKernelGGL(k_copy_out, dim3(L.R), dim3(256), 0, L.stream, L, packed_offsets, packed);
+    return hipGetLastError();
+}
+
+}  // namespace dsy

@@ -1,0 +1,189 @@
+/*
+ * dsybloom.h -- C-ABI of the MI355X (gfx950) Bloom-filter synchronisation hot path.
+ *
+ * This is the drop-in boundary between Dispersy's Python host code and the hand-written HIP kernels in
+ * dispersy_amd/csrc/.  Everything here is `extern "C"`, plain pointers and sizes; no C++ or torch types cross
+ * it.  The Python side binds it with ctypes (dispersy_amd/_native.py); INTEGRATION.md shows the binding a
+ * reference maintainer would add.
+ *
+ * Conventions
+ *  - Every function returns an int status: DSY_OK (0) or a negative DSY_E* code.  dsy_last_error() returns a
+ *    thread-local message for the last failure on the calling thread.
+ *  - "host" entry points take caller-owned host buffers; they stage through the ctx's device workspace and
+ *    block until the result is back on the host.  "_dev" entry points take device pointers (HBM) and enqueue on
+ *    the ctx's stream without synchronising; call dsy_ctx_synchronize() before reading results.
+ *  - Filters cross the boundary serialised exactly like BloomFilter.bytes (bloomfilter.py:288-298): m/8 bytes,
+ *    bit i of the filter is bit (i & 7) of byte (i >> 3).  Device filter buffers must be allocated with
+ *    dsy_filter_words(m) 32-bit words (zero tail padding), i.e. a multiple of 4 bytes.
+ *  - Keys/packets are packed: a byte blob plus uint64 offsets[n+1]; key i is blob[offsets[i] .. offsets[i+1]).
+ *  - A ctx is not reentrant (internal mutex); separate ctx objects may be used concurrently from different
+ *    threads.
+ */
+#ifndef DSYBLOOM_H
+#define DSYBLOOM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DSY_ABI_VERSION 1
+
+/* status codes */
+#define DSY_OK 0
+#define DSY_EINVAL -1    /* invalid argument: mirrors the reference's asserts (bloomfilter.py:125-145) */
+#define DSY_EHIP -2      /* a HIP runtime call failed */
+#define DSY_ENOMEM -3    /* device allocation failed */
+#define DSY_ECAPACITY -4 /* output capacity too small; the required size is returned through the count pointer */
+#define DSY_EUNSORTED -5 /* store rows are not in (meta, global_time) order */
+
+/* hash families, selected exactly as bloomfilter.py:134-156 does from (m, k) */
+#define DSY_MD5 0
+#define DSY_SHA1 1
+#define DSY_SHA256 2
+#define DSY_SHA384 3
+#define DSY_SHA512 4
+
+/* synchronisation directions of a SyncDistribution (distribution.py:180-184) */
+#define DSY_ASC 0
+#define DSY_DESC 1
+#define DSY_RANDOM 2
+
+typedef struct dsy_ctx dsy_ctx;
+typedef struct dsy_store dsy_store;
+
+/* One Bloom filter's hashing parameters.  The host computes them with the reference's formulas
+ * (bloomfilter.py:69-160); the library validates that hash_kind/chunk_bytes agree with (m_bits, k) and
+ * returns DSY_EINVAL otherwise.  prefix_len < 256 (bloomfilter.py:131). */
+typedef struct dsy_bloom_params {
+    uint64_t m_bits;     /* filter size in bits, > 0, multiple of 8 */
+    uint32_t k;          /* number of index chunks per key, 0 < k <= m_bits */
+    int32_t hash_kind;   /* DSY_MD5 .. DSY_SHA512 */
+    uint32_t chunk_bytes; /* 2 ('H'), 4 ('L') or 8 ('Q') */
+    uint32_t prefix_len; /* 0..255 */
+    uint8_t prefix[256]; /* the salt prefix: the digest input is prefix || key (bloomfilter.py:161,168-169) */
+} dsy_bloom_params;
+
+/* One incoming claim (an introduction-request's sync block, conversion.py:732-799, as resolved by
+ * on_introduction_request, community.py:2545-2553). */
+typedef struct dsy_request {
+    uint64_t time_low;      /* inclusive, already min(., 2^63-1) */
+    uint64_t time_high;     /* inclusive, already resolved (0 on the wire -> responder global_time) and clamped */
+    uint32_t modulo;        /* >= 1 */
+    uint32_t offset;        /* < modulo */
+    uint64_t filter_offset; /* byte offset of this claim's filter inside the `filters` buffer (multiple of 4) */
+    uint64_t m_bits;
+    uint32_t k;
+    int32_t hash_kind;
+    uint32_t chunk_bytes;
+    uint32_t prefix_len;
+    uint8_t prefix[256];
+} dsy_request;
+
+/* One syncable meta-message, in the order the responder serves them: priority DESC, stable
+ * (community.py:2790-2794).  Metas with priority <= 32 must not be passed. */
+typedef struct dsy_meta {
+    uint32_t meta_id;            /* value stored in the store's meta column (sync.meta_message) */
+    int32_t direction;           /* DSY_ASC / DSY_DESC / DSY_RANDOM */
+    uint32_t has_pruning;        /* 1 if the meta uses GlobalTimePruning (distribution.py:68-114) */
+    uint32_t _pad;
+    uint64_t inactive_threshold; /* GlobalTimePruning.inactive_threshold */
+} dsy_meta;
+
+/* ---------------------------------------------------------------------------------------------- library */
+int dsy_abi_version(void);
+const char* dsy_last_error(void);
+/* Number of 32-bit words a device filter buffer for an m-bit filter occupies. */
+uint64_t dsy_filter_words(uint64_t m_bits);
+/* Validate (m, k, hash_kind, chunk) against bloomfilter.py:134-156 and return the hash family it implies in
+ * *out_kind and chunk width in *out_chunk. */
+int dsy_hash_family(uint64_t m_bits, uint32_t k, int32_t* out_kind, uint32_t* out_chunk);
+
+int dsy_ctx_create(int device, dsy_ctx** out);
+int dsy_ctx_destroy(dsy_ctx* ctx);
+int dsy_ctx_synchronize(dsy_ctx* ctx);
+/* The HIP stream (hipStream_t) the ctx enqueues on. */
+void* dsy_ctx_stream(dsy_ctx* ctx);
+/* Kernel timing: when enabled, HIP events bracket every launch of the hash kernels on the ctx stream.
+ * dsy_ctx_kernel_time returns the accumulated milliseconds and launch count of kernel class `which`
+ * (0 = hash/test of the responder, 1 = single-filter bloom kernels, 2 = selection, 3 = compaction) and, for
+ * class 0, the algorithmic work those launches did: compression blocks and packet bytes hashed. */
+int dsy_ctx_set_timing(dsy_ctx* ctx, int enable);
+int dsy_ctx_kernel_time(dsy_ctx* ctx, int which, double* out_ms, uint64_t* out_launches, uint64_t* out_blocks,
+                        uint64_t* out_bytes);
+int dsy_ctx_reset_timing(dsy_ctx* ctx);
+
+/* ---------------------------------------------------------------------------------- BloomFilter kernels */
+/* Replaces BloomFilter.add / add_keys (bloomfilter.py:163-194): ORs the k bits of every key into filter_inout
+ * (m/8 bytes, serialised as BloomFilter.bytes). */
+int dsy_bloom_add(dsy_ctx* ctx, const dsy_bloom_params* p, const uint8_t* blob, uint64_t blob_len,
+                  const uint64_t* offsets, uint64_t n, uint8_t* filter_inout);
+/* Replaces the digest + probe of BloomFilter.__contains__ (bloomfilter.py:202-212) and not_filter
+ * (:214-237): out_present[i] = 1 iff every probe bit of key i is set. */
+int dsy_bloom_test(dsy_ctx* ctx, const dsy_bloom_params* p, const uint8_t* blob, uint64_t blob_len,
+                   const uint64_t* offsets, uint64_t n, const uint8_t* filter, uint8_t* out_present);
+/* The k bit positions of every key (digest slicing of bloomfilter.py:158-171): out_idx[i*k + j]. */
+int dsy_bloom_indices(dsy_ctx* ctx, const dsy_bloom_params* p, const uint8_t* blob, uint64_t blob_len,
+                      const uint64_t* offsets, uint64_t n, uint64_t* out_idx);
+
+/* Device-pointer forms.  d_blob must stay readable for DSY_BLOB_GUARD bytes past offsets[n] (the kernels read
+ * whole 64/128-byte blocks and mask); d_filter holds dsy_filter_words(m) words. */
+#define DSY_BLOB_GUARD 256
+int dsy_bloom_add_dev(dsy_ctx* ctx, const dsy_bloom_params* p, const uint8_t* d_blob, const uint64_t* d_offsets,
+                      uint64_t n, uint32_t* d_filter);
+int dsy_bloom_test_dev(dsy_ctx* ctx, const dsy_bloom_params* p, const uint8_t* d_blob, const uint64_t* d_offsets,
+                       uint64_t n, const uint32_t* d_filter, uint8_t* d_present);
+
+/* ------------------------------------------------------------------------------------------ packet store */
+/* The packed HBM export of the `sync` table (dispersydatabase.py:53-64): rows sorted by
+ * (meta_message, global_time, rowid) -- the order of the sync_meta_message_undone_global_time_index.
+ * undone may be NULL (all rows live).  Rows with undone != 0 never take part in selection. */
+int dsy_store_upload(dsy_ctx* ctx, const uint8_t* blob, uint64_t blob_len, const uint64_t* offsets, uint64_t n,
+                     const uint64_t* global_time, const uint32_t* meta, const uint8_t* undone, dsy_store** out);
+/* Same, over device buffers the caller keeps alive (no copy).  d_blob needs DSY_BLOB_GUARD readable bytes
+ * past offsets[n]. */
+int dsy_store_attach(dsy_ctx* ctx, const uint8_t* d_blob, uint64_t blob_len, const uint64_t* d_offsets, uint64_t n,
+                     const uint64_t* d_global_time, const uint32_t* d_meta, const uint8_t* d_undone, dsy_store** out);
+int dsy_store_free(dsy_store* store);
+uint64_t dsy_store_rows(const dsy_store* store);
+
+/* Claim side (community.py:821, :924 and dispersy_store :698): OR the packets of the given store rows into a
+ * filter.  rows are store row positions (0-based, export order). */
+int dsy_bloom_add_rows(dsy_ctx* ctx, const dsy_bloom_params* p, const dsy_store* store, const uint64_t* rows,
+                       uint64_t n, uint8_t* filter_inout);
+
+/* ------------------------------------------------------------------------------------------- responder */
+/* Batched responder: replaces _get_packets_for_bloomfilters (community.py:2746-2811) plus the byte-limited
+ * not_filter loop of on_introduction_request (:2555-2567) for R claims at once.
+ *
+ * For claim r the response is the ordered list of store rows the reference would send: metas in the given
+ * order; within a meta rows with undone == 0, time_low' <= global_time <= time_high and
+ * (global_time + offset) % modulo == 0, in global_time ASC / DESC (ties by row) or a seeded random order for
+ * DSY_RANDOM; keep rows whose packet is NOT in the claim's filter; stop after the packet whose length makes the
+ * running byte total reach byte_limit (that packet is included).  time_low' = max(time_low,
+ * responder_global_time - inactive_threshold + 1) for GlobalTimePruning metas when include_inactive == 0.
+ *
+ * Output: out_idx[out_req_offsets[r] .. out_req_offsets[r+1]) are claim r's rows in send order.  If out_cap
+ * is too small DSY_ECAPACITY is returned and out_req_offsets[R] holds the required size. */
+int dsy_sync_respond(dsy_ctx* ctx, const dsy_store* store, const dsy_request* reqs, uint32_t R,
+                     const uint8_t* filters, uint64_t filters_len, const dsy_meta* metas, uint32_t nmeta,
+                     uint64_t responder_global_time, int include_inactive, int64_t byte_limit, uint64_t random_seed,
+                     uint64_t* out_idx, uint64_t out_cap, uint64_t* out_req_offsets);
+
+/* Device form: reqs/metas stay host structs (uploaded into the ctx workspace), filters are device memory
+ * (d_filters), results stay in device memory owned by the ctx until the next call:
+ *   *d_out_idx   -> uint64 rows, claim r at [d_out_offsets[r], d_out_offsets[r+1])
+ *   *d_out_offsets -> uint64[R+1]
+ * *out_total_pairs receives the number of (claim, packet) pairs hashed and tested (the bench metric's unit). */
+int dsy_sync_respond_dev(dsy_ctx* ctx, const dsy_store* store, const dsy_request* reqs, uint32_t R,
+                         const uint8_t* d_filters, const dsy_meta* metas, uint32_t nmeta,
+                         uint64_t responder_global_time, int include_inactive, int64_t byte_limit,
+                         uint64_t random_seed, const uint64_t** d_out_idx, const uint64_t** d_out_offsets,
+                         uint64_t* out_total_pairs);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DSYBLOOM_H */

@@ -1,0 +1,139 @@
+"""BloomFilter parity on the MI355X: the HIP kernels against the reference's golden vectors and the CPU oracle.
+
+Bit-exact: filter bytes, bit positions, membership and not_filter output order.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from dispersy_amd import BloomFilter
+from dispersy_amd import _native
+from dispersy_amd.bloomfilter import pack_keys
+from golden_util import expected_bytes, keys_for, load
+from keys import packet_list, random_packets
+from oracle.bloom_ref import OracleBloom
+
+pytestmark = pytest.mark.gpu
+
+BLOOM = load("bloom_vectors.json")
+
+
+def make(case):
+    ctor, prefix = case["ctor"], bytes.fromhex(case["prefix"])
+    if ctor[0] == "m_f":
+        return BloomFilter(ctor[1], float(ctor[2]), prefix)
+    return BloomFilter(float(ctor[1]), ctor[2], prefix)
+
+
+@pytest.mark.parametrize("case", BLOOM["cases"], ids=[c["name"] for c in BLOOM["cases"]])
+def test_golden_case(case):
+    e = case["expect"]
+    keys, probes = keys_for(case["keys"]), keys_for(case["probes"])
+    bf = make(case)
+    assert (bf.size, bf.functions, bf.hash_name, bf.chunk_bytes) == (e["m"], e["k"], e["hash"], e["chunk"])
+    if keys:
+        blob, off = pack_keys(keys[:64])
+        idx = _native.default_context().bloom_indices(bf.params, blob, off)
+        assert idx.tolist() == e["indices"]
+    blob, off = pack_keys(probes[:16])
+    assert _native.default_context().bloom_indices(bf.params, blob, off).tolist() == e["probe_indices"]
+    bf.add_keys(keys)
+    assert hashlib.sha256(bf.bytes).hexdigest() == e["bytes_sha256"]
+    assert bf.bytes == expected_bytes(e)
+    assert bf.bits_checked == e["bits_checked"]
+    assert bf.contains_many(probes).astype(int).tolist() == e["present"]
+    assert [i for _, i in bf.not_filter((p, i) for i, p in enumerate(probes))] == e["missing"]
+    clone = BloomFilter(bf.bytes, bf.functions, bf.prefix)
+    assert clone.bytes == bf.bytes
+    assert [p in clone for p in probes[:20]] == [bool(x) for x in e["present"][:20]]
+
+
+def test_chunk_q_indices():
+    """m >= 2^31: 8-byte 'Q' chunks, 64-bit modulo (bloomfilter.py:135-136)."""
+    ctx = _native.default_context()
+    for row in BLOOM["chunk_q"]:
+        p = _native.bloom_params(row["m"], row["k"], _native.HASH_KINDS[row["hash"]], row["chunk"],
+                                 bytes.fromhex(row["prefix"]))
+        blob, off = pack_keys(keys_for(row["keys"]))
+        assert ctx.bloom_indices(p, blob, off).tolist() == row["indices"]
+
+
+def test_single_add_and_contains():
+    bf = BloomFilter(10160, 0.01, prefix=b"\x2a")
+    ref = OracleBloom.from_m_f(10160, 0.01, b"\x2a")
+    for i in range(50):
+        key = b"packet-%d" % i
+        bf.add(key)
+        ref.add(key)
+        assert bf.bytes == ref.to_bytes()
+    assert all(b"packet-%d" % i in bf for i in range(50))
+    assert bf._filter == ref.bits
+    bf.clear()
+    assert bf.bits_checked == 0 and not any(bf.bytes)
+
+
+@pytest.mark.parametrize("m,f,prefix", [(10160, 0.01, b"\x00\x01\x02\x03"), (4096, 0.001, b"x"),
+                                        (1 << 20, 0.01, b"\x07"), (1 << 16, 0.001, b"\x33" * 70),
+                                        (1 << 16, 0.0001, b""), (8192, 0.00001, b"q" * 200)])
+def test_heavy_tail_against_oracle(m, f, prefix):
+    """Pareto-ish lengths up to the UDP cap (endpoint.py:263), all hash families, vs the oracle."""
+    rng = np.random.Generator(np.random.PCG64(m + len(prefix)))
+    lengths = np.minimum((rng.pareto(1.2, 3000) + 1) * 60, 65476).astype(np.int64)
+    lengths[:5] = [0, 1, 55, 56, 64]
+    keys = [rng.bytes(int(n)) for n in lengths]
+    bf, ref = BloomFilter(m, f, prefix), OracleBloom.from_m_f(m, f, prefix)
+    bf.add_keys(keys[:1500])
+    ref.add_keys(keys[:1500])
+    assert bf.bytes == ref.to_bytes()
+    assert bf.contains_many(keys).tolist() == [k in ref for k in keys]
+
+
+def test_large_batch_against_oracle():
+    """100k adds + 200k tests at the MTU size (config 1 shape, scaled to finish in seconds on the oracle)."""
+    blob, off = random_packets(1234, 100_000, 100, 1500)
+    bf = BloomFilter(10160, 0.01, prefix=b"\x00\x01\x02\x03")
+    bf.add_packed(blob, off)
+    ref = OracleBloom.from_m_f(10160, 0.01, b"\x00\x01\x02\x03")
+    ref.add_keys(blob[int(off[i]):int(off[i + 1])] for i in range(len(off) - 1))
+    assert bf.bytes == ref.to_bytes()
+    # at capacity: 1059 keys, then 200k probes
+    keys = packet_list(99, 1059, 100, 1500)
+    probes_blob, probes_off = random_packets(4321, 200_000, 100, 1500)
+    bf2, ref2 = BloomFilter(10160, 0.01, prefix=b"\x00\x01\x02\x03"), OracleBloom.from_m_f(10160, 0.01, b"\x00\x01\x02\x03")
+    bf2.add_keys(keys)
+    ref2.add_keys(keys)
+    got = _native.default_context().bloom_test(bf2.params, probes_blob, probes_off, bf2.bytes)
+    want = [probes_blob[int(probes_off[i]):int(probes_off[i + 1])] in ref2 for i in range(len(probes_off) - 1)]
+    assert got.astype(bool).tolist() == want
+
+
+# ---- tests/test_bloomfilter.py of the reference, re-expressed (keys as bytes)
+def test_ref_fixed_size_constructor():
+    for bloom in (BloomFilter(128 * 8, 0.25), BloomFilter(128 * 8, 0.25, b""), BloomFilter(128 * 8, 0.25, prefix=b"")):
+        bloom.add_keys(str(i).encode() for i in range(100))
+        assert (bloom.size, len(bloom.bytes), bloom.prefix) == (1024, 128, b"")
+    for bloom in (BloomFilter(128 * 8, 0.25, b"p"), BloomFilter(128 * 8, 0.25, prefix=b"p")):
+        bloom.add_keys(str(i).encode() for i in range(100))
+        assert (bloom.size, len(bloom.bytes), bloom.prefix) == (1024, 128, b"p")
+
+
+def test_ref_load_constructor():
+    for prefix in (b"", b"p"):
+        bloom = BloomFilter(128 * 8, 0.25, prefix)
+        bloom.add_keys(str(i).encode() for i in range(100))
+        raw, k = bloom.bytes, bloom.functions
+        for clone in (BloomFilter(raw, k, prefix), BloomFilter(raw, k, prefix=prefix)):
+            assert clone.size == 1024 and clone.bytes == raw and clone.prefix == prefix
+            assert all(str(i).encode() in clone for i in range(100))
+
+
+def test_ref_false_positives():
+    for prefix in (b"", b"p"):
+        for n in (128, 1024):
+            for f in (0.1, 0.2, 0.3, 0.4):
+                bloom = BloomFilter(f, n, prefix)
+                bloom.add_keys(str(i).encode() for i in range(n))
+                assert bloom.contains_many([str(i).encode() for i in range(n)]).all()
+                fp = int(bloom.contains_many([str(i).encode() for i in range(n, n + 10000)]).sum())
+                assert abs(fp / 10000.0 - f) <= 0.05

@@ -1,0 +1,56 @@
+"""The C-ABI library loads and exports every symbol include/dsybloom.h declares (CPU only; no compute calls)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from dispersy_amd import _native
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "dsybloom.h")
+
+
+def declared_functions():
+    text = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w\s\*]+?\b(dsy_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_header_declares_the_boundary():
+    names = declared_functions()
+    for must in ("dsy_bloom_add", "dsy_bloom_test", "dsy_sync_respond", "dsy_store_upload", "dsy_ctx_create"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    if not os.path.isfile(_native.LIB_PATH):
+        pytest.fail("libdsybloom.so not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(_native.LIB_PATH)
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_binding_covers_every_declared_symbol():
+    assert sorted(_native.SIGNATURES) == declared_functions()
+
+
+def test_host_only_entry_points():
+    lib = _native.load_library()
+    assert lib.dsy_abi_version() == 1
+    assert lib.dsy_filter_words(10160) == 318
+    k, c = ctypes.c_int32(), ctypes.c_uint32()
+    # bloomfilter.py:134-156 table
+    for m, kf, kind, chunk in ((10160, 7, 0, 2), (4096, 10, 1, 2), (1 << 20, 7, 2, 4), (1 << 15, 10, 3, 4),
+                               (1 << 16, 14, 4, 4), (1 << 31, 7, 4, 8), (1 << 33, 5, 3, 8), (32768, 4, 0, 4)):
+        assert lib.dsy_hash_family(m, kf, ctypes.byref(k), ctypes.byref(c)) == 0
+        assert (k.value, c.value) == (kind, chunk), (m, kf)
+    assert lib.dsy_hash_family(12, 3, ctypes.byref(k), ctypes.byref(c)) == _native.DSY_EINVAL
+    assert b"multiple of eight" in lib.dsy_last_error()
+    assert lib.dsy_hash_family(1 << 16, 17, ctypes.byref(k), ctypes.byref(c)) == _native.DSY_EINVAL
+    assert lib.dsy_hash_family(64, 65, ctypes.byref(k), ctypes.byref(c)) == _native.DSY_EINVAL
+
+
+def test_struct_layouts_match_header():
+    assert ctypes.sizeof(_native.BloomParams) == 8 + 4 * 4 + 256
+    assert ctypes.sizeof(_native.Request) == 8 * 2 + 4 * 2 + 8 * 2 + 4 * 4 + 256
+    assert ctypes.sizeof(_native.Meta) == 24
