@@ -12,6 +12,7 @@ every digest of `prefix || key`, its slicing into k big-endian chunks mod m, and
 itself is kept as its serialised little-endian bytes (`.bytes`), which is the exact layout the kernels use.
 There is no CPU path for the digests: without the HIP library, add/test raise `NativeUnavailable`.
 """
+import ctypes
 import logging
 from math import ceil, log
 
@@ -135,6 +136,18 @@ class BloomFilter(object):
         """Add keys already packed as (blob, offsets[n+1]) -- avoids building a list of bytes objects."""
         if len(offsets) > 1:
             self._raw[:] = self._ctx().bloom_add(self.params, blob, offsets, self._raw)
+
+    def add_store_rows(self, store, rows):
+        """Add the packets of `store` rows (a SyncStore already in HBM): the claim side's bloom.add_keys over
+        selected rows (community.py:821, :924) without moving packets back to the host."""
+        rows = np.ascontiguousarray(rows, dtype=np.uint64)
+        if not len(rows):
+            return
+        ctx = store.ctx
+        buf = ctypes.create_string_buffer(bytes(self._raw), len(self._raw))
+        _native.check(ctx.lib.dsy_bloom_add_rows(ctx.handle, ctypes.byref(self.params), store.handle,
+                                                 rows.ctypes.data, len(rows), buf))
+        self._raw[:] = buf.raw
 
     def clear(self):
         """Set all bits in the filter to zero (bloomfilter.py:196-200)."""

@@ -1,0 +1,419 @@
+"""The sync surface of Dispersy's `Community` (community.py of the reference), over a `SyncStore` in HBM.
+
+Kept (same names, argument meaning, return values and statistics):
+  dispersy_claim_sync_bloom_filter(request_cache)      community.py:709-758   (reuse / adaptive skip / new claim)
+  _dispersy_claim_sync_bloom_filter_largest(rc)         community.py:763-837   (default strategy)
+  _select_bloomfilter_range / _select_and_fix           community.py:839-903
+  _dispersy_claim_sync_bloom_filter_modulo(rc)          community.py:908-933
+  dispersy_store(messages)                              community.py:680-707   (cached-claim update)
+  _get_packets_for_bloomfilters(requests, include_inactive)  community.py:2746-2811
+  the byte-limited responder loop                       community.py:2531-2572
+and the overridable properties of community.py:599-678, :935-941 (the reference's plugin hooks).
+
+The responder runs as ONE batched call into the HIP library (`respond`): selection, prefix-salted digest, probe
+and byte-limited compaction for every claim of a receive batch.  The claim side selects its packet range on the
+host from the store's index columns (the reference does this in SQLite) and builds the filter on the GPU from the
+store rows already in HBM.
+"""
+import ctypes
+import random as _random_module
+from collections import OrderedDict, namedtuple
+from math import ceil
+
+import numpy as np
+
+from . import _native
+from .bloomfilter import BloomFilter
+from .distribution import GlobalTimePruning, SyncDistribution
+
+MAX_GT = 2 ** 63 - 1  # sqlite's signed 64-bit ceiling (community.py:2545-2548)
+
+# the sync part of an introduction-request payload (payload.py:31-153): time_high == 0 means "up to the
+# responder's global time"
+ClaimRequest = namedtuple("ClaimRequest", "time_low time_high modulo offset bloom_filter")
+
+
+class SyncCache(object):
+    """community.py:57-67."""
+
+    def __init__(self, time_low, time_high, modulo, offset, bloom_filter):
+        self.time_low = time_low
+        self.time_high = time_high
+        self.modulo = modulo
+        self.offset = offset
+        self.bloom_filter = bloom_filter
+        self.times_used = 0
+        self.responses_received = 0
+        self.candidate = None
+
+
+class SyncStatistics(object):
+    """The four bloom counters of CommunityStatistics (statistics.py:305-308)."""
+
+    def __init__(self):
+        self.sync_bloom_new = 0
+        self.sync_bloom_reuse = 0
+        self.sync_bloom_send = 0
+        self.sync_bloom_skip = 0
+
+
+class SyncCommunity(object):
+    """Bloom-filter synchronisation of one community over a SyncStore."""
+
+    # probability steps to get a sync skipped if the previous one was empty (community.py:86-87)
+    _SKIP_CURVE_STEPS = [0, 0, 0.1, 0.2, 0.3, 0.4, 0.5, 0.6, 0.7, 0.8, 0.9]
+    _SKIP_STEPS = len(_SKIP_CURVE_STEPS)
+
+    def __init__(self, store, meta_messages, global_time=0, signature_length=60, rng=None, random_source=None):
+        """rng: the community's private Random (expovariate pivot, community.py:778-780); random_source: provider of
+        the module-level random()/randint() draws (prefix, skip, modulo offset).  Both default to `random`."""
+        self._store = store
+        self._meta_messages = OrderedDict((m.name, m) for m in meta_messages)
+        self._global_time = global_time
+        self._signature_length = signature_length
+        self._random = rng if rng is not None else _random_module.Random()
+        self._rand = random_source if random_source is not None else _random_module
+        self._statistics = SyncStatistics()
+        self._sync_cache = None
+        self._sync_cache_skip_count = 0
+        self._nrsyncpackets = 0
+        self.dispersy_acceptable_global_time_range = 10000  # community.py:952-953
+
+    # ------------------------------------------------------------------------ plugin hooks (properties)
+    @property
+    def dispersy_enable_bloom_filter_sync(self):
+        return True
+
+    @property
+    def dispersy_sync_bloom_filter_error_rate(self):
+        return 0.01
+
+    @property
+    def dispersy_sync_bloom_filter_bits(self):
+        # one MTU: 1500 - IP 60 - UDP 8 - header 51 - signature - payload 21 - sync 30 bytes (community.py:637-666)
+        return (1500 - 60 - 8 - 51 - self._signature_length - 21 - 30) * 8
+
+    @property
+    def dispersy_sync_bloom_filter_strategy(self):
+        return self._dispersy_claim_sync_bloom_filter_largest
+
+    @property
+    def dispersy_sync_skip_enable(self):
+        return True
+
+    @property
+    def dispersy_sync_cache_enable(self):
+        return True
+
+    @property
+    def dispersy_sync_response_limit(self):
+        return 5 * 1024
+
+    # ------------------------------------------------------------------------------------- community state
+    @property
+    def store(self):
+        return self._store
+
+    @property
+    def global_time(self):
+        return max(1, self._global_time)
+
+    @property
+    def acceptable_global_time(self):
+        """community.py:1015-1058, the branch without >5 candidate opinions (the walker is out of scope)."""
+        if not self.dispersy_enable_bloom_filter_sync:
+            return MAX_GT
+        return min(self._global_time + self.dispersy_acceptable_global_time_range, MAX_GT)
+
+    def update_global_time(self, global_time):
+        if global_time > self._global_time:
+            self._global_time = global_time
+
+    def get_meta_messages(self):
+        return list(self._meta_messages.values())
+
+    def _syncable_meta_ids(self):
+        return [m.database_id for m in self._meta_messages.values() if m.syncable]
+
+    def _served_metas(self):
+        """Syncable metas, priority DESC, stable (community.py:2790-2794)."""
+        return sorted((m for m in self._meta_messages.values() if m.syncable),
+                      key=lambda m: m.distribution.priority, reverse=True)
+
+    # ----------------------------------------------------------------------------------- requester side
+    def dispersy_store(self, messages):
+        """community.py:680-707: packets just stored that fall in the cached claim are added to its filter, and
+        responses from the claim's candidate are counted.  All qualifying packets go to the GPU in one launch."""
+        cache = self._sync_cache
+        if not cache:
+            return
+        packets = []
+        for message in messages:
+            gt = message.distribution.global_time
+            if (message.distribution.priority > 32 and cache.time_low <= gt <= cache.time_high and
+                    (gt + cache.offset) % cache.modulo == 0):
+                packets.append(message.packet)
+                if (cache.candidate and getattr(message, "candidate", None) and
+                        cache.candidate.sock_addr == message.candidate.sock_addr):
+                    cache.responses_received += 1
+        if packets:
+            cache.bloom_filter.add_keys(packets)
+
+    def dispersy_claim_sync_bloom_filter(self, request_cache):
+        """community.py:709-758.  Returns (time_low, time_high, modulo, offset, bloom_filter) or None."""
+        if self._sync_cache:
+            if self._sync_cache.responses_received > 0:
+                if self.dispersy_sync_skip_enable:
+                    self._sync_cache_skip_count = 0
+                if self.dispersy_sync_cache_enable and self._sync_cache.times_used < 100:
+                    self._statistics.sync_bloom_reuse += 1
+                    self._statistics.sync_bloom_send += 1
+                    cache = self._sync_cache
+                    cache.times_used += 1
+                    cache.responses_received = 0
+                    cache.candidate = getattr(request_cache, "helper_candidate", None)
+                    return cache.time_low, cache.time_high, cache.modulo, cache.offset, cache.bloom_filter
+            elif self._sync_cache.times_used == 0:
+                self._sync_cache_skip_count = min(self._sync_cache_skip_count + 1, self._SKIP_STEPS)
+
+        if (self.dispersy_sync_skip_enable and self._sync_cache_skip_count and
+                self._rand.random() < self._SKIP_CURVE_STEPS[self._sync_cache_skip_count - 1]):
+            self._statistics.sync_bloom_skip += 1
+            self._sync_cache = None
+            return None
+
+        sync = self.dispersy_sync_bloom_filter_strategy(request_cache)
+        if sync:
+            self._sync_cache = SyncCache(*sync)
+            self._sync_cache.candidate = getattr(request_cache, "helper_candidate", None)
+            self._statistics.sync_bloom_new += 1
+            self._statistics.sync_bloom_send += 1
+        return sync
+
+    def _new_claim_filter(self):
+        return BloomFilter(self.dispersy_sync_bloom_filter_bits, self.dispersy_sync_bloom_filter_error_rate,
+                           prefix=bytes([int(self._rand.random() * 256)]))
+
+    def _empty_claim(self, acceptable):
+        return (1, acceptable, 1, 0, BloomFilter(8, 0.1, prefix=b"\x00"))
+
+    def _dispersy_claim_sync_bloom_filter_largest(self, request_cache):
+        """community.py:763-837: a filter over <= capacity packets around an exponentially distributed pivot."""
+        syncable = self._syncable_meta_ids()
+        acceptable_global_time = self.acceptable_global_time
+        if not syncable:
+            return self._empty_claim(acceptable_global_time)
+        bloom = self._new_claim_filter()
+        capacity = bloom.get_capacity(self.dispersy_sync_bloom_filter_error_rate)
+        desired_mean = self.global_time / 2.0
+        from_gbtime = self.global_time - int(self._random.expovariate(1.0 / desired_mean))
+        if from_gbtime < 1:
+            from_gbtime = int(self._random.random() * self.global_time)
+
+        if from_gbtime > 1 and self._nrsyncpackets >= capacity:
+            right, rightdata = self._select_bloomfilter_range(request_cache, syncable, from_gbtime - 1, capacity, True)
+            if right[2] == capacity:
+                left, leftdata = self._select_bloomfilter_range(request_cache, syncable, from_gbtime + 1, capacity, False)
+                left_range = (left[1] or self.global_time) - left[0]
+                right_range = (right[1] or self.global_time) - right[0]
+                bloomfilter_range, data = (left, leftdata) if left_range > right_range else (right, rightdata)
+            else:
+                bloomfilter_range, data = right, rightdata
+        else:
+            bloomfilter_range = [1, acceptable_global_time]
+            data, fixed = self._select_and_fix(request_cache, syncable, 0, capacity, True)
+            if len(data) > 0 and fixed:
+                bloomfilter_range[1] = data[-1][0]
+                self._nrsyncpackets = capacity + 1
+
+        if len(data) > 0:
+            bloom.add_store_rows(self._store, [row for _, row in data])
+            return (min(bloomfilter_range[0], acceptable_global_time),
+                    min(bloomfilter_range[1], acceptable_global_time), 1, 0, bloom)
+        return self._empty_claim(acceptable_global_time)
+
+    def _select_bloomfilter_range(self, request_cache, syncable, global_time, to_select, higher=True):
+        """community.py:839-879."""
+        data, fixed = self._select_and_fix(request_cache, syncable, global_time, to_select, higher)
+        lowerfixed = higherfixed = True
+        if len(data) < to_select:
+            to_select = to_select - len(data)
+            if to_select > 25:
+                if higher:
+                    lowerdata, lowerfixed = self._select_and_fix(request_cache, syncable, global_time + 1, to_select, False)
+                    data = lowerdata + data
+                else:
+                    higherdata, higherfixed = self._select_and_fix(request_cache, syncable, global_time - 1, to_select, True)
+                    data = data + higherdata
+
+        bloomfilter_range = [data[0][0], data[-1][0], len(data)]
+        if higher:
+            bloomfilter_range[0] = min(bloomfilter_range[0], global_time + 1)
+            if not fixed:
+                bloomfilter_range[1] = self.acceptable_global_time
+            if not lowerfixed:
+                bloomfilter_range[0] = 1
+        else:
+            bloomfilter_range[1] = max(bloomfilter_range[1], global_time - 1)
+            if not fixed:
+                bloomfilter_range[0] = 1
+            if not higherfixed:
+                bloomfilter_range[1] = self.acceptable_global_time
+        return bloomfilter_range, data
+
+    def _select_and_fix(self, request_cache, syncable, global_time, to_select, higher=True):
+        """community.py:881-903 over the store's index: up to to_select+1 live packets strictly above (below) the
+        pivot in global-time order; when over-full, the trailing global-time group is dropped.  Returns
+        ([(global_time, store_row)], fixed)."""
+        st, limit = self._store, to_select + 1
+        gts, rows = [], []
+        for meta_id in syncable:
+            seg = st.live_rows(meta_id)
+            g = st.global_time[seg]
+            if higher:
+                i = int(np.searchsorted(g, global_time, side="right"))
+                part = seg[i:i + limit]
+            else:
+                i = int(np.searchsorted(g, max(global_time, 0), side="left")) if global_time > 0 else 0
+                part = seg[max(0, i - limit):i][::-1]
+            rows.append(part)
+            gts.append(st.global_time[part])
+        rows = np.concatenate(rows) if rows else np.zeros(0, dtype=np.int64)
+        gts = np.concatenate(gts) if gts else np.zeros(0, dtype=np.uint64)
+        order = np.argsort(gts, kind="stable")
+        if not higher:
+            order = order[::-1]
+        rows, gts = rows[order][:limit], gts[order][:limit]
+        data = [(int(g), int(r)) for g, r in zip(gts, rows)]
+        fixed = False
+        if len(data) > to_select:
+            fixed = True
+            cut = data[-1][0]
+            del data[-1]
+            while data and data[-1][0] == cut:
+                del data[-1]
+        if not higher:
+            data.reverse()
+        return data, fixed
+
+    def _dispersy_claim_sync_bloom_filter_modulo(self, request_cache):
+        """community.py:908-933: a filter over the residue class (global_time + offset) % modulo == 0."""
+        syncable = self._syncable_meta_ids()
+        if not syncable:
+            return self._empty_claim(self.acceptable_global_time)
+        bloom = self._new_claim_filter()
+        capacity = bloom.get_capacity(self.dispersy_sync_bloom_filter_error_rate)
+        st = self._store
+        live = [st.live_rows(m) for m in syncable]
+        live = np.concatenate(live) if live else np.zeros(0, dtype=np.int64)
+        self._nrsyncpackets = len(live)
+        modulo = int(ceil(self._nrsyncpackets / float(capacity)))
+        if modulo > 1:
+            offset = self._rand.randint(0, modulo - 1)
+            g = st.global_time[live]
+            live = live[(g + np.uint64(offset)) % np.uint64(modulo) == 0]
+        else:
+            offset, modulo = 0, 1
+        bloom.add_store_rows(st, live)
+        return (1, self.acceptable_global_time, modulo, offset, bloom)
+
+    # ----------------------------------------------------------------------------------- responder side
+    def _meta_time_low(self, meta, time_low, include_inactive):
+        # community.py:2800-2808
+        if include_inactive or not isinstance(meta.distribution.pruning, GlobalTimePruning):
+            return time_low
+        return min(max(time_low, self.global_time - meta.distribution.pruning.inactive_threshold + 1), MAX_GT)
+
+    def _select_rows(self, time_low, time_high, offset, modulo, include_inactive, shuffle):
+        """Store rows one request selects, in send order (the UNION ALL query of community.py:2764-2797)."""
+        st = self._store
+        out = []
+        for meta in self._served_metas():
+            seg = st.live_rows(meta.database_id)
+            g = st.global_time[seg]
+            lo = self._meta_time_low(meta, time_low, include_inactive)
+            a = int(np.searchsorted(g, lo, side="left")) if lo <= MAX_GT else len(seg)
+            b = int(np.searchsorted(g, time_high, side="right"))
+            part = seg[a:b] if a < b else seg[:0]
+            if modulo > 1 and len(part):
+                part = part[(st.global_time[part] + np.uint64(offset)) % np.uint64(modulo) == 0]
+            direction = meta.distribution.synchronization_direction
+            if direction == "DESC":
+                part = part[::-1]
+            elif direction == "RANDOM":
+                part = shuffle(part)
+            out.append(part)
+        return np.concatenate(out) if out else np.zeros(0, dtype=np.int64)
+
+    def _get_packets_for_bloomfilters(self, requests, include_inactive=True):
+        """community.py:2746-2811: yields (message, generator of (packet,)) per request
+        (message, time_low, time_high, offset, modulo), in the reference's send order."""
+        assert isinstance(requests, list)
+        assert all(len(request) == 5 for request in requests)
+        perm = lambda rows: rows[np.random.Generator(np.random.PCG64(self._random.getrandbits(64))).permutation(len(rows))]  # noqa: E731
+        for message, time_low, time_high, offset, modulo in requests:
+            rows = self._select_rows(time_low, time_high, offset, modulo, include_inactive, perm)
+            yield message, ((self._store.packet(int(r)),) for r in rows)
+
+    def respond(self, requests, include_inactive=False, byte_limit=None, random_seed=None):
+        """Batched responder (community.py:2531-2572): for each ClaimRequest (time_high already resolved), the store
+        rows the reference would send, in send order.  One call into the HIP library for the whole batch."""
+        byte_limit = self.dispersy_sync_response_limit if byte_limit is None else byte_limit
+        seed = self._random.getrandbits(64) if random_seed is None else random_seed
+        st = self._store
+        ctx = st.ctx
+        metas = self._served_metas()
+        R = len(requests)
+        reqs = (_native.Request * max(R, 1))()
+        filters, off = [], 0
+        for i, q in enumerate(requests):
+            bf = q.bloom_filter
+            raw = bf.bytes
+            raw += b"\x00" * ((-len(raw)) % 4)
+            r = reqs[i]
+            r.time_low, r.time_high = min(q.time_low, MAX_GT), min(q.time_high, MAX_GT)
+            r.modulo, r.offset = q.modulo, q.offset
+            r.filter_offset = off
+            r.m_bits, r.k = bf.size, bf.functions
+            r.hash_kind, r.chunk_bytes = _native.HASH_KINDS[bf.hash_name], bf.chunk_bytes
+            r.prefix_len = len(bf.prefix)
+            ctypes.memmove(r.prefix, bf.prefix, len(bf.prefix))
+            filters.append(raw)
+            off += len(raw)
+        mt = (_native.Meta * max(len(metas), 1))()
+        for j, m in enumerate(metas):
+            mt[j].meta_id = m.database_id
+            mt[j].direction = _native.DIRECTIONS[m.distribution.synchronization_direction]
+            pr = m.distribution.pruning
+            mt[j].has_pruning = 1 if isinstance(pr, GlobalTimePruning) else 0
+            mt[j].inactive_threshold = pr.inactive_threshold if isinstance(pr, GlobalTimePruning) else 0
+        blob = b"".join(filters)
+        out_off = np.zeros(R + 1, dtype=np.uint64)
+        cap = 1 << 16
+        while True:
+            out = np.zeros(cap, dtype=np.uint64)
+            rc = ctx.lib.dsy_sync_respond(ctx.handle, st.handle, reqs, R, blob, len(blob), mt, len(metas),
+                                          self.global_time, 1 if include_inactive else 0, int(byte_limit), seed,
+                                          out.ctypes.data, cap, out_off.ctypes.data)
+            if rc == _native.DSY_ECAPACITY and int(out_off[R]) > cap:
+                cap = int(out_off[R])
+                continue
+            _native.check(rc)
+            break
+        return [out[int(out_off[i]):int(out_off[i + 1])].astype(np.int64) for i in range(R)]
+
+    def on_introduction_request_sync(self, messages, include_inactive=False):
+        """The sync half of on_introduction_request (community.py:2531-2572) for a receive batch.
+
+        messages: list of (message, ClaimRequest).  Returns [(message, [packet bytes])] for the messages that get a
+        non-empty response, in input order."""
+        reqs = []
+        for _, q in messages:
+            time_high = q.time_high if q.time_high else self.global_time
+            reqs.append(q._replace(time_low=min(q.time_low, MAX_GT), time_high=min(time_high, MAX_GT)))
+        rows = self.respond(reqs, include_inactive=include_inactive)
+        out = []
+        for (message, _), rs in zip(messages, rows):
+            if len(rs):
+                out.append((message, self._store.packets(rs)))
+        return out

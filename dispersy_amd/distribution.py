@@ -1,0 +1,57 @@
+"""The parts of Dispersy's message model the sync hot path reads (distribution.py:68-242 of the reference):
+per meta-message priority, synchronisation direction and GlobalTimePruning thresholds."""
+
+
+class Pruning(object):
+    pass
+
+
+class NoPruning(Pruning):
+    """distribution.py:29-66 -- never inactive, never pruned."""
+
+
+class GlobalTimePruning(Pruning):
+    """distribution.py:68-114: active while community_gt - gt < inactive, pruned from community_gt - gt >= pruned."""
+
+    def __init__(self, inactive, pruned):
+        assert isinstance(inactive, int), type(inactive)
+        assert isinstance(pruned, int), type(pruned)
+        assert 0 < inactive < pruned, [inactive, pruned]
+        self.inactive_threshold = inactive
+        self.prune_threshold = pruned
+
+
+class SyncDistribution(object):
+    """distribution.py:142-242 (the Full/Last variants differ only in storage policy, not in sync selection)."""
+
+    def __init__(self, synchronization_direction="ASC", priority=127, pruning=None):
+        assert synchronization_direction in ("ASC", "DESC", "RANDOM"), synchronization_direction
+        assert isinstance(priority, int) and 0 <= priority <= 255, priority
+        self.synchronization_direction = synchronization_direction
+        self.priority = priority
+        self.pruning = pruning if pruning is not None else NoPruning()
+
+    @property
+    def synchronization_direction_value(self):
+        return {"ASC": 1, "DESC": -1, "RANDOM": 0}[self.synchronization_direction]
+
+
+FullSyncDistribution = SyncDistribution
+LastSyncDistribution = SyncDistribution
+
+
+class DirectDistribution(object):
+    """Messages that are never synced by bloom filters (distribution.py:316-325)."""
+    priority = 0
+
+
+class MetaMessage(object):
+    """The subset of a Message meta the sync path needs: name, database id (sync.meta_message) and distribution."""
+
+    def __init__(self, name, database_id, distribution):
+        self.name, self.database_id, self.distribution = name, database_id, distribution
+
+    @property
+    def syncable(self):
+        # community.py:767, :2790-2794: SyncDistribution with priority > 32
+        return isinstance(self.distribution, SyncDistribution) and self.distribution.priority > 32

@@ -1,0 +1,121 @@
+"""`SyncStore`: the packed HBM export of Dispersy's `sync` table (dispersydatabase.py:53-64).
+
+Rows are kept in the order of the reference's `sync_meta_message_undone_global_time_index`
+(meta_message, global_time, rowid) -- the order SQLite walks when it serves a sync range -- as columns:
+
+    blob        u8[sum L]   packets back to back        offsets   u64[N+1]
+    global_time u64[N]      meta u32[N]                 undone    u8[N]      rowid  i64[N]
+
+The device copy (dsy_store_upload) holds blob/offsets plus a live-row index (undone == 0) with per-meta
+segments; the host copy of the small columns serves the claim-side range selection
+(community.py:881-933) and maps responder output rows back to packets.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native
+
+
+class SyncStore(object):
+    def __init__(self, blob, offsets, global_time, meta, undone=None, rowid=None, ctx=None):
+        self.offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        self.n = len(self.offsets) - 1
+        self.blob = blob if isinstance(blob, (bytes, bytearray, memoryview, np.ndarray)) else bytes(blob)
+        self.global_time = np.ascontiguousarray(global_time, dtype=np.uint64)
+        self.meta = np.ascontiguousarray(meta, dtype=np.uint32)
+        self.undone = (np.zeros(self.n, dtype=np.uint8) if undone is None
+                       else np.ascontiguousarray(undone, dtype=np.uint8))
+        self.rowid = (np.arange(1, self.n + 1, dtype=np.int64) if rowid is None
+                      else np.ascontiguousarray(rowid, dtype=np.int64))
+        assert len(self.global_time) == len(self.meta) == len(self.undone) == len(self.rowid) == self.n
+        if self.n > 1:
+            m, g = self.meta, self.global_time
+            bad = (m[1:] < m[:-1]) | ((m[1:] == m[:-1]) & (g[1:] < g[:-1]))
+            if bad.any():
+                raise ValueError("SyncStore rows must be sorted by (meta_message, global_time, rowid)")
+        self._ctx = ctx
+        self._handle = None
+        self._row_of_id = None
+        # live (undone == 0) rows per meta, in global_time order: the claim side's index range scans
+        live = np.flatnonzero(self.undone == 0)
+        self._live = {}
+        if len(live):
+            lm = self.meta[live]
+            cuts = np.flatnonzero(lm[1:] != lm[:-1]) + 1
+            for seg in np.split(live, cuts):
+                self._live[int(self.meta[seg[0]])] = seg
+        self._empty = np.zeros(0, dtype=np.int64)
+
+    # ------------------------------------------------------------------------------------ constructors
+    @classmethod
+    def from_rows(cls, rows, ctx=None):
+        """rows: iterable of (rowid, global_time, meta_message, undone, packet)."""
+        rows = sorted(rows, key=lambda r: (r[2], r[1], r[0]))
+        n = len(rows)
+        offsets = np.zeros(n + 1, dtype=np.uint64)
+        if n:
+            np.cumsum([len(r[4]) for r in rows], out=offsets[1:])
+        return cls(b"".join(bytes(r[4]) for r in rows), offsets, [r[1] for r in rows], [r[2] for r in rows],
+                   [r[3] for r in rows], [r[0] for r in rows], ctx=ctx)
+
+    @classmethod
+    def from_sqlite(cls, conn, community=None, ctx=None):
+        """Export a Dispersy database's `sync` table (optionally one community) in index order."""
+        sql = "SELECT id, global_time, meta_message, undone, packet FROM sync"
+        args = ()
+        if community is not None:
+            sql += " WHERE community = ?"
+            args = (community,)
+        sql += " ORDER BY meta_message, global_time, id"
+        return cls.from_rows([(i, g, m, u, bytes(p)) for i, g, m, u, p in conn.execute(sql, args)], ctx=ctx)
+
+    # --------------------------------------------------------------------------------------- accessors
+    def packet(self, i):
+        a, b = int(self.offsets[i]), int(self.offsets[i + 1])
+        return bytes(self.blob[a:b])
+
+    def packets(self, rows):
+        return [self.packet(int(i)) for i in rows]
+
+    def length(self, i):
+        return int(self.offsets[i + 1] - self.offsets[i])
+
+    def row_of_id(self, rowid):
+        if self._row_of_id is None:
+            self._row_of_id = {int(r): i for i, r in enumerate(self.rowid)}
+        return self._row_of_id[int(rowid)]
+
+    def live_rows(self, meta_id):
+        """Store rows of one meta with undone == 0, in (global_time, rowid) order."""
+        return self._live.get(int(meta_id), self._empty)
+
+    def count_live(self, meta_ids):
+        return int(sum(len(self.live_rows(m)) for m in meta_ids))
+
+    # ------------------------------------------------------------------------------------------ device
+    @property
+    def ctx(self):
+        if self._ctx is None:
+            self._ctx = _native.default_context()
+        return self._ctx
+
+    @property
+    def handle(self):
+        """dsy_store* on the device (uploaded on first use)."""
+        if self._handle is None:
+            ctx = self.ctx
+            blob = self.blob if isinstance(self.blob, bytes) else bytes(self.blob)
+            h = ctypes.c_void_p()
+            _native.check(ctx.lib.dsy_store_upload(ctx.handle, blob, len(blob), self.offsets.ctypes.data, self.n,
+                                                   self.global_time.ctypes.data, self.meta.ctypes.data,
+                                                   self.undone.ctypes.data, ctypes.byref(h)))
+            self._handle = h
+        return self._handle
+
+    def close(self):
+        if self._handle is not None and self._ctx is not None and self._ctx.handle:
+            self._ctx.lib.dsy_store_free(self._handle)
+        self._handle = None
+
+    __del__ = close

@@ -1,0 +1,82 @@
+"""The batched HIP responder against the CPU oracle (sqlite3 + hashlib restatement) at sizes the reference
+golden vectors do not reach: multi-window claims, enumerate-mode selection, heavy global-time skew (one global
+time shared by thousands of rows), undone rows, pruning metas, every direction and mixed hash families."""
+import sqlite3
+
+import numpy as np
+import pytest
+
+from dispersy_amd import BloomFilter
+from dispersy_amd.community import ClaimRequest, SyncCommunity
+from dispersy_amd.distribution import GlobalTimePruning, MetaMessage, SyncDistribution
+from dispersy_amd.store import SyncStore
+from golden_util import SYNC_SCHEMA
+from oracle import sync_ref
+from oracle.bloom_ref import OracleBloom
+
+pytestmark = pytest.mark.gpu
+
+METAS = [("a", 1, "ASC", 128, None), ("d", 2, "DESC", 200, None), ("p", 3, "ASC", 150, (40, 80)),
+         ("n", 4, "ASC", 20, None)]
+
+
+def build(seed, n, gt_max, skew):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    meta = rng.choice([1, 2, 3, 4], size=n, p=[0.5, 0.25, 0.2, 0.05])
+    if skew:
+        gt = np.minimum(rng.zipf(1.1, size=n), gt_max)
+    else:
+        gt = rng.integers(1, gt_max + 1, size=n)
+    undone = (rng.random(n) < 0.03).astype(np.uint8)
+    lengths = rng.integers(20, 400, size=n)
+    rows = []
+    for i in range(n):
+        packet = i.to_bytes(4, "big") + rng.bytes(int(lengths[i]) - 4)
+        rows.append((i + 1, int(gt[i]), int(meta[i]), int(undone[i]), packet))
+    conn = sqlite3.connect(":memory:")
+    conn.executescript(SYNC_SCHEMA)
+    conn.executemany("INSERT INTO sync(id, community, member, global_time, meta_message, undone, packet, sequence) "
+                     "VALUES (?, 1, ?, ?, ?, ?, ?, 0)", [(r[0], r[0], r[1], r[2], r[3], r[4]) for r in rows])
+    return rows, conn
+
+
+def metas():
+    return [MetaMessage(n, i, SyncDistribution(d, p, GlobalTimePruning(*pr) if pr else None)) for n, i, d, p, pr in METAS]
+
+
+def oracle_metas():
+    return [dict(name=n, id=i, direction=d, priority=p, pruning=pr) for n, i, d, p, pr in METAS]
+
+
+@pytest.mark.parametrize("skew", [False, True])
+def test_respond_vs_oracle(skew):
+    rows, conn = build(11 + skew, 60_000, 200_000 if not skew else 5_000, skew)
+    store = SyncStore.from_rows(rows)
+    gt_now = 200_100 if not skew else 5_050
+    com = SyncCommunity(store, metas(), global_time=gt_now)
+    rng = np.random.Generator(np.random.PCG64(5 + skew))
+    packets = {r[0]: r[4] for r in rows}
+    reqs, oracle_blooms = [], []
+    shapes = [(10160, 0.01), (4096, 0.001), (1 << 15, 0.01), (1 << 16, 0.0001)]
+    for q in range(96):
+        modulo = int(rng.choice([1, 1, 3, 17, 997, 4093]))
+        offset = int(rng.integers(0, modulo))
+        lo = int(rng.integers(1, gt_now // 2))
+        hi = int(rng.integers(lo, gt_now + 10))
+        if q % 8 == 0:
+            lo, hi = 1, gt_now  # wide claims: many windows when the budget is large
+        m, f = shapes[q % len(shapes)]
+        prefix = bytes([int(rng.integers(0, 256))]) if q % 5 else bytes(rng.integers(0, 256, size=int(rng.integers(0, 90)), dtype=np.uint8))
+        bf, ob = BloomFilter(m, f, prefix), OracleBloom.from_m_f(m, f, prefix)
+        known = [packets[r[0]] for r in rows if rng.random() < (0.995 if q % 8 == 0 else 0.8)]
+        bf.add_keys(known)
+        ob.add_keys(known)
+        assert bf.bytes == ob.to_bytes()
+        reqs.append(ClaimRequest(lo, hi, modulo, offset, bf))
+        oracle_blooms.append(ob)
+    for include_inactive, limit in ((False, 5120), (True, 1 << 40), (False, 1)):
+        got = com.respond(reqs, include_inactive=include_inactive, byte_limit=limit)
+        for q, ob, g in zip(reqs, oracle_blooms, got):
+            want = sync_ref.respond_lists(conn, oracle_metas(), (q.time_low, q.time_high, q.offset, q.modulo), ob,
+                                          gt_now, limit, include_inactive)
+            assert store.rowid[g].tolist() == want, (q.time_low, q.time_high, q.modulo, q.offset, limit)
