@@ -196,8 +196,10 @@ int stage_keys(dsy_ctx* c, const uint8_t* blob, uint64_t blob_len, const uint64_
     int rc = check_offsets(offsets, n, blob_len);
     if (rc) return rc;
     void *b, *o;
-    if ((rc = ws_get(c, "keys_blob", blob_len + DSY_BLOB_GUARD, &b))) return rc;
+    if ((rc = ws_get(c, "keys_blob", blob_len + 2 * DSY_BLOB_GUARD, &b))) return rc;
     if ((rc = ws_get(c, "keys_off", (n + 1) * 8, &o))) return rc;
+    HIP_TRY(hipMemsetAsync(b, 0, DSY_BLOB_GUARD, c->stream));
+    b = (uint8_t*)b + DSY_BLOB_GUARD;  // the kernels may read a few bytes before the first key and a block past the last
     if (blob_len) HIP_TRY(hipMemcpyAsync(b, blob, blob_len, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemsetAsync((uint8_t*)b + blob_len, 0, DSY_BLOB_GUARD, c->stream));
     HIP_TRY(hipMemcpyAsync(o, offsets, (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
@@ -495,8 +497,10 @@ int dsy_store_upload(dsy_ctx* c, const uint8_t* blob, uint64_t blob_len, const u
     bool identity;
     if ((rc = store_index(s, offsets, global_time, meta, undone, &lg, &lr, &identity))) { delete s; return rc; }
     void *pb, *po;
-    if (hipMalloc(&pb, blob_len + DSY_BLOB_GUARD) != hipSuccess) { delete s; return fail(DSY_ENOMEM, "store blob alloc (%llu B)", (unsigned long long)blob_len); }
+    if (hipMalloc(&pb, blob_len + 2 * DSY_BLOB_GUARD) != hipSuccess) { delete s; return fail(DSY_ENOMEM, "store blob alloc (%llu B)", (unsigned long long)blob_len); }
     s->owned.push_back(pb);
+    HIP_TRY(hipMemsetAsync(pb, 0, DSY_BLOB_GUARD, c->stream));
+    pb = (uint8_t*)pb + DSY_BLOB_GUARD;
     if (hipMalloc(&po, (n + 1) * 8) != hipSuccess) { dsy_store_free(s); return fail(DSY_ENOMEM, "store offsets alloc"); }
     s->owned.push_back(po);
     if (blob_len) HIP_TRY(hipMemcpyAsync(pb, blob, blob_len, hipMemcpyHostToDevice, c->stream));
@@ -626,6 +630,8 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     if ((rc = ws_get(c, "upper", std::max<size_t>(R, 1) * 8, &d_upper))) return rc;
     if ((rc = ws_get(c, "pairs", std::max<size_t>((size_t)R * W, 1) * 8, &d_pairs))) return rc;
     if ((rc = ws_get(c, "miss", std::max<size_t>((size_t)R * W, 1), &d_miss))) return rc;
+    void* d_perm;
+    if ((rc = ws_get(c, "perm", std::max<size_t>((size_t)R * W, 1) * 4, &d_perm))) return rc;
     if ((rc = ws_get(c, "flags", 64, &d_flags))) return rc;
     if ((rc = ws_get(c, "total", 64, &d_total))) return rc;
     if ((rc = ws_get(c, "lists", std::max<size_t>(R, 1) * 4, &d_lists))) return rc;
@@ -664,6 +670,7 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     L.upper = (uint64_t*)d_upper;
     L.pair_row = (uint64_t*)d_pairs;
     L.miss = (uint8_t*)d_miss;
+    L.perm = (uint32_t*)d_perm;
     L.flags = (uint32_t*)d_flags;
     L.total_pairs = (uint64_t*)d_total;
     L.total_blocks = (uint64_t*)d_total + 1;

@@ -97,6 +97,7 @@ struct RespondLaunch {
     ReqState* state;          // device [R]
     uint64_t* upper;          // device [R]: upper bound of selected rows per claim
     uint64_t* pair_row;       // device [R*W]
+    uint32_t* perm;           // device [R*W]: per-claim hashing order (window slots sorted by block count)
     uint8_t* miss;            // device [R*W]
     uint64_t* out;            // device [sum cap]
     uint32_t* flags;          // device [4]: [0] any claim still active

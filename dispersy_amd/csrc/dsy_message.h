@@ -81,8 +81,9 @@ __device__ __forceinline__ void message_block(const KeyView& kv, uint32_t b, uin
     }
 }
 
+// Generic path: any prefix length (0..255); boundary blocks are assembled word by word.
 template <class H>
-__device__ __forceinline__ void hash_key(const KeyView& kv, H& st) {
+__device__ __forceinline__ void hash_key_generic(const KeyView& kv, H& st) {
     st.init();
     const uint32_t nb = n_blocks(kv.plen + kv.len, H::block_bytes, H::len_bytes);
     uint32_t w[H::words];
@@ -90,6 +91,189 @@ __device__ __forceinline__ void hash_key(const KeyView& kv, H& st) {
         message_block<H>(kv, b, nb, w);
         st.compress(w);
     }
+}
+
+// Fast path for prefixes of 0..3 bytes (the wire carries exactly one, conversion.py:725,769): every block is
+// four (eight) unaligned 16-byte loads of the key; block 0 is shifted right by the prefix length with
+// v_alignbyte and the prefix OR-ed in; the final block(s) are masked in registers (0x80 terminator, zeros,
+// bit length).  Loads of block b+1 are issued before block b is compressed (one block of software prefetch).
+// Reads may run up to block_bytes-1 bytes past the key: the blob carries DSY_BLOB_GUARD readable bytes.
+template <class H>
+__device__ __forceinline__ void hash_key_short_prefix(const KeyView& kv, H& st) {
+    constexpr int BLK = H::block_bytes, NW = H::words;
+    const uint32_t r = kv.plen;
+    const uint32_t total = r + kv.len;
+    const uint32_t nb = n_blocks(total, BLK, H::len_bytes);
+    uint32_t preword = 0;
+    for (uint32_t j = 0; j < r; ++j) preword |= (uint32_t)kv.pre[j] << (8 * j);
+    auto load = [&](uint32_t b, uint32_t* w) {
+        const bool has = b == 0 ? kv.len > 0 : b * BLK - r < kv.len;
+        const uint8_t* src = b == 0 ? kv.key : kv.key + (b * BLK - r);
+        if (has) {
+#pragma unroll
+            for (int q = 0; q < BLK / 16; ++q) {
+                const uint4 v = load_u128_unaligned(src + 16 * q);
+                w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < NW; ++i) w[i] = 0;
+        }
+    };
+    st.init();
+    uint32_t nxt[NW];
+    load(0, nxt);
+    for (uint32_t b = 0; b < nb; ++b) {
+        uint32_t w[NW];
+#pragma unroll
+        for (int i = 0; i < NW; ++i) w[i] = nxt[i];
+        if (b + 1 < nb) load(b + 1, nxt);
+        const uint32_t o0 = b * BLK;
+        if (b == 0 && r) {
+#pragma unroll
+            for (int i = NW - 1; i >= 1; --i) w[i] = __builtin_amdgcn_alignbyte(w[i], w[i - 1], 4 - r);
+            w[0] = (w[0] << (8 * r)) | preword;
+        }
+        if (o0 + BLK > total) {
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+                const int rel = (int)total - (int)o0 - 4 * i;
+                if (rel <= 0) w[i] = rel == 0 ? 0x80u : 0u;
+                else if (rel < 4) w[i] = (w[i] & ((1u << (8 * rel)) - 1u)) | (0x80u << (8 * rel));
+            }
+        }
+        if (H::big_endian) {
+#pragma unroll
+            for (int i = 0; i < NW; ++i) w[i] = bswap32(w[i]);
+        }
+        if (b + 1 == nb) {
+            const uint64_t bits = (uint64_t)total * 8u;
+            if (H::big_endian) {
+                w[NW - 2] = (uint32_t)(bits >> 32);
+                w[NW - 1] = (uint32_t)bits;
+                if (NW == 32) { w[28] = 0; w[29] = 0; }
+            } else {
+                w[14] = (uint32_t)bits;
+                w[15] = (uint32_t)(bits >> 32);
+            }
+        }
+        st.compress(w);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// LDS-DMA staged hashing for 64-byte-block hashes (MD5 / SHA-1 / SHA-256), one key per lane, called by ALL 64
+// lanes of a wave together (wave-uniform control flow; idle lanes pass a zero-length key at a readable address).
+//
+// Each stage copies the next S*64 bytes of all 64 keys into LDS with 4*S `global_load_lds_dwordx4` wave
+// instructions; every instruction moves 64/(4S) keys x S*64 contiguous bytes, so the memory system sees whole
+// 128-byte pieces instead of 64 scattered 16-byte ones.  Within a key's LDS row the 16-byte chunks are rotated by
+// (key >> SH) so the lanes' ds_read_b128 of "chunk c of my key" hit 16 distinct 4-bank groups.  NB buffers keep
+// NB-1 stages in flight (counted vmcnt).  Requires every lane's prefix to be <= 3 bytes and DSY_BLOB_GUARD
+// readable bytes before the first and after the last key (block 0 is fetched from key - plen).
+__device__ __forceinline__ void wait_vmcnt(int k) {
+    // s_waitcnt vmcnt(k), lgkm/exp counters untouched (immediates must be compile-time constants)
+    switch (k) {
+        case 0: __builtin_amdgcn_s_waitcnt(0x0f70); break;
+        case 8: __builtin_amdgcn_s_waitcnt(0x0f78); break;
+        case 16: __builtin_amdgcn_s_waitcnt(0x4f70); break;
+        default: __builtin_amdgcn_s_waitcnt(0x0f70); break;
+    }
+}
+
+template <int S, int NB>
+struct DmaGeometry {
+    static constexpr int kChunks = 4 * S;          // 16-byte chunks per key per stage
+    static constexpr int kKeysPerInst = 64 / kChunks;
+    static constexpr int kInsts = 4 * S;           // wave instructions per stage (64 keys * S*64 B / 1 KiB)
+    static constexpr int kShift = S == 1 ? 2 : S == 2 ? 1 : 0;
+    static constexpr int kStageBytes = S * 64 * 64;
+    static constexpr int kWaveBytes = NB * kStageBytes;
+};
+
+template <class H, int S = 2, int NB = 2>
+__device__ __forceinline__ void hash_key_dma(const KeyView& kv, H& st, uint8_t* lds_wave) {
+    static_assert(H::block_bytes == 64, "LDS-DMA staging is for 64-byte blocks");
+    using G = DmaGeometry<S, NB>;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t r = kv.plen;
+    const uint32_t total = r + kv.len;
+    const uint32_t nb = n_blocks(total, 64, H::len_bytes);
+    uint32_t nbmax = nb;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, d, 64));
+    const uint32_t nst = (nbmax + S - 1) / S;
+    uint32_t preword = 0;
+    for (uint32_t j = 0; j < r; ++j) preword |= (uint32_t)kv.pre[j] << (8 * j);
+    const uint64_t base = (uint64_t)(uintptr_t)kv.key - r;  // window of block b starts at base + 64 b
+    auto issue = [&](uint32_t s) {
+        uint8_t* buf = lds_wave + (s % NB) * G::kStageBytes;
+#pragma unroll
+        for (int i = 0; i < G::kInsts; ++i) {
+            const int p = G::kKeysPerInst * i + (int)(lane / G::kChunks);
+            const uint32_t blo = __shfl((int)(uint32_t)base, p, 64), bhi = __shfl((int)(uint32_t)(base >> 32), p, 64);
+            const uint32_t pend = __shfl((int)total, p, 64);
+            const uint32_t c = ((lane % G::kChunks) + ((uint32_t)p >> G::kShift)) % G::kChunks;
+            const uint64_t b64 = ((uint64_t)bhi << 32) | blo;
+            // always issue (the vmcnt accounting counts instructions); stages past the key re-read its start
+            const uint64_t a = (s * (S * 64) < pend) ? b64 + s * (S * 64) + 16 * c : b64;
+            __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)a,
+                                             (__attribute__((address_space(3))) void*)(buf + i * 1024), 16, 0, 0);
+        }
+    };
+    st.init();
+#pragma unroll
+    for (int k = 0; k < NB - 1; ++k)
+        if (k < (int)nst) issue(k);
+    for (uint32_t s = 0; s < nst; ++s) {
+        wait_vmcnt(((int)min(nst - 1, s + NB - 2) - (int)s) * G::kInsts);
+        __builtin_amdgcn_wave_barrier();
+        if (s + NB - 1 < nst) issue(s + NB - 1);
+        const uint8_t* cur = lds_wave + (s % NB) * G::kStageBytes;
+#pragma unroll
+        for (int bb = 0; bb < S; ++bb) {
+            const uint32_t b = S * s + bb;
+            uint32_t w[16];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t c = 4 * bb + q;
+                const uint32_t slot = (c - (lane >> G::kShift)) % G::kChunks;
+                const uint4 v = *(const uint4*)(cur + (lane / G::kKeysPerInst) * 1024 +
+                                                16 * (G::kChunks * (lane % G::kKeysPerInst) + slot));
+                w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+            }
+            if (b < nb) {
+                const uint32_t o0 = b * 64;
+                if (b == 0 && r) w[0] = (w[0] & ~((1u << (8 * r)) - 1u)) | preword;
+                if (o0 + 64 > total) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int rel = (int)total - (int)o0 - 4 * i;
+                        if (rel <= 0) w[i] = rel == 0 ? 0x80u : 0u;
+                        else if (rel < 4) w[i] = (w[i] & ((1u << (8 * rel)) - 1u)) | (0x80u << (8 * rel));
+                    }
+                }
+                if (H::big_endian) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) w[i] = bswap32(w[i]);
+                }
+                if (b + 1 == nb) {
+                    const uint64_t bits = (uint64_t)total * 8u;
+                    if (H::big_endian) { w[14] = (uint32_t)(bits >> 32); w[15] = (uint32_t)bits; }
+                    else { w[14] = (uint32_t)bits; w[15] = (uint32_t)(bits >> 32); }
+                }
+                st.compress(w);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this stage's reads retire before its buffer refills
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+template <class H>
+__device__ __forceinline__ void hash_key(const KeyView& kv, H& st) {
+    if (kv.plen < 4) hash_key_short_prefix<H>(kv, st);
+    else hash_key_generic<H>(kv, st);
 }
 
 // The i-th big-endian chunk of the digest (struct '>H' / '>L' / '>Q' codes, bloomfilter.py:135-140, :158-160).

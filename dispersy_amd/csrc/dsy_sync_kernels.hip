@@ -37,6 +37,29 @@ __device__ __forceinline__ uint64_t upper_bound_gt(const uint64_t* gt, uint64_t 
     return a;
 }
 
+// lower_bound over a sorted global-time column, interpolation first: each round probes gt[p-1], gt[p] at the
+// position the span's end values predict (one round-trip of independent loads), so dense or roughly uniform
+// global times resolve in one or two round-trips instead of ~log2(N) dependent loads; at most three rounds,
+// then plain binary search on what is left (skewed data stays O(log N)).
+__device__ __forceinline__ uint64_t lower_bound_interp(const uint64_t* gt, uint64_t lo, uint64_t hi, uint64_t v) {
+    // invariant: the answer lies in [lo, hi]
+#pragma unroll 1
+    for (int round = 0; round < 3 && hi - lo > 8; ++round) {
+        const uint64_t g0 = gt[lo], g1 = gt[hi - 1];
+        if (v <= g0) return lo;
+        if (v > g1) return hi;
+        // g0 < v <= g1: the answer is in [lo + 1, hi - 1]
+        const double f = (double)(v - g0) / (double)(g1 - g0);
+        uint64_t p = lo + 1 + (uint64_t)(f * (double)(hi - 2 - lo));
+        if (p > hi - 1) p = hi - 1;
+        const uint64_t gp = gt[p], gq = gt[p - 1];
+        if (gq < v && v <= gp) return p;
+        if (gp < v) lo = p + 1;
+        else hi = p - 1;
+    }
+    return lower_bound_gt(gt, lo, hi, v);
+}
+
 __device__ __forceinline__ uint32_t mix32(uint64_t x) {
     x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
     return (uint32_t)x;
@@ -78,8 +101,8 @@ __global__ void k_plan(RespondLaunch L) {
     p.dir = mt.dir;
     p.a = p.b = mt.seg_a;
     if (lo <= hi && mt.seg_a < mt.seg_b) {
-        p.a = lower_bound_gt(L.st.live_gt, mt.seg_a, mt.seg_b, lo);
-        p.b = upper_bound_gt(L.st.live_gt, p.a, mt.seg_b, hi);
+        p.a = lower_bound_interp(L.st.live_gt, mt.seg_a, mt.seg_b, lo);
+        p.b = hi >= kMaxGt ? mt.seg_b : lower_bound_interp(L.st.live_gt, p.a, mt.seg_b, hi + 1);
     }
     const uint64_t span = p.b - p.a;
     const uint64_t mod = q.modulo;
@@ -110,6 +133,8 @@ __global__ void k_plan(RespondLaunch L) {
 
 // ------------------------------------------------------------------------------------------- k_fill
 static constexpr int kFillThreads = 256;
+static constexpr uint32_t kSortBins = 1024;
+static constexpr uint32_t kMaxWindow = 4096;
 
 __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* lds, uint64_t* total) {
     // lds: kFillThreads + 1 words.  Simple Hillis-Steele over LDS (one per window step; not the hot loop).
@@ -159,8 +184,11 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
                 y = match ? x + 1 : x;
             } else {
                 const uint64_t g = p.g0 + cand * mod;
-                x = lower_bound_gt(L.st.live_gt, p.a, p.b, g);
-                y = upper_bound_gt(L.st.live_gt, x, p.b, g);
+                x = lower_bound_interp(L.st.live_gt, p.a, p.b, g);
+                y = x;
+                if (x < p.b && L.st.live_gt[x] == g) {  // equal range: usually a single row
+                    y = (x + 1 < p.b && L.st.live_gt[x + 1] == g) ? upper_bound_gt(L.st.live_gt, x + 1, p.b, g) : x + 1;
+                }
             }
         }
         uint64_t cnt = y - x;
@@ -202,30 +230,71 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
         S->n_window = filled;
         if (j >= L.J) S->exhausted = 1;
     }
+    // Load balance: order this window's pairs by compression-block count (counting sort in LDS) so the 64
+    // lanes of a hashing wave run the same number of blocks.  perm[i] = window slot hashed by lane-slot i; the
+    // send order (slot order) is untouched.
+    __shared__ uint32_t hist[kSortBins];
+    __shared__ uint16_t keyb[kMaxWindow];
+    const uint32_t blk = q.hash_kind >= DSY_SHA384 ? 128u : 64u, lenb = q.hash_kind >= DSY_SHA384 ? 16u : 8u;
+    for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads) hist[i] = 0;
+    __syncthreads();
+    for (uint64_t t = threadIdx.x; t < filled; t += kFillThreads) {
+        const uint64_t row = out[t];
+        const uint32_t len = (uint32_t)(L.st.offsets[row + 1] - L.st.offsets[row]);
+        const uint32_t nb = min(n_blocks(q.prefix_len + len, blk, lenb), (uint32_t)kSortBins - 1);
+        keyb[t] = (uint16_t)nb;
+        atomicAdd(&hist[nb], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // exclusive scan of kSortBins counters (cheap next to the fill itself)
+        uint32_t run = 0;
+        for (uint32_t i = 0; i < kSortBins; ++i) {
+            const uint32_t h = hist[i];
+            hist[i] = run;
+            run += h;
+        }
+    }
+    __syncthreads();
+    uint32_t* perm = L.perm + (uint64_t)r * W;
+    for (uint64_t t = threadIdx.x; t < filled; t += kFillThreads) perm[atomicAdd(&hist[keyb[t]], 1u)] = (uint32_t)t;
 }
 
 // -------------------------------------------------------------------------------------- k_pair_test
-template <class H, int CHUNK>
+template <class H, int CHUNK, bool DMA>
 __global__ void __launch_bounds__(256) k_pair_test(RespondLaunch L, const uint32_t* __restrict__ req_list,
                                                    uint32_t n_list) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dma_lds[];
     const uint64_t W = L.window;
     const uint64_t waves_per_req = W / 64;
     const uint64_t total_waves = (uint64_t)n_list * waves_per_req;
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t wave0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    uint8_t* my_lds = dma_lds + (threadIdx.x >> 6) * DmaGeometry<2, 2>::kWaveBytes;
     for (uint64_t wv = wave0; wv < total_waves; wv += wstride) {
         const uint32_t r = req_list[wv / waves_per_req];
-        const uint64_t t = (wv % waves_per_req) * 64 + lane;
+        const uint64_t i0 = (wv % waves_per_req) * 64;
         const uint64_t n = L.state[r].n_window;
-        if ((wv % waves_per_req) * 64 >= n) continue;  // whole wave past this claim's window (wave-uniform)
-        if (t >= n) continue;
+        if (i0 >= n) continue;  // wave-uniform: past this claim's window
+        const uint64_t i = i0 + lane;
+        const bool active = i < n;
         const dsy_request& q = L.reqs[r];
-        const uint64_t row = L.pair_row[(uint64_t)r * W + t];
-        const uint64_t a = L.st.offsets[row], e = L.st.offsets[row + 1];
-        KeyView kv{L.st.blob + a, (uint32_t)(e - a), q.prefix, q.prefix_len};
+        uint32_t t = 0;
+        KeyView kv{L.st.blob, 0u, q.prefix, q.prefix_len};  // idle lanes hash an empty key
+        if (active) {
+            t = L.perm[(uint64_t)r * W + i];
+            const uint64_t row = L.pair_row[(uint64_t)r * W + t];
+            const uint64_t a = L.st.offsets[row], e = L.st.offsets[row + 1];
+            kv.key = L.st.blob + a;
+            kv.len = (uint32_t)(e - a);
+        }
         H st;
-        hash_key<H>(kv, st);
+        if constexpr (DMA) {
+            if (q.prefix_len < 4) hash_key_dma<H, 2, 2>(kv, st, my_lds);
+            else hash_key<H>(kv, st);
+        } else {
+            hash_key<H>(kv, st);
+        }
         const uint32_t* filt = (const uint32_t*)(L.filters + q.filter_offset);
         const uint64_t m = q.m_bits;
         uint32_t ok = 1;
@@ -236,15 +305,16 @@ __global__ void __launch_bounds__(256) k_pair_test(RespondLaunch L, const uint32
                 ok &= (filt[pos >> 5] >> (pos & 31)) & 1u;
             }
         }
-        L.miss[(uint64_t)r * W + t] = (uint8_t)(ok ^ 1u);
+        if (active) L.miss[(uint64_t)r * W + t] = (uint8_t)(ok ^ 1u);
         if (L.total_blocks) {  // algorithmic work of this wave: compression blocks and packet bytes
-            unsigned long long nb = n_blocks(kv.plen + kv.len, H::block_bytes, H::len_bytes), by = kv.len;
+            unsigned long long nb = active ? n_blocks(kv.plen + kv.len, H::block_bytes, H::len_bytes) : 0;
+            unsigned long long by = active ? kv.len : 0;
 #pragma unroll
             for (int d = 32; d >= 1; d >>= 1) {
                 nb += __shfl_xor(nb, d, 64);
                 by += __shfl_xor(by, d, 64);
             }
-            if (lane == __builtin_ffsll(__ballot(1)) - 1) {
+            if (lane == 0) {
                 atomicAdd((unsigned long long*)&L.total_blocks[0], nb);
                 atomicAdd((unsigned long long*)&L.total_blocks[1], by);
             }
@@ -258,7 +328,11 @@ static hipError_t pair_test_family(const RespondLaunch& L, const uint32_t* list,
     uint64_t blocks = (waves + 3) / 4;
     if (blocks > 256 * 16) blocks = 256 * 16;
     if (blocks == 0) return hipSuccess;
-    hipLaunchKernelGGL((k_pair_test<H, CHUNK>), dim3((uint32_t)blocks), dim3(256), 0, L.stream, L, list, n_list);
+    // MD5 is load-bound: stage its blocks through LDS with DMA; the SHA families are compute-bound and keep the
+    // direct per-lane loads (higher occupancy)
+    constexpr bool dma = H::kind == DSY_MD5;
+    const size_t lds = dma ? 4 * DmaGeometry<2, 2>::kWaveBytes : 0;
+    hipLaunchKernelGGL((k_pair_test<H, CHUNK, dma>), dim3((uint32_t)blocks), dim3(256), lds, L.stream, L, list, n_list);
     return hipGetLastError();
 }
 

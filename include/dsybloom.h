@@ -128,8 +128,9 @@ int dsy_bloom_test(dsy_ctx* ctx, const dsy_bloom_params* p, const uint8_t* blob,
 int dsy_bloom_indices(dsy_ctx* ctx, const dsy_bloom_params* p, const uint8_t* blob, uint64_t blob_len,
                       const uint64_t* offsets, uint64_t n, uint64_t* out_idx);
 
-/* Device-pointer forms.  d_blob must stay readable for DSY_BLOB_GUARD bytes past offsets[n] (the kernels read
- * whole 64/128-byte blocks and mask); d_filter holds dsy_filter_words(m) words. */
+/* Device-pointer forms.  d_blob must stay readable for DSY_BLOB_GUARD bytes before offsets[0] and past
+ * offsets[n] (the kernels read whole 64/128-byte blocks and mask, and fetch block 0 from key - prefix_len);
+ * d_filter holds dsy_filter_words(m) words. */
 #define DSY_BLOB_GUARD 256
 int dsy_bloom_add_dev(dsy_ctx* ctx, const dsy_bloom_params* p, const uint8_t* d_blob, const uint64_t* d_offsets,
                       uint64_t n, uint32_t* d_filter);
@@ -143,7 +144,7 @@ int dsy_bloom_test_dev(dsy_ctx* ctx, const dsy_bloom_params* p, const uint8_t* d
 int dsy_store_upload(dsy_ctx* ctx, const uint8_t* blob, uint64_t blob_len, const uint64_t* offsets, uint64_t n,
                      const uint64_t* global_time, const uint32_t* meta, const uint8_t* undone, dsy_store** out);
 /* Same, over device buffers the caller keeps alive (no copy).  d_blob needs DSY_BLOB_GUARD readable bytes
- * past offsets[n]. */
+ * before offsets[0] and past offsets[n]. */
 int dsy_store_attach(dsy_ctx* ctx, const uint8_t* d_blob, uint64_t blob_len, const uint64_t* d_offsets, uint64_t n,
                      const uint64_t* d_global_time, const uint32_t* d_meta, const uint8_t* d_undone, dsy_store** out);
 int dsy_store_free(dsy_store* store);

@@ -171,3 +171,43 @@ def claim_modulo(conn, metas, bits, error_rate, acceptable, draws, bloom_cls):
             "SELECT packet FROM sync WHERE meta_message IN (%s) AND undone = 0" % ids)]
     bloom.add_keys(packets)
     return (1, acceptable, modulo, offset, bloom), nrsync
+
+
+# ------------------------------------------------------------------------ array form (bench cpu_baseline)
+def respond_arrays(packet_of, gt_by_meta, metas, request, bloom, global_time, byte_limit, include_inactive=False,
+                   counter=None):
+    """The responder over in-memory index columns instead of sqlite (used as the timed CPU baseline, where a
+    10-million-row sqlite table cannot be built in seconds).  Selection walks the same index range as
+    selected_rows() but evaluates the modulo predicate with numpy (faster than sqlite's per-row VM, so the baseline
+    is generous to the CPU); the not_filter/byte-limit loop is the reference's, lazily hashing only until the
+    budget is spent.
+
+    packet_of(row) -> bytes-like; gt_by_meta[meta_id] = (rows, gts) numpy arrays sorted by (global_time, row),
+    undone == 0 only.  counter: optional one-element list incremented per packet hashed."""
+    import numpy as np
+    time_low, time_high, offset, modulo = request
+
+    def gen():
+        for meta in ordered_metas(metas):
+            rows, gts = gt_by_meta.get(meta["id"], (np.zeros(0, np.int64), np.zeros(0, np.uint64)))
+            lo = meta_time_low(meta, time_low, global_time, include_inactive)
+            a = int(np.searchsorted(gts, lo, side="left"))
+            b = int(np.searchsorted(gts, time_high, side="right"))
+            sel = np.arange(a, b)
+            if modulo > 1 and len(sel):
+                sel = sel[(gts[a:b] + np.uint64(offset)) % np.uint64(modulo) == 0]
+            if meta["direction"] == "DESC":
+                sel = sel[::-1]
+            for i in sel.tolist():
+                if counter is not None:
+                    counter[0] += 1
+                r = int(rows[i])
+                yield (packet_of(r), r)
+
+    sent, budget = [], byte_limit
+    for packet, row in bloom.not_filter(gen()):
+        sent.append(row)
+        budget -= len(packet)
+        if budget <= 0:
+            break
+    return sent

@@ -1,0 +1,554 @@
+// hashbench.hip -- A/B microbenchmark of per-lane message loading strategies for the digest kernels.
+// Not part of the product; built and run by hand (see tools/README.md).  Each variant hashes the same packets
+// (one packet per lane, MD5 or SHA-1 of prefix || packet) and XORs the digest into an output word so nothing is
+// dead-code eliminated.  Variants interleave in one process (guide §5.4 rule 24).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <numeric>
+#include <random>
+#include <vector>
+
+#include "../dispersy_amd/csrc/dsy_message.h"
+
+using namespace dsy;
+
+#define CK(x)                                                                         \
+    do {                                                                              \
+        hipError_t e = (x);                                                           \
+        if (e != hipSuccess) {                                                        \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+            exit(1);                                                                  \
+        }                                                                             \
+    } while (0)
+
+static uint64_t g_checksum;
+enum Variant { kDirect = 0, kAlignedFake = 1, kNoLoad = 2, kAlignedFunnel = 3, kPrefetch = 4, kCoop = 5, kPure = 6, kDma = 7, kFast = 8 };
+
+// aligned 80-byte window + register funnel shift: correct for middle blocks
+__device__ __forceinline__ void load_block_funnel(const uint8_t* src, uint32_t* w) {
+    const uintptr_t a = (uintptr_t)src;
+    const uint4* base = (const uint4*)(a & ~(uintptr_t)15);
+    const uint32_t sh = (uint32_t)(a & 15);
+    uint32_t d[20];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        uint4 v = base[q];
+        d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+    }
+    const uint32_t dw = sh >> 2, by = (sh & 3) * 8;
+    uint32_t e[18];
+#pragma unroll
+    for (int i = 0; i < 18; ++i) e[i] = (dw & 2) ? d[i + 2] : d[i];
+    uint32_t f[17];
+#pragma unroll
+    for (int i = 0; i < 17; ++i) f[i] = (dw & 1) ? e[i + 1] : e[i];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = by ? __builtin_amdgcn_alignbyte(f[i + 1], f[i], sh & 3) : f[i];
+}
+
+template <class H, int V>
+__device__ __forceinline__ void block_variant(const KeyView& kv, uint32_t b, uint32_t nb, uint32_t* w) {
+    constexpr int BLK = H::block_bytes;
+    const uint32_t total = kv.plen + kv.len;
+    const uint32_t o0 = b * BLK;
+    const bool middle = o0 >= kv.plen && o0 + BLK <= total;
+    if (V == kDirect || !middle) {
+        message_block<H>(kv, b, nb, w);
+        return;
+    }
+    const uint8_t* src = kv.key + (o0 - kv.plen);
+    if (V == kAlignedFake) {
+        const uint4* p = (const uint4*)((uintptr_t)src & ~(uintptr_t)15);
+#pragma unroll
+        for (int q = 0; q < BLK / 16; ++q) {
+            uint4 v = p[q];
+            w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+        }
+    } else if (V == kNoLoad) {
+#pragma unroll
+        for (int i = 0; i < H::words; ++i) w[i] = (uint32_t)(uintptr_t)src * (i + 1);
+    } else {
+        load_block_funnel(src, w);
+    }
+    if (H::big_endian) {
+#pragma unroll
+        for (int i = 0; i < H::words; ++i) w[i] = bswap32(w[i]);
+    }
+}
+
+template <class H>
+__device__ __forceinline__ bool is_middle(const KeyView& kv, uint32_t b) {
+    const uint32_t o0 = b * H::block_bytes;
+    return o0 >= kv.plen && o0 + H::block_bytes <= kv.plen + kv.len;
+}
+
+// software-pipelined: the raw words of block b+1 are loaded before block b is compressed
+template <class H>
+__device__ __forceinline__ void hash_key_prefetch(const KeyView& kv, H& st) {
+    st.init();
+    const uint32_t nb = n_blocks(kv.plen + kv.len, H::block_bytes, H::len_bytes);
+    uint32_t nxt[H::words];
+    auto raw_load = [&](uint32_t b, uint32_t* w) {
+        const uint8_t* src = kv.key + (b * H::block_bytes - kv.plen);
+#pragma unroll
+        for (int q = 0; q < H::block_bytes / 16; ++q) {
+            uint4 v = load_u128_unaligned(src + 16 * q);
+            w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+        }
+    };
+    if (nb > 0 && is_middle<H>(kv, 0)) raw_load(0, nxt);
+    for (uint32_t b = 0; b < nb; ++b) {
+        uint32_t w[H::words];
+        const bool mid = is_middle<H>(kv, b);
+#pragma unroll
+        for (int i = 0; i < H::words; ++i) w[i] = nxt[i];
+        if (b + 1 < nb && is_middle<H>(kv, b + 1)) raw_load(b + 1, nxt);
+        if (mid) {
+            if (H::big_endian) {
+#pragma unroll
+                for (int i = 0; i < H::words; ++i) w[i] = bswap32(w[i]);
+            }
+        } else {
+            message_block<H>(kv, b, nb, w);
+        }
+        st.compress(w);
+    }
+}
+
+// cooperative wave load of one 64-byte block per lane: lane l fetches 16 B of lane (16*i + l/4)'s block in
+// instruction i, so 4 consecutive lanes read one packet's contiguous 64 bytes; staged through LDS (80-byte
+// lane stride: conflict-free ds_read_b128).  Global loads for block b+1 are issued before block b is hashed.
+template <class H>
+__device__ __forceinline__ void hash_key_coop(const KeyView& kv, H& st, uint32_t* lds) {
+    static_assert(H::block_bytes == 64, "coop path is for 64-byte blocks");
+    const uint32_t lane = threadIdx.x & 63;
+    st.init();
+    const uint32_t nb = n_blocks(kv.plen + kv.len, 64, H::len_bytes);
+    // wave-wide maximum block count (lanes are sorted by nb, so this is ~nb)
+    uint32_t nbmax = nb;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, d, 64));
+    uint4 pf[4];
+    auto issue = [&](uint32_t b) {
+        const bool mid = b < nb && is_middle<H>(kv, b);
+        const uint64_t a = (uint64_t)(uintptr_t)(kv.key + (b * 64 - kv.plen));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int j = 16 * i + (lane >> 2);
+            const uint32_t alo = __shfl((int)(uint32_t)a, j, 64), ahi = __shfl((int)(uint32_t)(a >> 32), j, 64);
+            const int mj = __shfl((int)mid, j, 64);
+            const uint8_t* src = (const uint8_t*)(uintptr_t)(((uint64_t)ahi << 32) | alo) + 16 * (lane & 3);
+            pf[i] = mj ? load_u128_unaligned(src) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    auto stage = [&]() {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int j = 16 * i + (lane >> 2);
+            *(uint4*)&lds[j * 20 + 4 * (lane & 3)] = pf[i];
+        }
+    };
+    issue(0);
+    for (uint32_t b = 0; b < nbmax; ++b) {
+        stage();
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+        uint32_t w[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            uint4 v = *(const uint4*)&lds[lane * 20 + 4 * q];
+            w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        if (b + 1 < nbmax) issue(b + 1);
+        if (b < nb) {
+            if (is_middle<H>(kv, b)) {
+                if (H::big_endian) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) w[i] = bswap32(w[i]);
+                }
+            } else {
+                message_block<H>(kv, b, nb, w);
+            }
+            st.compress(w);
+        }
+    }
+}
+
+// LDS-DMA staged: per stage, the wave copies the next 128 B of all 64 keys with 8 global_load_lds_dwordx4
+// (each instruction = 8 keys x 128 contiguous bytes), double-buffered; lanes read their own 2 blocks with
+// conflict-free ds_read_b128 (chunk slot (c - lane/2) & 7 within the key's 128-B row).
+template <class H>
+__device__ __forceinline__ void hash_key_dma(const KeyView& kv, H& st, uint8_t* buf0) {
+    static_assert(H::block_bytes == 64, "64-byte blocks");
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t r = kv.plen;  // <= 3
+    const uint32_t total = r + kv.len;
+    const uint32_t nb = n_blocks(total, 64, H::len_bytes);
+    uint32_t nbmax = nb;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, d, 64));
+    const uint32_t nst = (nbmax + 1) >> 1;
+    uint32_t preword = 0;
+    for (uint32_t j = 0; j < r; ++j) preword |= (uint32_t)kv.pre[j] << (8 * j);
+    const uint64_t base = (uint64_t)(uintptr_t)kv.key - r;
+    const uint32_t keyend = kv.len + r;  // bytes of window that hold prefix-slot + key
+    auto issue = [&](uint32_t s, uint8_t* buf) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int p = 8 * i + (lane >> 3);
+            const uint32_t blo = __shfl((int)(uint32_t)base, p, 64), bhi = __shfl((int)(uint32_t)(base >> 32), p, 64);
+            const uint32_t kend = __shfl((int)keyend, p, 64);
+            const uint32_t c = ((lane & 7) + (p >> 1)) & 7;
+            const uint8_t* src = (const uint8_t*)(uintptr_t)(((uint64_t)bhi << 32) | blo) + s * 128 + 16 * c;
+            if (s * 128 < kend)
+                __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(buf + i * 1024), 16, 0, 0);
+        }
+    };
+    st.init();
+    issue(0, buf0);
+    for (uint32_t s = 0; s < nst; ++s) {
+        uint8_t* cur = buf0 + (s & 1) * 8192;
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+        __builtin_amdgcn_wave_barrier();
+        if (s + 1 < nst) issue(s + 1, buf0 + ((s + 1) & 1) * 8192);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            const uint32_t b = 2 * s + bb;
+            uint32_t w[16];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t c = 4 * bb + q;
+                const uint32_t slot = (c - (lane >> 1)) & 7;
+                const uint4 v = *(const uint4*)(cur + (lane >> 3) * 1024 + 16 * (8 * (lane & 7) + slot));
+                w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+            }
+            if (b < nb) {
+                const uint32_t o0 = b * 64;
+                if (b == 0 && r) w[0] = (w[0] & ~((1u << (8 * r)) - 1u)) | preword;
+                if (o0 + 64 > total) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int rel = (int)total - (int)o0 - 4 * i;
+                        if (rel <= 0) w[i] = rel == 0 ? 0x80u : 0u;
+                        else if (rel < 4) w[i] = (w[i] & ((1u << (8 * rel)) - 1u)) | (0x80u << (8 * rel));
+                    }
+                }
+                if (H::big_endian) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) w[i] = bswap32(w[i]);
+                }
+                if (b + 1 == nb) {
+                    const uint64_t bits = (uint64_t)total * 8u;
+                    if (H::big_endian) { w[14] = (uint32_t)(bits >> 32); w[15] = (uint32_t)bits; }
+                    else { w[14] = (uint32_t)bits; w[15] = (uint32_t)(bits >> 32); }
+                }
+                st.compress(w);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): reads of `cur` done before it is re-filled
+    }
+}
+
+__device__ __forceinline__ void wait_vm(int k) {
+    // s_waitcnt vmcnt(k) for the few counts the DMA pipeline needs (immediates must be constants)
+    switch (k) {
+        case 0: __builtin_amdgcn_s_waitcnt(0x0f70); break;
+        case 4: __builtin_amdgcn_s_waitcnt(0x0f74); break;
+        case 8: __builtin_amdgcn_s_waitcnt(0x0f78); break;
+        case 12: __builtin_amdgcn_s_waitcnt(0x0f7c); break;
+        case 16: __builtin_amdgcn_s_waitcnt(0x4f70); break;
+        case 24: __builtin_amdgcn_s_waitcnt(0x4f78); break;
+        case 32: __builtin_amdgcn_s_waitcnt(0x8f70); break;
+        default: __builtin_amdgcn_s_waitcnt(0x0f70); break;
+    }
+}
+
+struct NullHash {
+    static constexpr int kind = 0, block_bytes = 64, len_bytes = 8, digest_bytes = 16, words = 16;
+    static constexpr bool big_endian = false;
+    uint32_t h[4];
+    __device__ __forceinline__ void init() { h[0] = h[1] = h[2] = h[3] = 0; }
+    __device__ __forceinline__ void compress(const uint32_t* m) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) h[i & 3] ^= m[i];
+    }
+    __device__ __forceinline__ uint32_t be_word(int i) const { return h[i]; }
+};
+
+template <class H, int S, int NB>
+__device__ __forceinline__ void hash_key_dma2(const KeyView& kv, H& st, uint8_t* buf0) {
+    constexpr int CS = 4 * S;          // 16-byte chunks per key per stage
+    constexpr int PPI = 64 / CS;       // keys per DMA instruction
+    constexpr int NI = 4 * S;          // DMA instructions per stage (64 keys * S * 64 B / 1 KiB)
+    constexpr int SH = S == 1 ? 2 : S == 2 ? 1 : 0;
+    constexpr int STAGE = S * 64 * 64; // bytes per stage buffer
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t r = kv.plen;
+    const uint32_t total = r + kv.len;
+    const uint32_t nb = n_blocks(total, 64, H::len_bytes);
+    uint32_t nbmax = nb;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, d, 64));
+    const uint32_t nst = (nbmax + S - 1) / S;
+    uint32_t preword = 0;
+    for (uint32_t j = 0; j < r; ++j) preword |= (uint32_t)kv.pre[j] << (8 * j);
+    const uint64_t base = (uint64_t)(uintptr_t)kv.key - r;
+    const uint32_t keyend = kv.len + r;
+    auto issue = [&](uint32_t s) {
+        uint8_t* buf = buf0 + (s % NB) * STAGE;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int p = PPI * i + lane / CS;
+            const uint32_t blo = __shfl((int)(uint32_t)base, p, 64), bhi = __shfl((int)(uint32_t)(base >> 32), p, 64);
+            const uint32_t kend = __shfl((int)keyend, p, 64);
+            const uint32_t c = ((lane % CS) + (p >> SH)) % CS;
+            const uint64_t b64 = ((uint64_t)bhi << 32) | blo;
+            const uint64_t a = (s * (S * 64) < kend) ? b64 + s * (S * 64) + 16 * c : b64;  // always issue
+            __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)a, (__attribute__((address_space(3))) void*)(buf + i * 1024), 16, 0, 0);
+        }
+    };
+    st.init();
+#pragma unroll
+    for (int k = 0; k < NB - 1; ++k)
+        if (k < (int)nst) issue(k);
+    for (uint32_t s = 0; s < nst; ++s) {
+        const int after = (int)min(nst - 1, s + NB - 2) - (int)s;
+        wait_vm(after * NI);
+        __builtin_amdgcn_wave_barrier();
+        if (s + NB - 1 < nst) issue(s + NB - 1);
+        const uint8_t* cur = buf0 + (s % NB) * STAGE;
+#pragma unroll
+        for (int bb = 0; bb < S; ++bb) {
+            const uint32_t b = S * s + bb;
+            uint32_t w[16];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t c = 4 * bb + q;
+                const uint32_t slot = (c - (lane >> SH)) % CS;
+                const uint4 v = *(const uint4*)(cur + (lane / PPI) * 1024 + 16 * (CS * (lane % PPI) + slot));
+                w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+            }
+            if (b < nb) {
+                const uint32_t o0 = b * 64;
+                if (b == 0 && r) w[0] = (w[0] & ~((1u << (8 * r)) - 1u)) | preword;
+                if (o0 + 64 > total) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int rel = (int)total - (int)o0 - 4 * i;
+                        if (rel <= 0) w[i] = rel == 0 ? 0x80u : 0u;
+                        else if (rel < 4) w[i] = (w[i] & ((1u << (8 * rel)) - 1u)) | (0x80u << (8 * rel));
+                    }
+                }
+                if (H::big_endian) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) w[i] = bswap32(w[i]);
+                }
+                if (b + 1 == nb) {
+                    const uint64_t bits = (uint64_t)total * 8u;
+                    if (H::big_endian) { w[14] = (uint32_t)(bits >> 32); w[15] = (uint32_t)bits; }
+                    else { w[14] = (uint32_t)bits; w[15] = (uint32_t)(bits >> 32); }
+                }
+                st.compress(w);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+template <class H, int S, int NB>
+__global__ void __launch_bounds__(64) k_hash_dma(const uint8_t* blob, const uint64_t* off, const uint32_t* order,
+                                                 uint32_t n, const uint8_t* pre, uint32_t plen, uint32_t* out) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+    const uint32_t key = order ? order[min(i, n - 1)] : min(i, n - 1);
+    const uint64_t a = off[key], e = off[key + 1];
+    KeyView kv{blob + a, (uint32_t)(e - a), pre, plen};
+    H st;
+    hash_key_dma2<H, S, NB>(kv, st, dyn);
+    uint32_t x = 0;
+#pragma unroll
+    for (int j = 0; j < H::digest_bytes / 4; ++j) x ^= st.be_word(j);
+    if (i < n) out[i] = x;
+}
+
+template <class H, int S, int NB>
+float run_dma(const uint8_t* blob, const uint64_t* off, const uint32_t* order, uint32_t n, const uint8_t* pre,
+              uint32_t plen, uint32_t* out, int reps) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    dim3 grid((n + 63) / 64);
+    const size_t dl = (size_t)NB * S * 4096;
+    hipLaunchKernelGGL((k_hash_dma<H, S, NB>), grid, dim3(64), dl, 0, blob, off, order, n, pre, plen, out);
+    CK(hipEventRecord(a));
+    for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((k_hash_dma<H, S, NB>), grid, dim3(64), dl, 0, blob, off, order, n, pre, plen, out);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    std::vector<uint32_t> h(n), ord(n), byk(n);
+    CK(hipMemcpy(h.data(), out, n * 4, hipMemcpyDeviceToHost));
+    if (order) {
+        CK(hipMemcpy(ord.data(), order, n * 4, hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < n; ++i) byk[ord[i]] = h[i];
+    } else byk = h;
+    uint64_t cs = 0;
+    for (uint32_t i = 0; i < n; ++i) cs = cs * 1000003u + byk[i];
+    g_checksum = cs;
+    return ms / reps;
+}
+
+template <class H, int V>
+__global__ void __launch_bounds__(256) k_hash(const uint8_t* blob, const uint64_t* off, const uint32_t* order,
+                                              uint32_t n, const uint8_t* pre, uint32_t plen, uint32_t* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t key = order ? order[i] : i;
+    const uint64_t a = off[key], e = off[key + 1];
+    KeyView kv{blob + a, (uint32_t)(e - a), pre, plen};
+    H st;
+    __shared__ uint32_t lds[4 * 64 * 20];
+    if (V == kPrefetch) {
+        hash_key_prefetch<H>(kv, st);
+    } else if (V == kDma) {
+        extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+        hash_key_dma<H>(kv, st, dyn + (threadIdx.x >> 6) * 16384);
+    } else if (V == kFast) {
+        hash_key<H>(kv, st);
+    } else if (V == kCoop) {
+        hash_key_coop<H>(kv, st, lds + (threadIdx.x >> 6) * 64 * 20);
+    } else if (V == kPure) {
+        st.init();
+        const uint32_t nb = n_blocks(kv.plen + kv.len, H::block_bytes, H::len_bytes);
+        uint32_t w[H::words];
+        for (uint32_t b = 0; b < nb; ++b) {
+#pragma unroll
+            for (int i = 0; i < H::words; ++i) w[i] = (uint32_t)a * (i + 1) + b;
+            st.compress(w);
+        }
+    } else {
+        st.init();
+        const uint32_t nb = n_blocks(kv.plen + kv.len, H::block_bytes, H::len_bytes);
+        uint32_t w[H::words];
+        for (uint32_t b = 0; b < nb; ++b) {
+            block_variant<H, V>(kv, b, nb, w);
+            st.compress(w);
+        }
+    }
+    uint32_t x = 0;
+#pragma unroll
+    for (int j = 0; j < H::digest_bytes / 4; ++j) x ^= st.be_word(j);
+    out[i] = x;
+}
+
+template <class H, int V>
+float run(const uint8_t* blob, const uint64_t* off, const uint32_t* order, uint32_t n, const uint8_t* pre,
+          uint32_t plen, uint32_t* out, int reps) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    dim3 grid((n + 255) / 256);
+    const size_t dl = V == kDma ? 4 * 16384 : 0;
+    hipLaunchKernelGGL((k_hash<H, V>), grid, dim3(256), dl, 0, blob, off, order, n, pre, plen, out);
+    CK(hipEventRecord(a));
+    for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((k_hash<H, V>), grid, dim3(256), dl, 0, blob, off, order, n, pre, plen, out);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    std::vector<uint32_t> h(n);
+    CK(hipMemcpy(h.data(), out, n * 4, hipMemcpyDeviceToHost));
+    uint64_t cs = 0;
+    for (uint32_t i = 0; i < n; ++i) cs = cs * 1000003u + h[order ? i : i];
+    // checksum over the digests in key order (invert the permutation) so variants are comparable
+    if (order) {
+        std::vector<uint32_t> ord(n);
+        CK(hipMemcpy(ord.data(), order, n * 4, hipMemcpyDeviceToHost));
+        std::vector<uint32_t> byk(n);
+        for (uint32_t i = 0; i < n; ++i) byk[ord[i]] = h[i];
+        cs = 0;
+        for (uint32_t i = 0; i < n; ++i) cs = cs * 1000003u + byk[i];
+    }
+    g_checksum = cs;
+    return ms / reps;
+}
+
+int main(int argc, char** argv) {
+    const uint32_t n = argc > 1 ? atoi(argv[1]) : 1000000;
+    const int reps = argc > 2 ? atoi(argv[2]) : 10;
+    const int lo = argc > 3 ? atoi(argv[3]) : 100, hi = argc > 4 ? atoi(argv[4]) : 1500;
+    std::mt19937_64 rng(42);
+    std::vector<uint64_t> off(n + 1, 0);
+    for (uint32_t i = 0; i < n; ++i) off[i + 1] = off[i] + lo + rng() % (hi - lo + 1);
+    const uint64_t bytes = off[n];
+    std::vector<uint8_t> blob((bytes + 256 + 7) & ~7ull);
+    for (size_t i = 0; i < blob.size(); i += 8) { uint64_t v = rng(); memcpy(&blob[i], &v, 8); }
+    // orders: by block count (descending: the load-balancing permutation), a random permutation (packets of a
+    // wave scattered over the whole blob, like modulo-style claims), and random-then-sorted
+    std::vector<uint32_t> order(n), scat(n), scat_sorted(n);
+    std::iota(order.begin(), order.end(), 0);
+    auto nbk = [&](uint32_t x) { return (off[x + 1] - off[x] + 1 + 8) / 64; };
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return nbk(x) > nbk(y); });
+    std::iota(scat.begin(), scat.end(), 0);
+    std::shuffle(scat.begin(), scat.end(), rng);
+    scat_sorted = scat;
+    std::stable_sort(scat_sorted.begin(), scat_sorted.end(), [&](uint32_t x, uint32_t y) { return nbk(x) > nbk(y); });
+    uint64_t blocks = 0;
+    for (uint32_t i = 0; i < n; ++i) blocks += (off[i + 1] - off[i] + 1 + 8) / 64 + 1;
+    uint8_t *d_blob, *d_pre;
+    uint64_t* d_off;
+    uint32_t *d_order, *d_out, *d_scat, *d_scat_sorted;
+    CK(hipMalloc(&d_blob, blob.size() + 64));
+    d_blob += 64;
+    CK(hipMalloc(&d_off, (n + 1) * 8));
+    CK(hipMalloc(&d_order, n * 4));
+    CK(hipMalloc(&d_out, n * 4));
+    CK(hipMalloc(&d_scat, n * 4));
+    CK(hipMalloc(&d_scat_sorted, n * 4));
+    CK(hipMemcpy(d_scat, scat.data(), n * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_scat_sorted, scat_sorted.data(), n * 4, hipMemcpyHostToDevice));
+    CK(hipMalloc(&d_pre, 256));
+    CK(hipMemcpy(d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_off, off.data(), (n + 1) * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_order, order.data(), n * 4, hipMemcpyHostToDevice));
+    CK(hipMemset(d_pre, 0x2a, 256));
+    printf("n=%u bytes=%.1f MB blocks(md5)=%llu\n", n, bytes / 1e6, (unsigned long long)blocks);
+    for (int round = 0; round < 2; ++round) {
+        struct R { const char* name; float ms; uint64_t cs = 0; };
+        std::vector<R> rs;
+        { float ms_ = run<Md5, kFast>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"md5 fast sorted", ms_, g_checksum}); }
+        { float ms_ = run<Md5, kDma>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"md5 dma(2,2,wg256) sorted", ms_, g_checksum}); }
+        { float ms_ = run_dma<Md5, 1, 2>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"md5 dma(1,2) sorted", ms_, g_checksum}); }
+        { float ms_ = run_dma<Md5, 1, 3>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"md5 dma(1,3) sorted", ms_, g_checksum}); }
+        { float ms_ = run_dma<Md5, 1, 4>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"md5 dma(1,4) sorted", ms_, g_checksum}); }
+        { float ms_ = run_dma<Md5, 2, 2>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"md5 dma(2,2) sorted", ms_, g_checksum}); }
+        { float ms_ = run_dma<Md5, 2, 3>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"md5 dma(2,3) sorted", ms_, g_checksum}); }
+        { float ms_ = run_dma<Md5, 4, 2>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"md5 dma(4,2) sorted", ms_, g_checksum}); }
+        { float ms_ = run_dma<Md5, 2, 3>(d_blob, d_off, d_scat_sorted, n, d_pre, 1, d_out, reps); rs.push_back({"md5 dma(2,3) scat-sorted", ms_, g_checksum}); }
+        { float ms_ = run<Md5, kPure>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"md5 pure sorted", ms_, g_checksum}); }
+        { float ms_ = run<NullHash, kFast>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"null fast sorted", ms_, g_checksum}); }
+        { float ms_ = run<NullHash, kFast>(d_blob, d_off, nullptr, n, d_pre, 1, d_out, reps); rs.push_back({"null fast natural", ms_, g_checksum}); }
+        { float ms_ = run_dma<NullHash, 1, 3>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"null dma(1,3) sorted", ms_, g_checksum}); }
+        { float ms_ = run_dma<NullHash, 2, 2>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"null dma(2,2) sorted", ms_, g_checksum}); }
+        { float ms_ = run_dma<NullHash, 4, 2>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"null dma(4,2) sorted", ms_, g_checksum}); }
+        { float ms_ = run_dma<NullHash, 2, 2>(d_blob, d_off, nullptr, n, d_pre, 1, d_out, reps); rs.push_back({"null dma(2,2) natural", ms_, g_checksum}); }
+        { float ms_ = run<Sha1, kFast>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"sha1 fast sorted", ms_, g_checksum}); }
+        { float ms_ = run_dma<Sha1, 1, 3>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"sha1 dma(1,3) sorted", ms_, g_checksum}); }
+        { float ms_ = run_dma<Sha1, 2, 3>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"sha1 dma(2,3) sorted", ms_, g_checksum}); }
+        { float ms_ = run<Sha1, kPure>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"sha1 pure sorted", ms_, g_checksum}); }
+        { float ms_ = run<Sha256, kFast>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"sha256 fast sorted", ms_, g_checksum}); }
+        { float ms_ = run<Sha256, kPure>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"sha256 pure sorted", ms_, g_checksum}); }
+        for (auto& r : rs) (void)0;
+        for (auto& r : rs)
+            printf("round %d  %-26s %8.3f ms  %7.1f GB/s  %6.2f Gblk/s  cs=%016llx\n", round, r.name, r.ms,
+                   bytes / r.ms / 1e6, blocks / r.ms / 1e6, (unsigned long long)r.cs);
+    }
+    return 0;
+}
