@@ -680,29 +680,38 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     timer_begin(c, &t, kTimeSelect);
     HIP_TRY(launch_plan(L));
     timer_end(c, &t);
-    // ---- per-claim output capacity: every emitted packet but the last costs >= min_len bytes of budget
-    std::vector<uint64_t> upper(R);
-    if (R) HIP_TRY(hipMemcpyAsync(upper.data(), d_upper, (size_t)R * 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    std::vector<ReqState> st(R);
-    uint64_t cap_total = 0;
-    for (uint32_t r = 0; r < R; ++r) {
-        uint64_t cap = upper[r];
-        if (byte_limit <= 0) cap = std::min<uint64_t>(cap, 1);
-        else if (s->min_len > 0) cap = std::min<uint64_t>(cap, (uint64_t)byte_limit / s->min_len + 2);
-        st[r] = ReqState{};
-        st[r].cap = cap;
-        st[r].out_base = cap_total;
-        st[r].done = upper[r] == 0;
-        cap_total += cap;
-    }
+    // ---- per-claim output capacity: every emitted packet but the last costs >= min_len bytes of budget, so a
+    // claim sends at most byte_limit / min_len + 2 packets.  When that bound is small the capacities and output
+    // bases are computed on the device (no host round-trip); otherwise from the plan's row counts on the host.
     void* d_out;
-    if ((rc = ws_get(c, "out", std::max<uint64_t>(cap_total, 1) * 8, &d_out))) return rc;
-    L.out = (uint64_t*)d_out;
-    if (R) HIP_TRY(hipMemcpyAsync(d_state, st.data(), (size_t)R * sizeof(ReqState), hipMemcpyHostToDevice, c->stream));
+    uint64_t cap_total = 0;
+    const uint64_t per_claim = byte_limit <= 0 ? 1 : (s->min_len > 0 ? (uint64_t)byte_limit / s->min_len + 2 : ~0ull);
+    if (per_claim != ~0ull && per_claim <= (1ull << 26) / std::max<uint32_t>(R, 1)) {
+        cap_total = per_claim * R;
+        if ((rc = ws_get(c, "out", std::max<uint64_t>(cap_total, 1) * 8, &d_out))) return rc;
+        L.out = (uint64_t*)d_out;
+        HIP_TRY(launch_caps(L, per_claim));
+    } else {
+        std::vector<uint64_t> upper(R);
+        if (R) HIP_TRY(hipMemcpyAsync(upper.data(), d_upper, (size_t)R * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        std::vector<ReqState> st(R);
+        for (uint32_t r = 0; r < R; ++r) {
+            st[r] = ReqState{};
+            st[r].cap = std::min<uint64_t>(upper[r], per_claim);
+            st[r].out_base = cap_total;
+            st[r].done = upper[r] == 0;
+            cap_total += st[r].cap;
+        }
+        if ((rc = ws_get(c, "out", std::max<uint64_t>(cap_total, 1) * 8, &d_out))) return rc;
+        L.out = (uint64_t*)d_out;
+        if (R) HIP_TRY(hipMemcpyAsync(d_state, st.data(), (size_t)R * sizeof(ReqState), hipMemcpyHostToDevice, c->stream));
+    }
 
+    // ---- windows: fill -> hash/test (one launch per hash family) -> compact; one host sync per window
     uint32_t* h_flags = (uint32_t*)c->pinned;
-    for (int window = 0;; ++window) {
+    uint64_t* h_tot = (uint64_t*)c->pinned + 8;
+    for (;;) {
         HIP_TRY(hipMemsetAsync(d_flags, 0, 64, c->stream));
         timer_begin(c, &t, kTimeSelect);
         HIP_TRY(launch_fill(L));
@@ -716,24 +725,17 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
         timer_begin(c, &t, kTimeCompact);
         HIP_TRY(launch_compact(L));
         timer_end(c, &t);
-        HIP_TRY(hipMemcpyAsync(h_flags, d_flags, 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(h_flags, d_flags, 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(h_tot, d_total, 24, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
+        // capacity overflow can only come from a wrong min_len bound; report it loudly
+        if (h_flags[1]) return fail(DSY_ECAPACITY, "internal: a claim overflowed its output capacity");
         if (!h_flags[0]) break;
     }
     void *d_packed_v, *d_packed_off_v;
     if ((rc = ws_get(c, "packed", std::max<uint64_t>(cap_total, 1) * 8, &d_packed_v))) return rc;
     if ((rc = ws_get(c, "packed_off", ((size_t)R + 1) * 8, &d_packed_off_v))) return rc;
     HIP_TRY(launch_pack(L, (uint64_t*)d_packed_v, (uint64_t*)d_packed_off_v, nullptr));
-    uint64_t* h_tot = (uint64_t*)c->pinned + 8;
-    HIP_TRY(hipMemcpyAsync(h_tot, d_total, 24, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    // capacity overflow can only come from a wrong min_len bound; report it loudly
-    std::vector<ReqState> fin(R);
-    if (R) {
-        HIP_TRY(hipMemcpy(fin.data(), d_state, (size_t)R * sizeof(ReqState), hipMemcpyDeviceToHost));
-        for (uint32_t r = 0; r < R; ++r)
-            if (fin[r].overflow) return fail(DSY_ECAPACITY, "internal: claim %u overflowed its output capacity", r);
-    }
     timers_collect(c);
     c->blocks[kTimePairTest] += h_tot[1];
     c->bytes[kTimePairTest] += h_tot[2];
@@ -759,10 +761,12 @@ int dsy_sync_respond(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, ui
     if ((rc = respond_core(c, s, reqs, R, (const uint8_t*)d_f, filters_len + 64, metas, nmeta, responder_global_time,
                            include_inactive, byte_limit, random_seed, &d_packed, &d_off, &pairs)))
         return rc;
-    HIP_TRY(hipMemcpy(out_req_offsets, d_off, ((size_t)R + 1) * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpyAsync(out_req_offsets, d_off, ((size_t)R + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     const uint64_t total = out_req_offsets[R];
     if (total > out_cap) return fail(DSY_ECAPACITY, "out_cap %llu < %llu rows", (unsigned long long)out_cap, (unsigned long long)total);
-    if (total) HIP_TRY(hipMemcpy(out_idx, d_packed, total * 8, hipMemcpyDeviceToHost));
+    if (total) HIP_TRY(hipMemcpyAsync(out_idx, d_packed, total * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
     return DSY_OK;
 }
 

@@ -111,6 +111,7 @@ hipError_t launch_fill(const RespondLaunch& L);
 // hash + test the window's pairs of the listed claims, all of one (hash kind, chunk) family
 hipError_t launch_pair_test_list(const RespondLaunch& L, int kind, uint32_t chunk, const uint32_t* d_list, uint32_t n);
 hipError_t launch_compact(const RespondLaunch& L);
+hipError_t launch_caps(const RespondLaunch& L, uint64_t per_claim_cap);
 hipError_t launch_pack(const RespondLaunch& L, uint64_t* packed, uint64_t* packed_offsets, uint64_t* d_scan_tmp);
 
 }  // namespace dsy

@@ -271,9 +271,12 @@ __global__ void __launch_bounds__(256) k_pair_test(RespondLaunch L, const uint32
     const uint64_t wave0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     uint8_t* my_lds = dma_lds + (threadIdx.x >> 6) * DmaGeometry<2, 2>::kWaveBytes;
+    unsigned long long acc_blocks = 0, acc_bytes = 0;  // this lane's algorithmic work, reduced once per block
+    // chunk-major task order: wave-task v hashes 64-pair chunk (v / n_list) of claim (v % n_list), so the
+    // non-empty chunks of every claim come first and spread evenly over the grid
     for (uint64_t wv = wave0; wv < total_waves; wv += wstride) {
-        const uint32_t r = req_list[wv / waves_per_req];
-        const uint64_t i0 = (wv % waves_per_req) * 64;
+        const uint32_t r = req_list[wv % n_list];
+        const uint64_t i0 = (wv / n_list) * 64;
         const uint64_t n = L.state[r].n_window;
         if (i0 >= n) continue;  // wave-uniform: past this claim's window
         const uint64_t i = i0 + lane;
@@ -305,19 +308,30 @@ __global__ void __launch_bounds__(256) k_pair_test(RespondLaunch L, const uint32
                 ok &= (filt[pos >> 5] >> (pos & 31)) & 1u;
             }
         }
-        if (active) L.miss[(uint64_t)r * W + t] = (uint8_t)(ok ^ 1u);
-        if (L.total_blocks) {  // algorithmic work of this wave: compression blocks and packet bytes
-            unsigned long long nb = active ? n_blocks(kv.plen + kv.len, H::block_bytes, H::len_bytes) : 0;
-            unsigned long long by = active ? kv.len : 0;
+        if (active) {
+            L.miss[(uint64_t)r * W + t] = (uint8_t)(ok ^ 1u);
+            acc_blocks += n_blocks(kv.plen + kv.len, H::block_bytes, H::len_bytes);
+            acc_bytes += kv.len;
+        }
+    }
+    if (L.total_blocks) {  // one pair of atomics per workgroup (a contended atomic per wave-task would stall
+                           // the next vmcnt wait of every wave behind it)
+        __shared__ unsigned long long red[2][4];
 #pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) {
-                nb += __shfl_xor(nb, d, 64);
-                by += __shfl_xor(by, d, 64);
-            }
-            if (lane == 0) {
-                atomicAdd((unsigned long long*)&L.total_blocks[0], nb);
-                atomicAdd((unsigned long long*)&L.total_blocks[1], by);
-            }
+        for (int d = 32; d >= 1; d >>= 1) {
+            acc_blocks += __shfl_xor(acc_blocks, d, 64);
+            acc_bytes += __shfl_xor(acc_bytes, d, 64);
+        }
+        if (lane == 0) {
+            red[0][threadIdx.x >> 6] = acc_blocks;
+            red[1][threadIdx.x >> 6] = acc_bytes;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long b = 0, y = 0;
+            for (uint32_t wv = 0; wv < blockDim.x / 64; ++wv) b += red[0][wv], y += red[1][wv];
+            if (b) atomicAdd((unsigned long long*)&L.total_blocks[0], b);
+            if (y) atomicAdd((unsigned long long*)&L.total_blocks[1], y);
         }
     }
 }
@@ -416,6 +430,7 @@ __global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
         S->emitted = emitted;
         S->spent = spent;
         S->overflow = overflow;
+        if (overflow) L.flags[1] = 1;
         if (done || S->exhausted) S->done = 1;
         else L.flags[0] = 1;
         atomicAdd((unsigned long long*)L.total_pairs, (unsigned long long)n);
@@ -450,6 +465,44 @@ __global__ void __launch_bounds__(1024) k_scan_counts(RespondLaunch L, uint64_t*
         }
     }
     if (t == 1023) packed_offsets[L.R] = part[1023];
+}
+
+// Per-claim output capacity and state, on the device (no host round-trip): cap = min(upper bound of selected
+// rows, per_claim_cap), out_base = exclusive scan of cap.  Single workgroup.
+__global__ void __launch_bounds__(1024) k_caps(RespondLaunch L, uint64_t per_claim_cap) {
+    __shared__ uint64_t part[1024];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (L.R + 1023) / 1024;
+    uint64_t sum = 0;
+    for (uint32_t i = 0; i < per; ++i) {
+        const uint32_t r = t * per + i;
+        if (r < L.R) sum += min(L.upper[r], per_claim_cap);
+    }
+    part[t] = sum;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+        const uint64_t add = t >= (uint32_t)d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += add;
+        __syncthreads();
+    }
+    uint64_t run = part[t] - sum;
+    for (uint32_t i = 0; i < per; ++i) {
+        const uint32_t r = t * per + i;
+        if (r < L.R) {
+            ReqState st{};
+            st.cap = min(L.upper[r], per_claim_cap);
+            st.out_base = run;
+            st.done = L.upper[r] == 0;
+            L.state[r] = st;
+            run += st.cap;
+        }
+    }
+}
+
+hipError_t launch_caps(const RespondLaunch& L, uint64_t per_claim_cap) {
+    hipLaunchKernelGGL(k_caps, dim3(1), dim3(1024), 0, L.stream, L, per_claim_cap);
+    return hipGetLastError();
 }
 
 __global__ void __launch_bounds__(256) k_copy_out(RespondLaunch L, const uint64_t* packed_offsets, uint64_t* packed) {
