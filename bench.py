@@ -45,6 +45,11 @@ def parse():
     ap.add_argument("--byte-limit", type=int, default=5120)
     ap.add_argument("--cpu-claims", type=int, default=96, help="claims in the CPU-baseline sample (0: skip)")
     ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--sim-peers", type=int, default=1_000_000, help="config 3 gossip simulator peers (0: skip)")
+    ap.add_argument("--sim-universe", type=int, default=10_000)
+    ap.add_argument("--sim-initial", type=int, default=100)
+    ap.add_argument("--sim-rounds", type=int, default=10)
+    ap.add_argument("--sim-warmup", type=int, default=2)
     return ap.parse_args()
 
 
@@ -193,6 +198,10 @@ def main():
         with open(traffic_file) as f:
             roofline["traffic"] = json.load(f).get("hbm_bytes_per_launch")
 
+    gossip = None
+    if args.sim_peers > 0:
+        gossip = gossip_sim(args, ctx, dev, rank, world, dist)
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_claims > 0:
         cpu = cpu_baseline(args, ctx, lib, store, reqs, claims, blob, offsets, total_bytes, N, fblob)
@@ -219,11 +228,51 @@ def main():
                        "parallelism": "claims sharded over %d GPU(s), store replicated" % world},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "gossip_sim": gossip,
         }
         print(json.dumps(line))
     lib.dsy_store_free(store)
     if dist:
         dist.destroy_process_group()
+
+
+def gossip_sim(args, ctx, dev, rank, world, dist):
+    """BASELINE config 3: the epidemic-sync simulator (dispersy_amd/sim.py) -- P peers block-sharded over the
+    ranks, one gossip round = every peer claims (MTU filter over its store), every claim is answered, every peer
+    stores what it got; two RCCL all-to-all(v) exchanges per round.  Total work is fixed (strong scaling)."""
+    import torch
+    from dispersy_amd.sim import EpidemicSim, GpuEngine, make_config, make_universe
+    blob, offs = make_universe(args.sim_universe, seed=11)
+    cfg = make_config(args.sim_peers, args.sim_universe, rank, world, seed=11)
+    eng = GpuEngine(cfg, blob, offs, dev, ctx=ctx)
+    eng.seed(args.sim_initial)
+    sim = EpidemicSim(eng, cfg, rank, world, dist, dev)
+    held0 = sim.global_stats()[0]
+    for r in range(args.sim_warmup):
+        sim.round(r)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for r in range(args.sim_warmup, args.sim_warmup + args.sim_rounds):
+        sim.round(r)
+    eng.sync()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    held, chk = sim.global_stats()
+    return {"metric": "gossip sync rounds/sec", "value": round(args.sim_rounds / dt, 3), "unit": "rounds/s",
+            "n_gpus": world, "scaling": "strong", "rounds": args.sim_rounds, "warmup_rounds": args.sim_warmup,
+            "ms_per_round": round(dt / args.sim_rounds * 1e3, 3),
+            "config": {"peers": args.sim_peers, "universe": args.sim_universe, "initial_packets": args.sim_initial,
+                       "filter": "m=%d k=%d md5" % (cfg.m_bits, cfg.k), "byte_limit": cfg.byte_limit},
+            "packets_held_start": held0, "packets_held_end": held, "store_checksum": "%016x" % chk,
+            "exchange_bytes_rank0": sim.exchanged_bytes}
 
 
 def cpu_baseline(args, ctx, lib, store, reqs, claims, blob, offsets, total_bytes, N, fblob):

@@ -85,6 +85,14 @@ SIGNATURES = {
     "dsy_sync_respond_dev": (ctypes.c_int, [_P, _P, ctypes.POINTER(Request), _U32, _P, ctypes.POINTER(Meta), _U32,
                                             _U64, ctypes.c_int, ctypes.c_int64, _U64, ctypes.POINTER(_P),
                                             ctypes.POINTER(_P), _PU64]),
+    "dsy_sim_setup": (ctypes.c_int, [_P]),
+    "dsy_sim_seed": (ctypes.c_int, [_P, _P, _P, _U32]),
+    "dsy_sim_claim_counts": (ctypes.c_int, [_P, _P, _U32, _P, _U32]),
+    "dsy_sim_build_claims": (ctypes.c_int, [_P, _P, _U32, _P, _P, _P, _P, _P, _U32]),
+    "dsy_sim_resp_counts": (ctypes.c_int, [_P, _P, _P, _U64, _P, _U32]),
+    "dsy_sim_respond": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _U64, _P, _P, _U32, _PU64]),
+    "dsy_sim_merge": (ctypes.c_int, [_P, _P, _P, _P, _U64]),
+    "dsy_sim_stats": (ctypes.c_int, [_P, _P, _P, _P]),
 }
 
 _lib = None

@@ -787,4 +787,185 @@ int dsy_sync_respond_dev(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs
     return DSY_OK;
 }
 
+// ------------------------------------------------------------------------------------------- simulator
+static int sim_check(const dsy_sim_config* c) {
+    if (!c) return fail(DSY_EINVAL, "cfg is NULL");
+    if (c->n_peers < 2 || c->peer_begin > c->peer_end || c->peer_end > c->n_peers || c->peers_per_rank == 0)
+        return fail(DSY_EINVAL, "bad peer partition");
+    if (c->universe == 0 || c->universe > 65536) return fail(DSY_EINVAL, "universe must be 1..65536 packets");
+    if (c->m_bits > 32ull * kSimFilterWordsMax) return fail(DSY_EINVAL, "sim filters are limited to %u bits", 32 * kSimFilterWordsMax);
+    int32_t kind;
+    uint32_t chunk;
+    int rc = check_family(c->m_bits, c->k, &kind, &chunk);
+    if (rc) return rc;
+    if (kind != c->hash_kind || chunk != c->chunk_bytes || kind > DSY_SHA256)
+        return fail(DSY_EINVAL, "sim filter family must match bloomfilter.py and be MD5/SHA-1/SHA-256");
+    if (c->capacity == 0 || c->capacity > 2048) return fail(DSY_EINVAL, "capacity must be 1..2048");
+    return DSY_OK;
+}
+
+static SimLaunch sim_launch(dsy_ctx* c, const dsy_sim_config* cfg) {
+    SimLaunch L{};
+    L.cfg = *cfg;
+    L.stream = c->stream;
+    return L;
+}
+
+int dsy_sim_setup(dsy_sim_config* c) {
+    if (!c) return fail(DSY_EINVAL, "cfg is NULL");
+    c->words = (c->universe + 31) / 32;
+    c->claim_bytes = (uint32_t)((sizeof(dsy_sim_claim_header) + filter_words(c->m_bits) * 4 + 15) / 16 * 16);
+    c->resp_bytes = (uint32_t)((sizeof(dsy_sim_resp_header) + 2 * DSY_SIM_RESP_MAX + 15) / 16 * 16);
+    return sim_check(c);
+}
+
+int dsy_sim_seed(dsy_ctx* c, const dsy_sim_config* cfg, uint32_t* d_bits, uint32_t initial) {
+    if (!c || !d_bits) return fail(DSY_EINVAL, "NULL argument");
+    int rc = sim_check(cfg);
+    if (rc) return rc;
+    Guard g(c);
+    SimLaunch L = sim_launch(c, cfg);
+    L.bits = d_bits;
+    L.initial = initial;
+    HIP_TRY(launch_sim(kSimSeed, L));
+    return DSY_OK;
+}
+
+static int sim_counts(dsy_ctx* c, SimLaunch& L, int op, uint32_t* h_counts, uint32_t n_ranks) {
+    void* d;
+    int rc;
+    if ((rc = ws_get(c, "sim_counts", 4 * std::max<uint32_t>(n_ranks, 1), &d))) return rc;
+    HIP_TRY(hipMemsetAsync(d, 0, 4 * n_ranks, c->stream));
+    L.counts = (uint32_t*)d;
+    HIP_TRY(launch_sim(op, L));
+    HIP_TRY(hipMemcpyAsync(h_counts, d, 4 * n_ranks, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return DSY_OK;
+}
+
+int dsy_sim_claim_counts(dsy_ctx* c, const dsy_sim_config* cfg, uint32_t round, uint32_t* h_counts, uint32_t n_ranks) {
+    if (!c || !h_counts || !n_ranks) return fail(DSY_EINVAL, "NULL argument");
+    int rc = sim_check(cfg);
+    if (rc) return rc;
+    if ((cfg->n_peers + cfg->peers_per_rank - 1) / cfg->peers_per_rank > n_ranks) return fail(DSY_EINVAL, "n_ranks too small");
+    Guard g(c);
+    SimLaunch L = sim_launch(c, cfg);
+    L.round = round;
+    return sim_counts(c, L, kSimClaimCounts, h_counts, n_ranks);
+}
+
+static int sim_cursor(dsy_ctx* c, const uint32_t* h_offsets, uint32_t n_ranks, uint32_t** out) {
+    void* d;
+    int rc;
+    if ((rc = ws_get(c, "sim_cursor", 4 * std::max<uint32_t>(n_ranks, 1), &d))) return rc;
+    HIP_TRY(hipMemcpyAsync(d, h_offsets, 4 * n_ranks, hipMemcpyHostToDevice, c->stream));
+    *out = (uint32_t*)d;
+    return DSY_OK;
+}
+
+int dsy_sim_build_claims(dsy_ctx* c, const dsy_sim_config* cfg, uint32_t round, const uint8_t* d_ublob,
+                         const uint64_t* d_uoff, const uint32_t* d_bits, uint8_t* d_out, const uint32_t* h_offsets,
+                         uint32_t n_ranks) {
+    if (!c || !d_ublob || !d_uoff || !d_bits || !h_offsets) return fail(DSY_EINVAL, "NULL argument");
+    int rc = sim_check(cfg);
+    if (rc) return rc;
+    Guard g(c);
+    SimLaunch L = sim_launch(c, cfg);
+    L.round = round;
+    L.ublob = d_ublob;
+    L.uoff = d_uoff;
+    L.bits = (uint32_t*)d_bits;
+    L.out = d_out;
+    if ((rc = sim_cursor(c, h_offsets, n_ranks, &L.cursor))) return rc;
+    PendingTimer t;
+    timer_begin(c, &t, kTimeBuild);
+    HIP_TRY(launch_sim(kSimBuild, L));
+    timer_end(c, &t);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    timers_collect(c);
+    return DSY_OK;
+}
+
+int dsy_sim_resp_counts(dsy_ctx* c, const dsy_sim_config* cfg, const uint8_t* d_claims, uint64_t n_claims,
+                        uint32_t* h_counts, uint32_t n_ranks) {
+    if (!c || !h_counts || !n_ranks || (n_claims && !d_claims)) return fail(DSY_EINVAL, "NULL argument");
+    int rc = sim_check(cfg);
+    if (rc) return rc;
+    Guard g(c);
+    SimLaunch L = sim_launch(c, cfg);
+    L.in = d_claims;
+    L.n_in = n_claims;
+    return sim_counts(c, L, kSimRespCounts, h_counts, n_ranks);
+}
+
+int dsy_sim_respond(dsy_ctx* c, const dsy_sim_config* cfg, const uint8_t* d_ublob, const uint64_t* d_uoff,
+                    const uint32_t* d_bits, const uint8_t* d_claims, uint64_t n_claims, uint8_t* d_out,
+                    const uint32_t* h_offsets, uint32_t n_ranks, uint64_t* out_tested) {
+    if (!c || !d_ublob || !d_uoff || !d_bits || !h_offsets || (n_claims && (!d_claims || !d_out)))
+        return fail(DSY_EINVAL, "NULL argument");
+    int rc = sim_check(cfg);
+    if (rc) return rc;
+    Guard g(c);
+    SimLaunch L = sim_launch(c, cfg);
+    L.ublob = d_ublob;
+    L.uoff = d_uoff;
+    L.bits = (uint32_t*)d_bits;
+    L.in = d_claims;
+    L.n_in = n_claims;
+    L.out = d_out;
+    void* dt;
+    if ((rc = ws_get(c, "sim_tested", 16, &dt))) return rc;
+    HIP_TRY(hipMemsetAsync(dt, 0, 16, c->stream));
+    L.tested = (unsigned long long*)dt;
+    if ((rc = sim_cursor(c, h_offsets, n_ranks, &L.cursor))) return rc;
+    PendingTimer t;
+    timer_begin(c, &t, kTimePairTest);
+    HIP_TRY(launch_sim(kSimRespond, L));
+    timer_end(c, &t);
+    uint64_t* h = (uint64_t*)c->pinned + 16;
+    HIP_TRY(hipMemcpyAsync(h, dt, 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    timers_collect(c);
+    if (out_tested) *out_tested = h[0];
+    return DSY_OK;
+}
+
+int dsy_sim_merge(dsy_ctx* c, const dsy_sim_config* cfg, uint32_t* d_bits, const uint8_t* d_resps, uint64_t n_resps) {
+    if (!c || !d_bits || (n_resps && !d_resps)) return fail(DSY_EINVAL, "NULL argument");
+    int rc = sim_check(cfg);
+    if (rc) return rc;
+    Guard g(c);
+    SimLaunch L = sim_launch(c, cfg);
+    L.bits = d_bits;
+    L.in = d_resps;
+    L.n_in = n_resps;
+    void* d;
+    if ((rc = ws_get(c, "sim_overflow", 16, &d))) return rc;
+    HIP_TRY(hipMemsetAsync(d, 0, 16, c->stream));
+    L.counts = (uint32_t*)d;
+    HIP_TRY(launch_sim(kSimMerge, L));
+    uint32_t* h = (uint32_t*)c->pinned + 48;
+    HIP_TRY(hipMemcpyAsync(h, d, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (h[0]) return fail(DSY_ECAPACITY, "a response exceeded DSY_SIM_RESP_MAX packets (byte_limit / shortest packet too large)");
+    return DSY_OK;
+}
+
+int dsy_sim_stats(dsy_ctx* c, const dsy_sim_config* cfg, const uint32_t* d_bits, uint64_t* out) {
+    if (!c || !d_bits || !out) return fail(DSY_EINVAL, "NULL argument");
+    int rc = sim_check(cfg);
+    if (rc) return rc;
+    Guard g(c);
+    SimLaunch L = sim_launch(c, cfg);
+    L.bits = (uint32_t*)d_bits;
+    void* d;
+    if ((rc = ws_get(c, "sim_stats", 16, &d))) return rc;
+    HIP_TRY(hipMemsetAsync(d, 0, 16, c->stream));
+    L.stats = (unsigned long long*)d;
+    HIP_TRY(launch_sim(kSimStats, L));
+    HIP_TRY(hipMemcpyAsync(out, d, 16, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return DSY_OK;
+}
+
 }  // extern "C"

@@ -114,4 +114,28 @@ hipError_t launch_compact(const RespondLaunch& L);
 hipError_t launch_caps(const RespondLaunch& L, uint64_t per_claim_cap);
 hipError_t launch_pack(const RespondLaunch& L, uint64_t* packed, uint64_t* packed_offsets, uint64_t* d_scan_tmp);
 
+// ---------------------------------------------------------------------------------------- simulator
+static constexpr uint32_t kSimFilterWordsMax = 2048;  // m <= 65536 bits
+static constexpr uint32_t kSimRespMax = DSY_SIM_RESP_MAX;
+enum { kSimSeed = 0, kSimClaimCounts, kSimBuild, kSimRespCounts, kSimRespond, kSimMerge, kSimStats };
+
+struct SimLaunch {
+    dsy_sim_config cfg;
+    uint32_t round;
+    uint32_t initial;
+    const uint8_t* ublob;
+    const uint64_t* uoff;
+    uint32_t* bits;
+    const uint8_t* in;
+    uint64_t n_in;
+    uint8_t* out;
+    uint32_t* cursor;
+    uint32_t* counts;
+    unsigned long long* tested;
+    unsigned long long* stats;
+    hipStream_t stream;
+};
+
+hipError_t launch_sim(int op, const SimLaunch& L);
+
 }  // namespace dsy

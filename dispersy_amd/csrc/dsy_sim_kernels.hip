@@ -1,0 +1,326 @@
+// dsy_sim_kernels.hip -- the multi-peer epidemic-sync simulator (BASELINE config 3) on gfx950.
+//
+// Every simulated peer runs the reference protocol once per round:
+//   requester: _dispersy_claim_sync_bloom_filter_largest's "fewer than capacity packets" branch
+//              (community.py:808-821): an MTU filter over its packets in global-time order, prefix one random
+//              byte, range [1, acceptable] (or [1, gt of the capacity-th packet] when over-full)
+//   responder: _get_packets_for_bloomfilters + the byte-limited not_filter loop (community.py:2555-2567) over its
+//              own packets in global-time order
+//   requester: stores what it received (Dispersy._store, dispersy.py:1475-1532)
+// Peers are sharded over ranks by contiguous blocks; claims and responses travel between ranks as fixed-size
+// records (the host side runs the two all-to-all(v) exchanges over RCCL).  Stores are bitsets over a universe of
+// U packets with global_time(i) = i + 1, so "ascending global time" is "ascending bit index".
+#include "dsy_kernels.h"
+
+namespace dsy {
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    x += 0x9e3779b97f4a7c15ull;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ uint64_t sim_partner(const dsy_sim_config& c, uint32_t round, uint64_t p) {
+    const uint64_t h = splitmix64(c.seed ^ ((uint64_t)round << 40) ^ (p * 0x2545f4914f6cdd1dull));
+    return (p + 1 + h % (c.n_peers - 1)) % c.n_peers;
+}
+
+__device__ __forceinline__ uint32_t sim_prefix(const dsy_sim_config& c, uint32_t round, uint64_t p) {
+    return (uint32_t)(splitmix64(c.seed * 3 + 0x51ed27ull + (uint64_t)round * c.n_peers + p) >> 32) & 0xffu;
+}
+
+__device__ __forceinline__ uint32_t sim_owner(const dsy_sim_config& c, uint64_t p) {
+    return (uint32_t)(p / c.peers_per_rank);
+}
+
+// ------------------------------------------------------------------------------------------ seeding
+__global__ void k_sim_seed(dsy_sim_config c, uint32_t* __restrict__ bits, uint32_t initial) {
+    const uint64_t lp = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lp >= c.peer_end - c.peer_begin) return;
+    const uint64_t p = c.peer_begin + lp;
+    uint32_t* b = bits + lp * c.words;
+    for (uint32_t w = 0; w < c.words; ++w) b[w] = 0;
+    uint32_t have = 0;
+    for (uint64_t j = 0; have < initial && have < c.universe; ++j) {
+        const uint32_t id = (uint32_t)(splitmix64(c.seed * 7 + 0xabcdefull + p * 1000003ull + j) % c.universe);
+        const uint32_t m = 1u << (id & 31);
+        if (!(b[id >> 5] & m)) {
+            b[id >> 5] |= m;
+            ++have;
+        }
+    }
+}
+
+// ascending ids of one bitset into an LDS list (whole wave); returns the count
+__device__ __forceinline__ uint32_t wave_list_ids(const uint32_t* __restrict__ b, uint32_t words, uint16_t* list,
+                                                  uint32_t cap) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t n = 0;
+    for (uint32_t w0 = 0; w0 < words; w0 += 64) {
+        const uint32_t w = w0 + lane;
+        uint32_t word = w < words ? b[w] : 0u;
+        const uint32_t pc = __popc(word);
+        uint32_t incl = pc;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(incl, d, 64);
+            if ((int)lane >= d) incl += o;
+        }
+        uint32_t pos = n + incl - pc;
+        while (word) {
+            const uint32_t bit = __builtin_ctz(word);
+            word &= word - 1;
+            if (pos < cap) list[pos] = (uint16_t)(w * 32 + bit);
+            ++pos;
+        }
+        n += __shfl(incl, 63, 64);
+    }
+    __builtin_amdgcn_wave_barrier();
+    return n;
+}
+
+// --------------------------------------------------------------------------------------- claims
+__global__ void k_sim_claim_counts(dsy_sim_config c, uint32_t round, uint32_t* __restrict__ counts) {
+    const uint64_t lp = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lp >= c.peer_end - c.peer_begin) return;
+    atomicAdd(&counts[sim_owner(c, sim_partner(c, round, c.peer_begin + lp))], 1u);
+}
+
+static constexpr uint32_t kSimListCap = 2048;
+
+// one wave per local requester: list its packets, hash them into an LDS-resident filter (ds_or_b32; lanes that
+// hit the same word in one instruction are merged by the LDS atomic unit), write the claim record
+template <class H, int CHUNK>
+__global__ void __launch_bounds__(256) k_sim_build_claims(dsy_sim_config c, uint32_t round, const uint8_t* __restrict__ ublob,
+                                                          const uint64_t* __restrict__ uoff, const uint32_t* __restrict__ bits,
+                                                          uint8_t* __restrict__ out, uint32_t* __restrict__ cursor) {
+    __shared__ uint16_t lists[4][kSimListCap];
+    __shared__ uint32_t filt[4][kSimFilterWordsMax];
+    __shared__ uint8_t pre[4][4];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t lp = (uint64_t)blockIdx.x * 4 + wv;
+    if (lp >= c.peer_end - c.peer_begin) return;  // wave-uniform
+    const uint64_t p = c.peer_begin + lp;
+    const uint32_t nwords = (uint32_t)((c.m_bits + 31) / 32);
+    for (uint32_t i = lane; i < nwords; i += 64) filt[wv][i] = 0;
+    uint32_t n = wave_list_ids(bits + lp * c.words, c.words, lists[wv], kSimListCap);
+    // _select_and_fix(..., 0, capacity, True): the first capacity packets; over-full drops the (capacity+1)-th
+    // global time (global times are distinct here) and the range ends at the last kept one
+    uint64_t time_high = 0x7fffffffffffffffull;
+    if (n > c.capacity) {
+        n = c.capacity;
+        time_high = (uint64_t)lists[wv][n - 1] + 1;
+    }
+    const uint32_t prefix = sim_prefix(c, round, p);
+    if (lane == 0) pre[wv][0] = (uint8_t)prefix;
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        if (i < n) {
+            const uint32_t id = lists[wv][i];
+            KeyView kv{ublob + uoff[id], (uint32_t)(uoff[id + 1] - uoff[id]), pre[wv], 1};
+            H st;
+            hash_key<H>(kv, st);
+#pragma unroll
+            for (int j = 0; j < ChunkLimit<H, CHUNK>::kmax; ++j) {
+                if (j < (int)c.k) {
+                    const uint64_t pos = bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, j), c.m_bits);
+                    atomicOr(&filt[wv][pos >> 5], 1u << (pos & 31));
+                }
+            }
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t q = sim_partner(c, round, p);
+    uint32_t slot = 0;
+    if (lane == 0) slot = atomicAdd(&cursor[sim_owner(c, q)], 1u);
+    slot = __shfl(slot, 0, 64);
+    uint8_t* rec = out + (uint64_t)slot * c.claim_bytes;
+    if (lane == 0) {
+        dsy_sim_claim_header h;
+        h.requester = p;
+        h.responder = q;
+        h.time_high = time_high;
+        h.prefix = prefix;
+        h.n_sent = n;
+        *(dsy_sim_claim_header*)rec = h;
+    }
+    uint32_t* fw = (uint32_t*)(rec + sizeof(dsy_sim_claim_header));
+    for (uint32_t i = lane; i < nwords; i += 64) fw[i] = filt[wv][i];
+}
+
+// -------------------------------------------------------------------------------------- responses
+__global__ void k_sim_resp_counts(dsy_sim_config c, const uint8_t* __restrict__ claims, uint64_t n_claims,
+                                  uint32_t* __restrict__ counts) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_claims) return;
+    const dsy_sim_claim_header* h = (const dsy_sim_claim_header*)(claims + i * c.claim_bytes);
+    atomicAdd(&counts[sim_owner(c, h->requester)], 1u);
+}
+
+// one wave per incoming claim: the responder's packets in global-time order, 64 at a time; hash + probe; send the
+// missing ones until the byte budget is spent (the crossing packet is sent), then stop -- lazily, as the
+// reference's generator chain does
+template <class H, int CHUNK>
+__global__ void __launch_bounds__(256) k_sim_respond(dsy_sim_config c, const uint8_t* __restrict__ ublob,
+                                                     const uint64_t* __restrict__ uoff, const uint32_t* __restrict__ bits,
+                                                     const uint8_t* __restrict__ claims, uint64_t n_claims,
+                                                     uint8_t* __restrict__ out, uint32_t* __restrict__ cursor,
+                                                     unsigned long long* __restrict__ tested) {
+    __shared__ uint16_t lists[4][kSimListCap];
+    __shared__ uint32_t filt[4][kSimFilterWordsMax];
+    __shared__ uint8_t pre[4][4];
+    __shared__ uint16_t outl[4][kSimRespMax];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint64_t ci = (uint64_t)blockIdx.x * 4 + wv;
+    if (ci >= n_claims) return;
+    const uint8_t* rec = claims + ci * c.claim_bytes;
+    const dsy_sim_claim_header h = *(const dsy_sim_claim_header*)rec;
+    const uint32_t nwords = (uint32_t)((c.m_bits + 31) / 32);
+    const uint32_t* fw = (const uint32_t*)(rec + sizeof(dsy_sim_claim_header));
+    for (uint32_t i = lane; i < nwords; i += 64) filt[wv][i] = fw[i];
+    if (lane == 0) pre[wv][0] = (uint8_t)h.prefix;
+    const uint64_t lq = h.responder - c.peer_begin;
+    const uint32_t n = min(wave_list_ids(bits + lq * c.words, c.words, lists[wv], kSimListCap), kSimListCap);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    uint32_t sent = 0;
+    int64_t spent = 0;
+    uint32_t ntested = 0;
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const uint32_t id = i < n ? lists[wv][i] : 0u;
+        // range [1, time_high]: global_time = id + 1
+        const bool sel = i < n && (uint64_t)id + 1 <= h.time_high;
+        bool miss = false;
+        int64_t len = 0;
+        if (sel) {
+            KeyView kv{ublob + uoff[id], (uint32_t)(uoff[id + 1] - uoff[id]), pre[wv], 1};
+            H st;
+            hash_key<H>(kv, st);
+            uint32_t ok = 1;
+#pragma unroll
+            for (int j = 0; j < ChunkLimit<H, CHUNK>::kmax; ++j) {
+                if (j < (int)c.k) {
+                    const uint64_t pos = bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, j), c.m_bits);
+                    ok &= (filt[wv][pos >> 5] >> (pos & 31)) & 1u;
+                }
+            }
+            miss = !ok;
+            len = miss ? (int64_t)kv.len : 0;
+        }
+        ntested += __popcll(__ballot(sel));
+        int64_t incl = len;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int64_t o = __shfl_up(incl, d, 64);
+            if ((int)lane >= d) incl += o;
+        }
+        const uint64_t mmask = __ballot(miss);
+        const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+        const uint32_t rank = __popcll(mmask & lt);
+        const bool inc = miss && ((sent + rank == 0) || (spent + incl - len < c.byte_limit));
+        const uint64_t imask = __ballot(inc);
+        const uint32_t nin = __popcll(imask);
+        if (inc && sent + rank < kSimRespMax) outl[wv][sent + rank] = (uint16_t)id;
+        if (nin) spent += __shfl(incl, 63 - __builtin_clzll(imask), 64);
+        sent += nin;
+        if (sent > 0 && spent >= c.byte_limit) break;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t q_owner = sim_owner(c, h.requester);
+    uint32_t slot = 0;
+    if (lane == 0) slot = atomicAdd(&cursor[q_owner], 1u);
+    slot = __shfl(slot, 0, 64);
+    uint8_t* o = out + (uint64_t)slot * c.resp_bytes;
+    dsy_sim_resp_header* oh = (dsy_sim_resp_header*)o;
+    const uint32_t cnt = min(sent, (uint32_t)kSimRespMax);
+    if (lane == 0) {
+        oh->requester = h.requester;
+        oh->count = cnt;
+        oh->overflow = sent > kSimRespMax;
+        atomicAdd(tested, (unsigned long long)ntested);
+    }
+    uint16_t* ids = (uint16_t*)(o + sizeof(dsy_sim_resp_header));
+    if (lane < cnt) ids[lane] = outl[wv][lane];
+}
+
+// ------------------------------------------------------------------------------------------- merge
+__global__ void k_sim_merge(dsy_sim_config c, uint32_t* __restrict__ bits, const uint8_t* __restrict__ resps,
+                            uint64_t n_resps, uint32_t* __restrict__ overflow) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_resps) return;
+    const uint8_t* r = resps + i * c.resp_bytes;
+    const dsy_sim_resp_header h = *(const dsy_sim_resp_header*)r;
+    if (h.overflow) atomicOr(overflow, 1u);
+    uint32_t* b = bits + (h.requester - c.peer_begin) * c.words;
+    const uint16_t* ids = (const uint16_t*)(r + sizeof(dsy_sim_resp_header));
+    for (uint32_t j = 0; j < h.count; ++j) b[ids[j] >> 5] |= 1u << (ids[j] & 31);  // one response per requester
+}
+
+// per-rank digest of the stores: number of packets held and an order-independent checksum
+__global__ void k_sim_stats(dsy_sim_config c, const uint32_t* __restrict__ bits, unsigned long long* __restrict__ out) {
+    const uint64_t lp = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (lp >= c.peer_end - c.peer_begin) return;
+    const uint32_t* b = bits + lp * c.words;
+    unsigned long long held = 0, h = 0;
+    for (uint32_t w = 0; w < c.words; ++w) {
+        held += __popc(b[w]);
+        h ^= splitmix64(((c.peer_begin + lp) << 20) ^ ((uint64_t)w << 32) ^ b[w]);
+    }
+    atomicAdd(&out[0], held);
+    atomicXor(&out[1], h);
+}
+
+// ---------------------------------------------------------------------------------------- launchers
+template <class H, int CHUNK>
+static hipError_t sim_family(int op, const SimLaunch& L) {
+    const uint64_t local = L.cfg.peer_end - L.cfg.peer_begin;
+    if (op == 0) {
+        if (!local) return hipSuccess;
+        hipLaunchKernelGGL((k_sim_build_claims<H, CHUNK>), dim3((uint32_t)((local + 3) / 4)), dim3(256), 0, L.stream, L.cfg,
+                           L.round, L.ublob, L.uoff, L.bits, L.out, L.cursor);
+    } else {
+        if (!L.n_in) return hipSuccess;
+        hipLaunchKernelGGL((k_sim_respond<H, CHUNK>), dim3((uint32_t)((L.n_in + 3) / 4)), dim3(256), 0, L.stream, L.cfg,
+                           L.ublob, L.uoff, L.bits, L.in, L.n_in, L.out, L.cursor, L.tested);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_sim(int op, const SimLaunch& L) {
+    const dsy_sim_config& c = L.cfg;
+    const uint64_t local = c.peer_end - c.peer_begin;
+    switch (op) {
+        case kSimSeed:
+            if (local) hipLaunchKernelGGL(k_sim_seed, dim3((uint32_t)((local + 255) / 256)), dim3(256), 0, L.stream, c, L.bits, L.initial);
+            return hipGetLastError();
+        case kSimClaimCounts:
+            if (local) hipLaunchKernelGGL(k_sim_claim_counts, dim3((uint32_t)((local + 255) / 256)), dim3(256), 0, L.stream, c, L.round, L.counts);
+            return hipGetLastError();
+        case kSimRespCounts:
+            if (L.n_in) hipLaunchKernelGGL(k_sim_resp_counts, dim3((uint32_t)((L.n_in + 255) / 256)), dim3(256), 0, L.stream, c, L.in, L.n_in, L.counts);
+            return hipGetLastError();
+        case kSimMerge:
+            if (L.n_in) hipLaunchKernelGGL(k_sim_merge, dim3((uint32_t)((L.n_in + 255) / 256)), dim3(256), 0, L.stream, c, L.bits, L.in, L.n_in, L.counts);
+            return hipGetLastError();
+        case kSimStats:
+            if (local) hipLaunchKernelGGL(k_sim_stats, dim3((uint32_t)((local + 255) / 256)), dim3(256), 0, L.stream, c, L.bits, L.stats);
+            return hipGetLastError();
+        case kSimBuild:
+        case kSimRespond: {
+            const int o = op == kSimBuild ? 0 : 1;
+            switch (c.hash_kind) {
+                case DSY_MD5: return c.chunk_bytes == 2 ? sim_family<Md5, 2>(o, L) : sim_family<Md5, 4>(o, L);
+                case DSY_SHA1: return c.chunk_bytes == 2 ? sim_family<Sha1, 2>(o, L) : sim_family<Sha1, 4>(o, L);
+                default: return c.chunk_bytes == 2 ? sim_family<Sha256, 2>(o, L) : sim_family<Sha256, 4>(o, L);
+            }
+        }
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace dsy

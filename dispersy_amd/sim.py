@@ -1,0 +1,198 @@
+"""Multi-GPU epidemic-sync simulator (BASELINE config 3): many peers run Dispersy's Bloom-filter sync against each
+other, round after round, sharded over the GPUs of one node.
+
+Every round each peer
+  1. claims: builds its MTU bloom filter over the packets it holds (community.py:808-821) with a fresh 1-byte
+     prefix and sends it to a partner chosen by a counter-based RNG (the walker's role, community.py:1209-1221);
+  2. responds: for every claim it receives, returns its packets the filter lacks, in global-time order, until
+     the 5 KiB budget is spent (community.py:2555-2567);
+  3. stores what it received (Dispersy._store, dispersy.py:1475-1532).
+
+Peers are block-sharded over ranks (one process per GPU).  The two exchanges of a round -- claims to the
+responders' ranks, responses back -- are all-to-all(v) collectives over RCCL (torch.distributed "nccl"); the
+record counts travel first in a small all-to-all.  Pairing, prefixes and initial stores come from splitmix64 of
+(seed, round, peer), so the outcome is identical at 1, 2, 4 or 8 GPUs.
+
+The per-rank work runs in an *engine*: `GpuEngine` calls the HIP kernels through the C-ABI (dsy_sim_* in
+include/dsybloom.h).  Tests can pass the CPU engine of oracle/sim_ref.py to exercise the distributed logic with
+the gloo backend.
+"""
+import ctypes
+import math
+
+import numpy as np
+
+from . import _native
+from .bloomfilter import BloomFilter
+
+
+class SimConfig(ctypes.Structure):
+    _fields_ = [("n_peers", ctypes.c_uint64), ("peer_begin", ctypes.c_uint64), ("peer_end", ctypes.c_uint64),
+                ("peers_per_rank", ctypes.c_uint64), ("universe", ctypes.c_uint32), ("words", ctypes.c_uint32),
+                ("m_bits", ctypes.c_uint64), ("k", ctypes.c_uint32), ("hash_kind", ctypes.c_int32),
+                ("chunk_bytes", ctypes.c_uint32), ("capacity", ctypes.c_uint32), ("byte_limit", ctypes.c_int64),
+                ("seed", ctypes.c_uint64), ("claim_bytes", ctypes.c_uint32), ("resp_bytes", ctypes.c_uint32)]
+
+
+def make_config(n_peers, universe, rank, world, bits=10160, error_rate=0.01, byte_limit=5120, seed=11):
+    """The claim filter is the community's MTU filter (community.py:637-666, f = 0.01 -> MD5, k = 7)."""
+    probe = BloomFilter(bits, error_rate)
+    ppr = int(math.ceil(n_peers / float(world)))
+    c = SimConfig()
+    c.n_peers, c.peers_per_rank = n_peers, ppr
+    c.peer_begin, c.peer_end = min(n_peers, rank * ppr), min(n_peers, (rank + 1) * ppr)
+    c.universe = universe
+    c.words = (universe + 31) // 32
+    c.m_bits, c.k = probe.size, probe.functions
+    c.hash_kind, c.chunk_bytes = _native.HASH_KINDS[probe.hash_name], probe.chunk_bytes
+    c.capacity = probe.get_capacity(error_rate)
+    c.byte_limit = byte_limit
+    c.seed = seed
+    c.claim_bytes = (32 + ((c.m_bits + 31) // 32) * 4 + 15) // 16 * 16
+    c.resp_bytes = (16 + 2 * 64 + 15) // 16 * 16
+    return c
+
+
+def make_universe(universe, seed=11, lo=100, hi=1500):
+    """The packet universe (identical on every rank): lengths ~ U[lo, hi], random bytes, global_time = id + 1."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    lengths = rng.integers(lo, hi + 1, size=universe, dtype=np.int64)
+    offsets = np.zeros(universe + 1, dtype=np.uint64)
+    np.cumsum(lengths, out=offsets[1:])
+    return rng.bytes(int(offsets[-1])), offsets
+
+
+class GpuEngine(object):
+    """Per-rank simulator state in HBM + the dsy_sim_* kernels."""
+
+    def __init__(self, cfg, blob, offsets, device, ctx=None):
+        import torch
+        self.torch = torch
+        self.cfg = cfg
+        self.dev = device
+        self.ctx = ctx or _native.Context(device.index if device.index is not None else 0)
+        self.lib = self.ctx.lib
+        _native.check(self.lib.dsy_sim_setup(ctypes.byref(cfg)))
+        G = _native.BLOB_GUARD
+        full = bytearray(G) + bytearray(blob) + bytearray(G)
+        self.ublob_t = torch.frombuffer(full, dtype=torch.uint8).to(device)
+        self.ublob = self.ublob_t.data_ptr() + G
+        self.uoff_t = torch.from_numpy(offsets.astype(np.int64)).to(device)
+        local = cfg.peer_end - cfg.peer_begin
+        self.bits = torch.zeros(max(local, 1) * cfg.words, dtype=torch.int32, device=device)
+
+    def empty(self, nbytes):
+        return self.torch.empty(max(nbytes, 1), dtype=self.torch.uint8, device=self.dev)
+
+    def seed(self, initial):
+        _native.check(self.lib.dsy_sim_seed(self.ctx.handle, ctypes.byref(self.cfg), self.bits.data_ptr(), initial))
+        self.ctx.synchronize()
+
+    def claim_counts(self, rnd, world):
+        out = (ctypes.c_uint32 * world)()
+        _native.check(self.lib.dsy_sim_claim_counts(self.ctx.handle, ctypes.byref(self.cfg), rnd, out, world))
+        return np.array(out, dtype=np.int64)
+
+    def build_claims(self, rnd, offsets, total):
+        buf = self.empty(total * self.cfg.claim_bytes)
+        offs = (ctypes.c_uint32 * len(offsets))(*[int(x) for x in offsets])
+        _native.check(self.lib.dsy_sim_build_claims(self.ctx.handle, ctypes.byref(self.cfg), rnd, self.ublob,
+                                                    self.uoff_t.data_ptr(), self.bits.data_ptr(), buf.data_ptr(),
+                                                    offs, len(offsets)))
+        return buf
+
+    def resp_counts(self, claims, n, world):
+        out = (ctypes.c_uint32 * world)()
+        _native.check(self.lib.dsy_sim_resp_counts(self.ctx.handle, ctypes.byref(self.cfg), claims.data_ptr(), n,
+                                                   out, world))
+        return np.array(out, dtype=np.int64)
+
+    def respond(self, claims, n, offsets, total):
+        buf = self.empty(total * self.cfg.resp_bytes)
+        offs = (ctypes.c_uint32 * len(offsets))(*[int(x) for x in offsets])
+        tested = ctypes.c_uint64()
+        _native.check(self.lib.dsy_sim_respond(self.ctx.handle, ctypes.byref(self.cfg), self.ublob,
+                                               self.uoff_t.data_ptr(), self.bits.data_ptr(), claims.data_ptr(), n,
+                                               buf.data_ptr(), offs, len(offsets), ctypes.byref(tested)))
+        return buf, tested.value
+
+    def merge(self, resps, n):
+        _native.check(self.lib.dsy_sim_merge(self.ctx.handle, ctypes.byref(self.cfg), self.bits.data_ptr(),
+                                             resps.data_ptr(), n))
+
+    def stats(self):
+        out = (ctypes.c_uint64 * 2)()
+        _native.check(self.lib.dsy_sim_stats(self.ctx.handle, ctypes.byref(self.cfg), self.bits.data_ptr(), out))
+        return int(out[0]), int(out[1])
+
+    def sync(self):
+        self.ctx.synchronize()
+
+
+class EpidemicSim(object):
+    """Drives the rounds on one rank; `dist` is torch.distributed (or None for a single process)."""
+
+    def __init__(self, engine, cfg, rank=0, world=1, dist=None, device=None):
+        self.e, self.cfg, self.rank, self.world, self.dist = engine, cfg, rank, world, dist
+        self.device = device
+        self.tested = 0
+        self.exchanged_bytes = 0
+
+    def _alltoall_counts(self, counts):
+        if self.world == 1:
+            return counts.copy()
+        import torch
+        send = torch.tensor(counts, dtype=torch.int64, device=self.device)
+        recv = torch.empty_like(send)
+        self.dist.all_to_all_single(recv, send)
+        return recv.cpu().numpy()
+
+    def _alltoall_records(self, buf, send_counts, recv_counts, rec_bytes):
+        if self.world == 1:
+            return buf
+        import torch
+        self.e.sync()
+        out = torch.empty(max(int(recv_counts.sum()) * rec_bytes, 1), dtype=torch.uint8, device=self.device)
+        in_splits = [int(c) * rec_bytes for c in send_counts]
+        out_splits = [int(c) * rec_bytes for c in recv_counts]
+        if sum(in_splits) == 0:
+            buf = buf[:0]
+        else:
+            buf = buf[:sum(in_splits)]
+        self.dist.all_to_all_single(out[:sum(out_splits)] if sum(out_splits) else out[:0], buf,
+                                    output_split_sizes=out_splits, input_split_sizes=in_splits)
+        if self.device is not None and self.device.type == "cuda":
+            torch.cuda.current_stream(self.device).synchronize()
+        self.exchanged_bytes += sum(in_splits)
+        return out
+
+    def round(self, rnd):
+        c = self.cfg
+        counts = self.e.claim_counts(rnd, self.world)
+        offs = np.concatenate([[0], np.cumsum(counts)[:-1]])
+        claims = self.e.build_claims(rnd, offs, int(counts.sum()))
+        rcounts = self._alltoall_counts(counts)
+        claims_in = self._alltoall_records(claims, counts, rcounts, c.claim_bytes)
+        n_in = int(rcounts.sum())
+        pcounts = self.e.resp_counts(claims_in, n_in, self.world)
+        poffs = np.concatenate([[0], np.cumsum(pcounts)[:-1]])
+        resps, tested = self.e.respond(claims_in, n_in, poffs, int(pcounts.sum()))
+        self.tested += tested
+        back = self._alltoall_counts(pcounts)
+        resps_in = self._alltoall_records(resps, pcounts, back, c.resp_bytes)
+        self.e.merge(resps_in, int(back.sum()))
+
+    def global_stats(self):
+        held, chk = self.e.stats()
+        chk &= 0x7fffffffffffffff
+        if self.world == 1:
+            return held, chk
+        import torch
+        t = torch.tensor([held], dtype=torch.int64, device=self.device)
+        self.dist.all_reduce(t)
+        parts = [torch.zeros(1, dtype=torch.int64, device=self.device) for _ in range(self.world)]
+        self.dist.all_gather(parts, torch.tensor([chk & 0x7fffffffffffffff], dtype=torch.int64, device=self.device))
+        x = 0
+        for p in parts:
+            x ^= int(p.item())
+        return int(t.item()), x

@@ -184,6 +184,62 @@ int dsy_sync_respond_dev(dsy_ctx* ctx, const dsy_store* store, const dsy_request
                          uint64_t random_seed, const uint64_t** d_out_idx, const uint64_t** d_out_offsets,
                          uint64_t* out_total_pairs);
 
+/* ------------------------------------------------------------------ epidemic-sync simulator (config 3) */
+/* Simulated peers run the reference protocol once per round (see dispersy_amd/csrc/dsy_sim_kernels.hip):
+ * requester claim = _dispersy_claim_sync_bloom_filter_largest's below-capacity branch (community.py:808-821),
+ * responder = _get_packets_for_bloomfilters + the byte-limited loop (community.py:2555-2567), then the requester
+ * stores what it got.  Peers are block-sharded over ranks; claims and responses are fixed-size records the host
+ * exchanges between ranks (RCCL all-to-all(v)).  Stores are bitsets over a universe of packets whose global time
+ * is index + 1.  All buffers are device pointers; count queries synchronise the ctx stream. */
+#define DSY_SIM_RESP_MAX 64
+
+typedef struct dsy_sim_config {
+    uint64_t n_peers;        /* P, all ranks */
+    uint64_t peer_begin;     /* this rank's peers [peer_begin, peer_end) */
+    uint64_t peer_end;
+    uint64_t peers_per_rank; /* owner(p) = p / peers_per_rank */
+    uint32_t universe;       /* U packets, id 0..U-1, global_time = id + 1; U <= 65536 */
+    uint32_t words;          /* bitset words per peer (set by dsy_sim_setup) */
+    uint64_t m_bits;         /* claim filter (community.py:637-666), m <= 65536 */
+    uint32_t k;
+    int32_t hash_kind;
+    uint32_t chunk_bytes;
+    uint32_t capacity;       /* BloomFilter.get_capacity(f) (community.py:774) */
+    int64_t byte_limit;      /* dispersy_sync_response_limit (community.py:935-941) */
+    uint64_t seed;
+    uint32_t claim_bytes;    /* record sizes (set by dsy_sim_setup) */
+    uint32_t resp_bytes;
+} dsy_sim_config;
+
+typedef struct dsy_sim_claim_header {
+    uint64_t requester, responder, time_high;
+    uint32_t prefix, n_sent;
+} dsy_sim_claim_header;  /* followed by the filter words */
+
+typedef struct dsy_sim_resp_header {
+    uint64_t requester;
+    uint32_t count, overflow;
+} dsy_sim_resp_header;   /* followed by count uint16 packet ids */
+
+int dsy_sim_setup(dsy_sim_config* cfg);
+int dsy_sim_seed(dsy_ctx* ctx, const dsy_sim_config* cfg, uint32_t* d_bits, uint32_t initial);
+/* claims this rank's requesters send to each rank in `round` (h_counts[n_ranks]) */
+int dsy_sim_claim_counts(dsy_ctx* ctx, const dsy_sim_config* cfg, uint32_t round, uint32_t* h_counts, uint32_t n_ranks);
+/* build the claim records into d_out, grouped by destination rank at h_offsets[dest] (records, exclusive scan) */
+int dsy_sim_build_claims(dsy_ctx* ctx, const dsy_sim_config* cfg, uint32_t round, const uint8_t* d_ublob,
+                         const uint64_t* d_uoff, const uint32_t* d_bits, uint8_t* d_out, const uint32_t* h_offsets,
+                         uint32_t n_ranks);
+int dsy_sim_resp_counts(dsy_ctx* ctx, const dsy_sim_config* cfg, const uint8_t* d_claims, uint64_t n_claims,
+                        uint32_t* h_counts, uint32_t n_ranks);
+/* answer the received claims (responders are this rank's peers); responses grouped by the requester's rank */
+int dsy_sim_respond(dsy_ctx* ctx, const dsy_sim_config* cfg, const uint8_t* d_ublob, const uint64_t* d_uoff,
+                    const uint32_t* d_bits, const uint8_t* d_claims, uint64_t n_claims, uint8_t* d_out,
+                    const uint32_t* h_offsets, uint32_t n_ranks, uint64_t* out_tested);
+/* store the received packets (each requester gets exactly one response per round) */
+int dsy_sim_merge(dsy_ctx* ctx, const dsy_sim_config* cfg, uint32_t* d_bits, const uint8_t* d_resps, uint64_t n_resps);
+/* out[0] = packets held by this rank's peers, out[1] = order-independent checksum of their stores */
+int dsy_sim_stats(dsy_ctx* ctx, const dsy_sim_config* cfg, const uint32_t* d_bits, uint64_t* out);
+
 #ifdef __cplusplus
 }
 #endif

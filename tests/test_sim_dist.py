@@ -1,0 +1,69 @@
+"""The epidemic simulator's multi-rank path (block-sharded peers, two all-to-all(v) exchanges per round) on CPU:
+world_size 2 over gloo with the oracle CPU engine must reproduce world_size 1 exactly."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from dispersy_amd.sim import EpidemicSim, make_config, make_universe
+from oracle.sim_ref import OracleEngine
+
+P, U, INITIAL, ROUNDS = 240, 600, 12, 4
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def run_sim(rank, world, dist_mod=None, byte_limit=2000):
+    blob, offs = make_universe(U, seed=3)
+    cfg = make_config(P, U, rank, world, bits=2048, error_rate=0.01, byte_limit=byte_limit, seed=5)
+    eng = OracleEngine(cfg, blob, offs)
+    eng.seed(INITIAL)
+    sim = EpidemicSim(eng, cfg, rank, world, dist_mod, torch.device("cpu"))
+    history = [sim.global_stats()]
+    for r in range(ROUNDS):
+        sim.round(r)
+        history.append(sim.global_stats())
+    return history
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        h = run_sim(rank, world, dist)
+        if rank == 0:
+            q.put(h)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_equal_one():
+    single = run_sim(0, 1)
+    assert single[-1][0] > single[0][0]  # packets spread
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == single
+
+
+def test_sim_config_matches_community_filter():
+    cfg = make_config(1_000_000, 10_000, 0, 8)
+    assert (cfg.m_bits, cfg.k, cfg.hash_kind, cfg.chunk_bytes) == (10160, 7, 0, 2)  # MD5 MTU filter
+    assert cfg.capacity == 1059
+    assert cfg.peers_per_rank == 125_000 and cfg.peer_end == 125_000
