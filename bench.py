@@ -50,6 +50,11 @@ def parse():
     ap.add_argument("--sim-initial", type=int, default=100)
     ap.add_argument("--sim-rounds", type=int, default=10)
     ap.add_argument("--sim-warmup", type=int, default=2)
+    ap.add_argument("--extra", default="1,3,4,5",
+                    help="BASELINE configs measured beside the headline (config 2): 1 single filter, 3 gossip "
+                         "simulator, 4 large filters, 5 heavy-tailed packets; '' for none")
+    ap.add_argument("--large-keys", type=int, default=100_000_000, help="config 4: keys added per filter")
+    ap.add_argument("--large-tests", type=int, default=10_000_000, help="config 4: keys tested per filter")
     return ap.parse_args()
 
 
@@ -173,7 +178,7 @@ def main():
     avg_s = kt["ms"] / 1e3 / launches
     pairs_per_launch = total_pairs / max(args.steps, 1) / max(world, 1)
     blocks_per_launch = kt["blocks"] / launches
-    bytes_per_launch = kt["bytes"] / launches + pairs_per_launch * 25  # packet bytes + offsets/row/flag per pair
+    bytes_per_launch = kt["bytes"] / launches + pairs_per_launch * 17  # packet bytes + 16 B task record + miss flag
     hash_name = cap_probe.hash_name
     roofline = {
         "kernel": "k_pair_test<%s>" % hash_name,
@@ -198,18 +203,40 @@ def main():
         with open(traffic_file) as f:
             roofline["traffic"] = json.load(f).get("hbm_bytes_per_launch")
 
-    gossip = None
-    if args.sim_peers > 0:
-        gossip = gossip_sim(args, ctx, dev, rank, world, dist)
+    work = ctx.work(_native.TIME_PAIR_TEST)  # the timed steps only (reset before them)
+    useful = work["useful_pairs"]
+    roofline["lane_utilization"] = round(work["blocks"] / max(work["lane_slots"], 1), 4)
+    if dist:
+        u = torch.tensor([useful], device=dev, dtype=torch.int64)
+        dist.all_reduce(u, op=dist.ReduceOp.SUM)
+        useful = int(u.item())
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_claims > 0:
         cpu = cpu_baseline(args, ctx, lib, store, reqs, claims, blob, offsets, total_bytes, N, fblob)
 
+    extra = set(x for x in args.extra.split(",") if x)
+
+    gossip = None
+    if "3" in extra and args.sim_peers > 0:
+        gossip = gossip_sim(args, ctx, dev, rank, world, dist)
+    single = large = heavy = None
+    if "1" in extra:
+        single = single_filter(args, ctx, lib, blob, offsets, N, dev, rank, world)
+    if "5" in extra:
+        heavy = heavy_tail(args, ctx, lib, dev, rank, world, dist)
+    if "4" in extra:
+        lib.dsy_store_free(store)
+        store = None
+        del blob_full, blob, offsets, gt, meta, d_filters
+        torch.cuda.empty_cache()
+        large = large_filter(args, ctx, lib, dev, rank, world)
+
+
     if rank == 0:
         line = {
             "metric": "packets hashed+tested/sec",
-            "value": round(total_pairs / elapsed, 1),
+            "value": round(useful / elapsed, 1),
             "unit": "packets/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -226,12 +253,20 @@ def main():
                                       args.byte_limit),
                        "stored_packets": N, "claims_per_gpu": R, "pairs_per_step_per_gpu": int(pairs_per_launch),
                        "parallelism": "claims sharded over %d GPU(s), store replicated" % world},
+            "value_counts": "(claim, packet) pairs the reference hashes+tests for these claims: its lazy not_filter "
+                            "stops at the packet that spends the 5 KiB budget (community.py:2559-2567)",
+            "pairs_hashed_per_s": round(total_pairs / elapsed, 1),
+            "claims_per_s": round(R * world * args.steps / elapsed, 1),
             "roofline": roofline,
             "cpu_baseline": cpu,
             "gossip_sim": gossip,
+            "single_filter": single,
+            "large_filter": large,
+            "heavy_tail": heavy,
         }
         print(json.dumps(line))
-    lib.dsy_store_free(store)
+    if store is not None:
+        lib.dsy_store_free(store)
     if dist:
         dist.destroy_process_group()
 
@@ -273,6 +308,273 @@ def gossip_sim(args, ctx, dev, rank, world, dist):
                        "filter": "m=%d k=%d md5" % (cfg.m_bits, cfg.k), "byte_limit": cfg.byte_limit},
             "packets_held_start": held0, "packets_held_end": held, "store_checksum": "%016x" % chk,
             "exchange_bytes_rank0": sim.exchanged_bytes}
+
+
+def _blocks(lengths, plen, hash_name):
+    """Compression blocks of prefix || key per key (SURVEY §8 conventions): floor((p+L+8)/64)+1, or /128 with a
+    16-byte length field for SHA-384/512."""
+    blk, lb = (128, 16) if hash_name in ("sha384", "sha512") else (64, 8)
+    return int(((lengths + plen + lb) // blk + 1).sum().item())
+
+
+def _timed_bloom(ctx, fn, reps):
+    """Run fn() reps times on the ctx stream with HIP-event timing of the bloom kernel class; returns (avg kernel
+    seconds, wall seconds per rep)."""
+    ctx.synchronize()
+    ctx.reset_timing()
+    ctx.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    ctx.synchronize()
+    wall = (time.perf_counter() - t0) / reps
+    ctx.set_timing(False)
+    kt = ctx.kernel_time(_native.TIME_BLOOM)
+    return kt["ms"] / 1e3 / max(kt["launches"], 1), wall
+
+
+def single_filter(args, ctx, lib, blob, offsets, N, dev, rank, world):
+    """BASELINE config 1 at GPU scale: BloomFilter(10160, 0.01, 4-byte prefix) (MD5, k=7) and the reference's test
+    filter BloomFilter(4096, 0.001, b"x") (SHA-1, k=10, tests/debugcommunity/node.py:617): add 100 k packets, then
+    test all N packets of the config-2 store (already in HBM) -- dsy_bloom_add_dev / dsy_bloom_test_dev."""
+    import torch
+    from dispersy_amd.bloomfilter import BloomFilter
+    n_add = min(100_000, N)
+    lengths = offsets[1:] - offsets[:-1]
+    out = {}
+    present = torch.empty(N, dtype=torch.uint8, device=dev)
+    for name, m, f, prefix in (("md5", 10160, 0.01, b"\x00\x01\x02\x03"), ("sha1", 4096, 0.001, b"x")):
+        bf = BloomFilter(m, f, prefix)
+        assert bf.hash_name == name
+        filt = torch.zeros(int(lib.dsy_filter_words(m)), dtype=torch.int32, device=dev)
+        add = lambda: _native.check(lib.dsy_bloom_add_dev(ctx.handle, ctypes.byref(bf.params), blob.data_ptr(),  # noqa: E731
+                                                          offsets.data_ptr(), n_add, filt.data_ptr()))
+        test = lambda: _native.check(lib.dsy_bloom_test_dev(ctx.handle, ctypes.byref(bf.params), blob.data_ptr(),  # noqa: E731
+                                                            offsets.data_ptr(), N, filt.data_ptr(), present.data_ptr()))
+        add()
+        test()  # warm-up
+        k_add, _ = _timed_bloom(ctx, add, 3)
+        k_test, wall = _timed_bloom(ctx, test, 5)
+        blocks = _blocks(lengths, len(prefix), name)
+        nbytes = int(lengths.sum().item())
+        ops = blocks * OPS_PER_BLOCK[name]
+        out[name] = {
+            "filter": "BloomFilter(%d, %g, prefix=%r): %s k=%d" % (m, f, prefix, name, bf.functions),
+            "add_keys_per_s": round(n_add / k_add, 1), "test_keys": N,
+            "test_keys_per_s": round(N / k_test, 1), "test_wall_keys_per_s": round(N / wall, 1),
+            "present_fraction": round(float(present.float().mean().item()), 4),
+            "roofline_test": {"kernel": "k_bloom_test<%s>" % name, "avg_launch_us": round(k_test * 1e6, 1),
+                              "gblocks_per_s": round(blocks / k_test / 1e9, 2),
+                              "hbm": {"achieved": round((nbytes + 16 * N + N) / k_test / 1e9, 1), "peak": PEAK_HBM_GBS,
+                                      "unit": "GB/s", "frac": round((nbytes + 17 * N) / k_test / 1e9 / PEAK_HBM_GBS, 4)},
+                              "valu_int32": {"achieved": round(ops / k_test / 1e12, 2), "peak": PEAK_INT32_TOPS,
+                                             "unit": "Tops/s", "frac": round(ops / k_test / 1e12 / PEAK_INT32_TOPS, 4),
+                                             "ops_per_block": OPS_PER_BLOCK[name]}},
+        }
+    if rank == 0 and world == 1:
+        out["cpu_baseline"] = single_filter_cpu(blob, offsets)
+    return out
+
+
+def single_filter_cpu(blob, offsets):
+    """oracle/bloom_ref (hashlib + Python int bit array, one core) on a bounded sample of the same packets."""
+    from oracle.bloom_ref import OracleBloom
+    n_add, n_test = 20_000, 200_000
+    end = int(offsets[n_test].item())
+    host = bytes(blob[:end].cpu().numpy())
+    off = offsets[:n_test + 1].cpu().numpy()
+    keys = [host[int(off[i]):int(off[i + 1])] for i in range(n_test)]
+    res = {}
+    for name, m, f, prefix in (("md5", 10160, 0.01, b"\x00\x01\x02\x03"), ("sha1", 4096, 0.001, b"x")):
+        ob = OracleBloom.from_m_f(m, f, prefix)
+        t0 = time.perf_counter()
+        ob.add_keys(keys[:n_add])
+        t1 = time.perf_counter()
+        hits = sum(1 for k in keys if k in ob)
+        t2 = time.perf_counter()
+        res[name] = {"add_keys_per_s": round(n_add / (t1 - t0), 1), "test_keys_per_s": round(n_test / (t2 - t1), 1),
+                     "present": hits}
+    return {"kind": "port", "cores": 1, "sample": "%d adds + %d tests of the same packets per filter" % (n_add, n_test),
+            "results": res}
+
+
+def large_filter(args, ctx, lib, dev, rank, world):
+    """BASELINE config 4: BloomFilter(2**b, 0.01, b"\x07") for b in (20, 22, 24) -- SHA-256, 'L' chunks, k=7 --
+    filled with --large-keys packets (100-1500 B, seed 99, generated in HBM) and probed with --large-tests other
+    packets.  The filters (128 KB - 2 MB) exceed LDS: the build ORs bits into the L2/HBM-resident array."""
+    import torch
+    from dispersy_amd.bloomfilter import BloomFilter
+    G = _native.BLOB_GUARD
+    n_add, n_test = args.large_keys, args.large_tests
+    n = n_add + n_test
+    g = torch.Generator(device=dev)
+    g.manual_seed(99 + 1000 * rank)
+    lengths = torch.randint(100, 1501, (n,), device=dev, generator=g, dtype=torch.int64)
+    offsets = torch.zeros(n + 1, device=dev, dtype=torch.int64)
+    torch.cumsum(lengths, 0, out=offsets[1:])
+    total = int(offsets[-1].item())
+    blob_full = torch.randint(0, 256, (total + 2 * G,), device=dev, generator=g, dtype=torch.uint8)
+    blob = blob_full[G:]
+    test_off = offsets[n_add:]
+    present = torch.empty(n_test, dtype=torch.uint8, device=dev)
+    out = {"keys_added": n_add, "keys_tested": n_test, "key_bytes_added": int(offsets[n_add].item()), "filters": {}}
+    add_blocks = _blocks(lengths[:n_add], 1, "sha256")
+    test_blocks = _blocks(lengths[n_add:], 1, "sha256")
+    for bits in (20, 22, 24):
+        m = 1 << bits
+        bf = BloomFilter(m, 0.01, b"\x07")
+        filt = torch.zeros(int(lib.dsy_filter_words(m)), dtype=torch.int32, device=dev)
+        add = lambda: _native.check(lib.dsy_bloom_add_dev(ctx.handle, ctypes.byref(bf.params), blob.data_ptr(),  # noqa: E731
+                                                          offsets.data_ptr(), n_add, filt.data_ptr()))
+        test = lambda: _native.check(lib.dsy_bloom_test_dev(ctx.handle, ctypes.byref(bf.params), blob.data_ptr(),  # noqa: E731
+                                                            test_off.data_ptr(), n_test, filt.data_ptr(),
+                                                            present.data_ptr()))
+        filt.zero_()
+        k_add, _ = _timed_bloom(ctx, add, 1)
+        k_test, _ = _timed_bloom(ctx, test, 3)
+        ones = int(torch.bitwise_count(filt).sum().item()) if hasattr(torch, "bitwise_count") else None
+        out["filters"]["2^%d" % bits] = {
+            "hash": "%s k=%d chunk=%d" % (bf.hash_name, bf.functions, bf.chunk_bytes),
+            "add_keys_per_s": round(n_add / k_add, 1), "add_ms": round(k_add * 1e3, 2),
+            "add_gblocks_per_s": round(add_blocks / k_add / 1e9, 2),
+            "add_valu_frac": round(add_blocks * OPS_PER_BLOCK["sha256"] / k_add / 1e12 / PEAK_INT32_TOPS, 4),
+            "test_keys_per_s": round(n_test / k_test, 1), "test_ms": round(k_test * 1e3, 2),
+            "test_gblocks_per_s": round(test_blocks / k_test / 1e9, 2),
+            "bits_set": ones, "present_fraction": round(float(present.float().mean().item()), 4),
+        }
+    if rank == 0 and world == 1:
+        out["cpu_baseline"] = large_filter_cpu(blob, offsets)
+    del blob_full, blob, offsets, lengths
+    torch.cuda.empty_cache()
+    return out
+
+
+def large_filter_cpu(blob, offsets):
+    """oracle/bloom_ref at m = 2^20 (hashlib + Python int bit array: O(m) per set bit, the reference's cost
+    model), one core, on 3000 adds and 20000 tests of the same packets."""
+    from oracle.bloom_ref import OracleBloom
+    n_add, n_test = 3000, 20000
+    end = int(offsets[n_add + n_test].item())
+    host = bytes(blob[:end].cpu().numpy())
+    off = offsets[:n_add + n_test + 1].cpu().numpy()
+    keys = [host[int(off[i]):int(off[i + 1])] for i in range(n_add + n_test)]
+    ob = OracleBloom.from_m_f(1 << 20, 0.01, b"\x07")
+    t0 = time.perf_counter()
+    ob.add_keys(keys[:n_add])
+    t1 = time.perf_counter()
+    sum(1 for k in keys[n_add:] if k in ob)
+    t2 = time.perf_counter()
+    return {"kind": "port", "cores": 1, "filter": "2^20",
+            "sample": "%d adds + %d tests, extrapolated per key" % (n_add, n_test),
+            "add_keys_per_s": round(n_add / (t1 - t0), 1), "test_keys_per_s": round(n_test / (t2 - t1), 1)}
+
+
+def heavy_tail(args, ctx, lib, dev, rank, world, dist):
+    """BASELINE config 5: one responder, 10 M packets with discretised Pareto(1.2) lengths clipped to [60, 65476]
+    (the UDP cap, endpoint.py:263) and Zipf(1.1) global times over 1..10^6, serving 1024 claims as in config 2.
+    Rows sharing a global time are many (gt = 1 holds ~9 %), so claims vary from a few hundred to ~10^6 rows."""
+    import torch
+    from dispersy_amd.bloomfilter import BloomFilter
+    G = _native.BLOB_GUARD
+    N, R = args.packets, args.claims
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    u = torch.rand(N, device=dev, generator=g, dtype=torch.float64)
+    lengths = torch.clamp(torch.floor(60.0 * u.pow(-1.0 / 1.2)), max=65476).to(torch.int64)
+    del u
+    offsets = torch.zeros(N + 1, device=dev, dtype=torch.int64)
+    torch.cumsum(lengths, 0, out=offsets[1:])
+    total = int(offsets[-1].item())
+    blob_full = torch.randint(0, 256, (total + 2 * G,), device=dev, generator=g, dtype=torch.uint8)
+    blob = blob_full[G:]
+    G_MAX = 1_000_000
+    w = torch.arange(1, G_MAX + 1, device=dev, dtype=torch.float64).pow(-1.1)
+    cdf = torch.cumsum(w, 0)
+    cdf /= cdf[-1].clone()
+    gt = torch.searchsorted(cdf, torch.rand(N, device=dev, generator=g, dtype=torch.float64)) + 1
+    gt = torch.clamp(gt, max=G_MAX).sort().values.contiguous()
+    meta = torch.ones(N, device=dev, dtype=torch.int32)
+    torch.cuda.synchronize()
+    store = ctypes.c_void_p()
+    _native.check(lib.dsy_store_attach(ctx.handle, blob.data_ptr(), total, offsets.data_ptr(), N, gt.data_ptr(),
+                                       meta.data_ptr(), None, ctypes.byref(store)))
+    h_gt = gt.cpu().numpy()
+    # row range of every distinct global time (for residue-class selection without scanning 10 M rows per claim)
+    starts = np.searchsorted(h_gt, np.arange(1, G_MAX + 2, dtype=np.int64), side="left")
+    rng = np.random.Generator(np.random.PCG64(5 + 1000 * rank))
+    cap = BloomFilter(args.filter_bits, args.error_rate).get_capacity(args.error_rate)
+    modulo_m = int(math.ceil(N / float(cap)))
+    reqs = (_native.Request * R)()
+    filters, off, sel_rows = [], 0, 0
+    for i in range(R):
+        if i % 2 == 0:
+            a = int(rng.integers(0, N))
+            lo, hi = int(h_gt[a]), int(h_gt[min(a + cap - 1, N - 1)])
+            modulo, offset = 1, 0
+            rows = np.arange(starts[lo - 1], starts[hi], dtype=np.uint64)
+        else:
+            lo, hi, modulo = 1, G_MAX, modulo_m
+            offset = int(rng.integers(0, modulo))
+            first = (modulo - offset) % modulo or modulo
+            gs = np.arange(first, G_MAX + 1, modulo, dtype=np.int64)
+            rows = np.concatenate([np.arange(starts[x - 1], starts[x], dtype=np.uint64) for x in gs]) if len(gs) \
+                else np.zeros(0, dtype=np.uint64)
+        sel_rows += len(rows)
+        prefix = bytes([int(rng.integers(0, 256))])
+        bf = BloomFilter(args.filter_bits, args.error_rate, prefix)
+        known = np.ascontiguousarray(rows[rng.random(len(rows)) >= 0.01])
+        buf = ctypes.create_string_buffer(bf.bytes, len(bf.bytes))
+        if len(known):
+            _native.check(lib.dsy_bloom_add_rows(ctx.handle, ctypes.byref(bf.params), store, known.ctypes.data,
+                                                 len(known), buf))
+        raw = buf.raw + b"\x00" * ((-len(buf.raw)) % 4)
+        q = reqs[i]
+        q.time_low, q.time_high, q.modulo, q.offset = lo, hi, modulo, offset
+        q.filter_offset, q.m_bits, q.k = off, bf.size, bf.functions
+        q.hash_kind, q.chunk_bytes = _native.HASH_KINDS[bf.hash_name], bf.chunk_bytes
+        q.prefix_len = 1
+        q.prefix[0] = prefix[0]
+        filters.append(raw)
+        off += len(raw)
+    d_filters = torch.frombuffer(bytearray(b"".join(filters) + bytes(64)), dtype=torch.uint8).to(dev)
+    metas = (_native.Meta * 1)()
+    metas[0].meta_id, metas[0].direction = 1, _native.DSY_ASC
+    p_out, p_off, pairs = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+
+    def step():
+        _native.check(lib.dsy_sync_respond_dev(ctx.handle, store, reqs, R, d_filters.data_ptr(), metas, 1, G_MAX, 0,
+                                               args.byte_limit, 99, ctypes.byref(p_out), ctypes.byref(p_off),
+                                               ctypes.byref(pairs)))
+    step()
+    steps = max(3, args.steps // 4)
+    ctx.synchronize()
+    ctx.reset_timing()
+    ctx.set_timing(True)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    hashed = 0
+    for _ in range(steps):
+        step()
+        hashed += pairs.value
+    ctx.synchronize()
+    dt = time.perf_counter() - t0
+    ctx.set_timing(False)
+    kt = ctx.kernel_time(_native.TIME_PAIR_TEST)
+    work = ctx.work(_native.TIME_PAIR_TEST)
+    lib.dsy_store_free(store)
+    out = {"metric": "packets hashed+tested/sec", "value": round(work["useful_pairs"] / dt, 1), "unit": "packets/s",
+           "pairs_hashed_per_s": round(hashed / dt, 1), "ms_per_step": round(dt / steps * 1e3, 3), "steps": steps,
+           "stored_packets": N, "stored_bytes": total, "mean_packet_bytes": round(total / N, 1),
+           "max_packet_bytes": int(lengths.max().item()), "selected_rows_per_step": int(sel_rows),
+           "lane_utilization": round(work["blocks"] / max(work["lane_slots"], 1), 4),
+           "pair_test": {"avg_launch_us": round(kt["ms"] * 1e3 / max(kt["launches"], 1), 1),
+                         "launches_per_step": round(kt["launches"] / steps, 1),
+                         "gblocks_per_s": round(work["blocks"] / (kt["ms"] / 1e3) / 1e9, 2) if kt["ms"] else None,
+                         "hbm_gbs": round(work["bytes"] / (kt["ms"] / 1e3) / 1e9, 1) if kt["ms"] else None}}
+    del blob_full, blob, offsets, lengths, gt, meta, d_filters
+    torch.cuda.empty_cache()
+    return out
 
 
 def cpu_baseline(args, ctx, lib, store, reqs, claims, blob, offsets, total_bytes, N, fblob):

@@ -70,6 +70,7 @@ SIGNATURES = {
     "dsy_ctx_set_timing": (ctypes.c_int, [_P, ctypes.c_int]),
     "dsy_ctx_kernel_time": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), _PU64, _PU64, _PU64]),
     "dsy_ctx_reset_timing": (ctypes.c_int, [_P]),
+    "dsy_ctx_work": (ctypes.c_int, [_P, ctypes.c_int, _PU64]),
     "dsy_bloom_add": (ctypes.c_int, [_P, ctypes.POINTER(BloomParams), _P, _U64, _P, _U64, _P]),
     "dsy_bloom_test": (ctypes.c_int, [_P, ctypes.POINTER(BloomParams), _P, _U64, _P, _U64, _P, _P]),
     "dsy_bloom_indices": (ctypes.c_int, [_P, ctypes.POINTER(BloomParams), _P, _U64, _P, _U64, _P]),
@@ -182,6 +183,12 @@ class Context(object):
         check(self.lib.dsy_ctx_kernel_time(self.handle, which, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(blocks),
                                            ctypes.byref(nbytes)))
         return dict(ms=ms.value, launches=n.value, blocks=blocks.value, bytes=nbytes.value)
+
+    def work(self, which):
+        """Algorithmic work counters of a timer class (dsy_ctx_work)."""
+        out = (ctypes.c_uint64 * 4)()
+        check(self.lib.dsy_ctx_work(self.handle, which, out))
+        return dict(blocks=out[0], bytes=out[1], useful_pairs=out[2], lane_slots=out[3])
 
     # ---- single filter
     @staticmethod

@@ -64,6 +64,8 @@ struct dsy_ctx {
     uint64_t launches[kTimeClasses] = {0, 0, 0, 0};
     uint64_t blocks[kTimeClasses] = {0, 0, 0, 0};
     uint64_t bytes[kTimeClasses] = {0, 0, 0, 0};
+    uint64_t useful[kTimeClasses] = {0, 0, 0, 0};  // pairs the reference would have hashed (responder)
+    uint64_t slots[kTimeClasses] = {0, 0, 0, 0};   // lane-block slots of the hashing waves (load balance)
     void* pinned = nullptr;  // small pinned staging for flags/counters
 };
 
@@ -333,7 +335,18 @@ int dsy_ctx_reset_timing(dsy_ctx* c) {
     Guard g(c);
     HIP_TRY(hipStreamSynchronize(c->stream));
     timers_collect(c);
-    for (int i = 0; i < kTimeClasses; ++i) c->time_ms[i] = 0, c->launches[i] = 0, c->blocks[i] = 0, c->bytes[i] = 0;
+    for (int i = 0; i < kTimeClasses; ++i)
+        c->time_ms[i] = 0, c->launches[i] = 0, c->blocks[i] = 0, c->bytes[i] = 0, c->useful[i] = 0, c->slots[i] = 0;
+    return DSY_OK;
+}
+
+int dsy_ctx_work(dsy_ctx* c, int which, uint64_t* out4) {
+    if (!c || !out4 || which < 0 || which >= kTimeClasses) return fail(DSY_EINVAL, "bad ctx, output or class");
+    Guard g(c);
+    out4[0] = c->blocks[which];
+    out4[1] = c->bytes[which];
+    out4[2] = c->useful[which];
+    out4[3] = c->slots[which];
     return DSY_OK;
 }
 
@@ -630,8 +643,8 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     if ((rc = ws_get(c, "upper", std::max<size_t>(R, 1) * 8, &d_upper))) return rc;
     if ((rc = ws_get(c, "pairs", std::max<size_t>((size_t)R * W, 1) * 8, &d_pairs))) return rc;
     if ((rc = ws_get(c, "miss", std::max<size_t>((size_t)R * W, 1), &d_miss))) return rc;
-    void* d_perm;
-    if ((rc = ws_get(c, "perm", std::max<size_t>((size_t)R * W, 1) * 4, &d_perm))) return rc;
+    void* d_task;
+    if ((rc = ws_get(c, "task", std::max<size_t>((size_t)R * W, 1) * sizeof(PairTask), &d_task))) return rc;
     if ((rc = ws_get(c, "flags", 64, &d_flags))) return rc;
     if ((rc = ws_get(c, "total", 64, &d_total))) return rc;
     if ((rc = ws_get(c, "lists", std::max<size_t>(R, 1) * 4, &d_lists))) return rc;
@@ -670,10 +683,9 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     L.upper = (uint64_t*)d_upper;
     L.pair_row = (uint64_t*)d_pairs;
     L.miss = (uint8_t*)d_miss;
-    L.perm = (uint32_t*)d_perm;
+    L.task = (PairTask*)d_task;
     L.flags = (uint32_t*)d_flags;
-    L.total_pairs = (uint64_t*)d_total;
-    L.total_blocks = (uint64_t*)d_total + 1;
+    L.counters = (uint64_t*)d_total;
     L.stream = c->stream;
 
     PendingTimer t;
@@ -726,7 +738,7 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
         HIP_TRY(launch_compact(L));
         timer_end(c, &t);
         HIP_TRY(hipMemcpyAsync(h_flags, d_flags, 8, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipMemcpyAsync(h_tot, d_total, 24, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(h_tot, d_total, kCntN * 8, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
         // capacity overflow can only come from a wrong min_len bound; report it loudly
         if (h_flags[1]) return fail(DSY_ECAPACITY, "internal: a claim overflowed its output capacity");
@@ -737,9 +749,11 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     if ((rc = ws_get(c, "packed_off", ((size_t)R + 1) * 8, &d_packed_off_v))) return rc;
     HIP_TRY(launch_pack(L, (uint64_t*)d_packed_v, (uint64_t*)d_packed_off_v, nullptr));
     timers_collect(c);
-    c->blocks[kTimePairTest] += h_tot[1];
-    c->bytes[kTimePairTest] += h_tot[2];
-    *total_pairs = h_tot[0];
+    c->blocks[kTimePairTest] += h_tot[kCntBlocks];
+    c->bytes[kTimePairTest] += h_tot[kCntBytes];
+    c->useful[kTimePairTest] += h_tot[kCntUseful];
+    c->slots[kTimePairTest] += h_tot[kCntSlots];
+    *total_pairs = h_tot[kCntPairs];
     *d_packed = (uint64_t*)d_packed_v;
     *d_packed_off = (uint64_t*)d_packed_off_v;
     return DSY_OK;

@@ -19,6 +19,24 @@ __device__ __forceinline__ uint64_t rotr64(uint64_t x, uint32_t s) { return (x >
 __device__ __forceinline__ uint32_t sel32(uint32_t m, uint32_t a, uint32_t b) { return b ^ (m & (a ^ b)); }
 __device__ __forceinline__ uint64_t sel64(uint64_t m, uint64_t a, uint64_t b) { return b ^ (m & (a ^ b)); }
 
+// CDNA4's v_bitop3_b32: any boolean function of three operands in ONE full-rate instruction (tools/valupeak:
+// v_bitop3_b32 issues at the v_xor_b32 rate, while the three-operand v_bfi_b32 / v_add3_u32 / v_alignbit_b32
+// issue at half of it).  The truth table is indexed the usual way: operand 0 <-> 0xF0, 1 <-> 0xCC, 2 <-> 0xAA.
+template <uint32_t LUT>
+__device__ __forceinline__ uint32_t bop3(uint32_t a, uint32_t b, uint32_t c) {
+    return (uint32_t)__builtin_amdgcn_bitop3_b32((int)a, (int)b, (int)c, LUT);
+}
+template <uint32_t LUT>
+__device__ __forceinline__ uint64_t bop3_64(uint64_t a, uint64_t b, uint64_t c) {
+    return ((uint64_t)bop3<LUT>((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)) << 32) |
+           bop3<LUT>((uint32_t)a, (uint32_t)b, (uint32_t)c);
+}
+constexpr uint32_t kXor3 = 0xF0 ^ 0xCC ^ 0xAA;                   // a ^ b ^ c
+constexpr uint32_t kCh = (0xF0 & 0xCC) | (~0xF0 & 0xAA & 0xFF);    // a ? b : c   (MD5 F, SHA Ch)
+constexpr uint32_t kMaj = (0xF0 & 0xCC) | (0xF0 & 0xAA) | (0xCC & 0xAA);
+constexpr uint32_t kMd5G = (0xF0 & 0xAA) | (0xCC & ~0xAA & 0xFF);  // (b & d) | (c & ~d)
+constexpr uint32_t kMd5I = (0xCC ^ (0xF0 | (~0xAA & 0xFF))) & 0xFF; // c ^ (b | ~d)
+
 // --------------------------------------------------------------------------------------------------- MD5
 struct Md5 {
     static constexpr int kind = 0;
@@ -36,74 +54,74 @@ struct Md5 {
     __device__ __forceinline__ void compress(const uint32_t* m) {
         uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
 #define DSY_MD5_STEP(f, a, b, c, d, x, k, s) a = b + rotl32(a + (f) + (x) + (k), s)
-        // round 1: F = sel(b, c, d)
-        DSY_MD5_STEP(sel32(b, c, d), a, b, c, d, m[0], 0xd76aa478u, 7);
-        DSY_MD5_STEP(sel32(a, b, c), d, a, b, c, m[1], 0xe8c7b756u, 12);
-        DSY_MD5_STEP(sel32(d, a, b), c, d, a, b, m[2], 0x242070dbu, 17);
-        DSY_MD5_STEP(sel32(c, d, a), b, c, d, a, m[3], 0xc1bdceeeu, 22);
-        DSY_MD5_STEP(sel32(b, c, d), a, b, c, d, m[4], 0xf57c0fafu, 7);
-        DSY_MD5_STEP(sel32(a, b, c), d, a, b, c, m[5], 0x4787c62au, 12);
-        DSY_MD5_STEP(sel32(d, a, b), c, d, a, b, m[6], 0xa8304613u, 17);
-        DSY_MD5_STEP(sel32(c, d, a), b, c, d, a, m[7], 0xfd469501u, 22);
-        DSY_MD5_STEP(sel32(b, c, d), a, b, c, d, m[8], 0x698098d8u, 7);
-        DSY_MD5_STEP(sel32(a, b, c), d, a, b, c, m[9], 0x8b44f7afu, 12);
-        DSY_MD5_STEP(sel32(d, a, b), c, d, a, b, m[10], 0xffff5bb1u, 17);
-        DSY_MD5_STEP(sel32(c, d, a), b, c, d, a, m[11], 0x895cd7beu, 22);
-        DSY_MD5_STEP(sel32(b, c, d), a, b, c, d, m[12], 0x6b901122u, 7);
-        DSY_MD5_STEP(sel32(a, b, c), d, a, b, c, m[13], 0xfd987193u, 12);
-        DSY_MD5_STEP(sel32(d, a, b), c, d, a, b, m[14], 0xa679438eu, 17);
-        DSY_MD5_STEP(sel32(c, d, a), b, c, d, a, m[15], 0x49b40821u, 22);
-        // round 2: G = sel(d, b, c)
-        DSY_MD5_STEP(sel32(d, b, c), a, b, c, d, m[1], 0xf61e2562u, 5);
-        DSY_MD5_STEP(sel32(c, a, b), d, a, b, c, m[6], 0xc040b340u, 9);
-        DSY_MD5_STEP(sel32(b, d, a), c, d, a, b, m[11], 0x265e5a51u, 14);
-        DSY_MD5_STEP(sel32(a, c, d), b, c, d, a, m[0], 0xe9b6c7aau, 20);
-        DSY_MD5_STEP(sel32(d, b, c), a, b, c, d, m[5], 0xd62f105du, 5);
-        DSY_MD5_STEP(sel32(c, a, b), d, a, b, c, m[10], 0x02441453u, 9);
-        DSY_MD5_STEP(sel32(b, d, a), c, d, a, b, m[15], 0xd8a1e681u, 14);
-        DSY_MD5_STEP(sel32(a, c, d), b, c, d, a, m[4], 0xe7d3fbc8u, 20);
-        DSY_MD5_STEP(sel32(d, b, c), a, b, c, d, m[9], 0x21e1cde6u, 5);
-        DSY_MD5_STEP(sel32(c, a, b), d, a, b, c, m[14], 0xc33707d6u, 9);
-        DSY_MD5_STEP(sel32(b, d, a), c, d, a, b, m[3], 0xf4d50d87u, 14);
-        DSY_MD5_STEP(sel32(a, c, d), b, c, d, a, m[8], 0x455a14edu, 20);
-        DSY_MD5_STEP(sel32(d, b, c), a, b, c, d, m[13], 0xa9e3e905u, 5);
-        DSY_MD5_STEP(sel32(c, a, b), d, a, b, c, m[2], 0xfcefa3f8u, 9);
-        DSY_MD5_STEP(sel32(b, d, a), c, d, a, b, m[7], 0x676f02d9u, 14);
-        DSY_MD5_STEP(sel32(a, c, d), b, c, d, a, m[12], 0x8d2a4c8au, 20);
+        // round 1: F = (b & c) | (~b & d)
+        DSY_MD5_STEP(bop3<kCh>(b, c, d), a, b, c, d, m[0], 0xd76aa478u, 7);
+        DSY_MD5_STEP(bop3<kCh>(a, b, c), d, a, b, c, m[1], 0xe8c7b756u, 12);
+        DSY_MD5_STEP(bop3<kCh>(d, a, b), c, d, a, b, m[2], 0x242070dbu, 17);
+        DSY_MD5_STEP(bop3<kCh>(c, d, a), b, c, d, a, m[3], 0xc1bdceeeu, 22);
+        DSY_MD5_STEP(bop3<kCh>(b, c, d), a, b, c, d, m[4], 0xf57c0fafu, 7);
+        DSY_MD5_STEP(bop3<kCh>(a, b, c), d, a, b, c, m[5], 0x4787c62au, 12);
+        DSY_MD5_STEP(bop3<kCh>(d, a, b), c, d, a, b, m[6], 0xa8304613u, 17);
+        DSY_MD5_STEP(bop3<kCh>(c, d, a), b, c, d, a, m[7], 0xfd469501u, 22);
+        DSY_MD5_STEP(bop3<kCh>(b, c, d), a, b, c, d, m[8], 0x698098d8u, 7);
+        DSY_MD5_STEP(bop3<kCh>(a, b, c), d, a, b, c, m[9], 0x8b44f7afu, 12);
+        DSY_MD5_STEP(bop3<kCh>(d, a, b), c, d, a, b, m[10], 0xffff5bb1u, 17);
+        DSY_MD5_STEP(bop3<kCh>(c, d, a), b, c, d, a, m[11], 0x895cd7beu, 22);
+        DSY_MD5_STEP(bop3<kCh>(b, c, d), a, b, c, d, m[12], 0x6b901122u, 7);
+        DSY_MD5_STEP(bop3<kCh>(a, b, c), d, a, b, c, m[13], 0xfd987193u, 12);
+        DSY_MD5_STEP(bop3<kCh>(d, a, b), c, d, a, b, m[14], 0xa679438eu, 17);
+        DSY_MD5_STEP(bop3<kCh>(c, d, a), b, c, d, a, m[15], 0x49b40821u, 22);
+        // round 2: G = (b & d) | (c & ~d)
+        DSY_MD5_STEP(bop3<kMd5G>(b, c, d), a, b, c, d, m[1], 0xf61e2562u, 5);
+        DSY_MD5_STEP(bop3<kMd5G>(a, b, c), d, a, b, c, m[6], 0xc040b340u, 9);
+        DSY_MD5_STEP(bop3<kMd5G>(d, a, b), c, d, a, b, m[11], 0x265e5a51u, 14);
+        DSY_MD5_STEP(bop3<kMd5G>(c, d, a), b, c, d, a, m[0], 0xe9b6c7aau, 20);
+        DSY_MD5_STEP(bop3<kMd5G>(b, c, d), a, b, c, d, m[5], 0xd62f105du, 5);
+        DSY_MD5_STEP(bop3<kMd5G>(a, b, c), d, a, b, c, m[10], 0x02441453u, 9);
+        DSY_MD5_STEP(bop3<kMd5G>(d, a, b), c, d, a, b, m[15], 0xd8a1e681u, 14);
+        DSY_MD5_STEP(bop3<kMd5G>(c, d, a), b, c, d, a, m[4], 0xe7d3fbc8u, 20);
+        DSY_MD5_STEP(bop3<kMd5G>(b, c, d), a, b, c, d, m[9], 0x21e1cde6u, 5);
+        DSY_MD5_STEP(bop3<kMd5G>(a, b, c), d, a, b, c, m[14], 0xc33707d6u, 9);
+        DSY_MD5_STEP(bop3<kMd5G>(d, a, b), c, d, a, b, m[3], 0xf4d50d87u, 14);
+        DSY_MD5_STEP(bop3<kMd5G>(c, d, a), b, c, d, a, m[8], 0x455a14edu, 20);
+        DSY_MD5_STEP(bop3<kMd5G>(b, c, d), a, b, c, d, m[13], 0xa9e3e905u, 5);
+        DSY_MD5_STEP(bop3<kMd5G>(a, b, c), d, a, b, c, m[2], 0xfcefa3f8u, 9);
+        DSY_MD5_STEP(bop3<kMd5G>(d, a, b), c, d, a, b, m[7], 0x676f02d9u, 14);
+        DSY_MD5_STEP(bop3<kMd5G>(c, d, a), b, c, d, a, m[12], 0x8d2a4c8au, 20);
         // round 3: H = b ^ c ^ d
-        DSY_MD5_STEP(b ^ c ^ d, a, b, c, d, m[5], 0xfffa3942u, 4);
-        DSY_MD5_STEP(a ^ b ^ c, d, a, b, c, m[8], 0x8771f681u, 11);
-        DSY_MD5_STEP(d ^ a ^ b, c, d, a, b, m[11], 0x6d9d6122u, 16);
-        DSY_MD5_STEP(c ^ d ^ a, b, c, d, a, m[14], 0xfde5380cu, 23);
-        DSY_MD5_STEP(b ^ c ^ d, a, b, c, d, m[1], 0xa4beea44u, 4);
-        DSY_MD5_STEP(a ^ b ^ c, d, a, b, c, m[4], 0x4bdecfa9u, 11);
-        DSY_MD5_STEP(d ^ a ^ b, c, d, a, b, m[7], 0xf6bb4b60u, 16);
-        DSY_MD5_STEP(c ^ d ^ a, b, c, d, a, m[10], 0xbebfbc70u, 23);
-        DSY_MD5_STEP(b ^ c ^ d, a, b, c, d, m[13], 0x289b7ec6u, 4);
-        DSY_MD5_STEP(a ^ b ^ c, d, a, b, c, m[0], 0xeaa127fau, 11);
-        DSY_MD5_STEP(d ^ a ^ b, c, d, a, b, m[3], 0xd4ef3085u, 16);
-        DSY_MD5_STEP(c ^ d ^ a, b, c, d, a, m[6], 0x04881d05u, 23);
-        DSY_MD5_STEP(b ^ c ^ d, a, b, c, d, m[9], 0xd9d4d039u, 4);
-        DSY_MD5_STEP(a ^ b ^ c, d, a, b, c, m[12], 0xe6db99e5u, 11);
-        DSY_MD5_STEP(d ^ a ^ b, c, d, a, b, m[15], 0x1fa27cf8u, 16);
-        DSY_MD5_STEP(c ^ d ^ a, b, c, d, a, m[2], 0xc4ac5665u, 23);
+        DSY_MD5_STEP(bop3<kXor3>(b, c, d), a, b, c, d, m[5], 0xfffa3942u, 4);
+        DSY_MD5_STEP(bop3<kXor3>(a, b, c), d, a, b, c, m[8], 0x8771f681u, 11);
+        DSY_MD5_STEP(bop3<kXor3>(d, a, b), c, d, a, b, m[11], 0x6d9d6122u, 16);
+        DSY_MD5_STEP(bop3<kXor3>(c, d, a), b, c, d, a, m[14], 0xfde5380cu, 23);
+        DSY_MD5_STEP(bop3<kXor3>(b, c, d), a, b, c, d, m[1], 0xa4beea44u, 4);
+        DSY_MD5_STEP(bop3<kXor3>(a, b, c), d, a, b, c, m[4], 0x4bdecfa9u, 11);
+        DSY_MD5_STEP(bop3<kXor3>(d, a, b), c, d, a, b, m[7], 0xf6bb4b60u, 16);
+        DSY_MD5_STEP(bop3<kXor3>(c, d, a), b, c, d, a, m[10], 0xbebfbc70u, 23);
+        DSY_MD5_STEP(bop3<kXor3>(b, c, d), a, b, c, d, m[13], 0x289b7ec6u, 4);
+        DSY_MD5_STEP(bop3<kXor3>(a, b, c), d, a, b, c, m[0], 0xeaa127fau, 11);
+        DSY_MD5_STEP(bop3<kXor3>(d, a, b), c, d, a, b, m[3], 0xd4ef3085u, 16);
+        DSY_MD5_STEP(bop3<kXor3>(c, d, a), b, c, d, a, m[6], 0x04881d05u, 23);
+        DSY_MD5_STEP(bop3<kXor3>(b, c, d), a, b, c, d, m[9], 0xd9d4d039u, 4);
+        DSY_MD5_STEP(bop3<kXor3>(a, b, c), d, a, b, c, m[12], 0xe6db99e5u, 11);
+        DSY_MD5_STEP(bop3<kXor3>(d, a, b), c, d, a, b, m[15], 0x1fa27cf8u, 16);
+        DSY_MD5_STEP(bop3<kXor3>(c, d, a), b, c, d, a, m[2], 0xc4ac5665u, 23);
         // round 4: I = c ^ (b | ~d)
-        DSY_MD5_STEP(c ^ (b | ~d), a, b, c, d, m[0], 0xf4292244u, 6);
-        DSY_MD5_STEP(b ^ (a | ~c), d, a, b, c, m[7], 0x432aff97u, 10);
-        DSY_MD5_STEP(a ^ (d | ~b), c, d, a, b, m[14], 0xab9423a7u, 15);
-        DSY_MD5_STEP(d ^ (c | ~a), b, c, d, a, m[5], 0xfc93a039u, 21);
-        DSY_MD5_STEP(c ^ (b | ~d), a, b, c, d, m[12], 0x655b59c3u, 6);
-        DSY_MD5_STEP(b ^ (a | ~c), d, a, b, c, m[3], 0x8f0ccc92u, 10);
-        DSY_MD5_STEP(a ^ (d | ~b), c, d, a, b, m[10], 0xffeff47du, 15);
-        DSY_MD5_STEP(d ^ (c | ~a), b, c, d, a, m[1], 0x85845dd1u, 21);
-        DSY_MD5_STEP(c ^ (b | ~d), a, b, c, d, m[8], 0x6fa87e4fu, 6);
-        DSY_MD5_STEP(b ^ (a | ~c), d, a, b, c, m[15], 0xfe2ce6e0u, 10);
-        DSY_MD5_STEP(a ^ (d | ~b), c, d, a, b, m[6], 0xa3014314u, 15);
-        DSY_MD5_STEP(d ^ (c | ~a), b, c, d, a, m[13], 0x4e0811a1u, 21);
-        DSY_MD5_STEP(c ^ (b | ~d), a, b, c, d, m[4], 0xf7537e82u, 6);
-        DSY_MD5_STEP(b ^ (a | ~c), d, a, b, c, m[11], 0xbd3af235u, 10);
-        DSY_MD5_STEP(a ^ (d | ~b), c, d, a, b, m[2], 0x2ad7d2bbu, 15);
-        DSY_MD5_STEP(d ^ (c | ~a), b, c, d, a, m[9], 0xeb86d391u, 21);
+        DSY_MD5_STEP(bop3<kMd5I>(b, c, d), a, b, c, d, m[0], 0xf4292244u, 6);
+        DSY_MD5_STEP(bop3<kMd5I>(a, b, c), d, a, b, c, m[7], 0x432aff97u, 10);
+        DSY_MD5_STEP(bop3<kMd5I>(d, a, b), c, d, a, b, m[14], 0xab9423a7u, 15);
+        DSY_MD5_STEP(bop3<kMd5I>(c, d, a), b, c, d, a, m[5], 0xfc93a039u, 21);
+        DSY_MD5_STEP(bop3<kMd5I>(b, c, d), a, b, c, d, m[12], 0x655b59c3u, 6);
+        DSY_MD5_STEP(bop3<kMd5I>(a, b, c), d, a, b, c, m[3], 0x8f0ccc92u, 10);
+        DSY_MD5_STEP(bop3<kMd5I>(d, a, b), c, d, a, b, m[10], 0xffeff47du, 15);
+        DSY_MD5_STEP(bop3<kMd5I>(c, d, a), b, c, d, a, m[1], 0x85845dd1u, 21);
+        DSY_MD5_STEP(bop3<kMd5I>(b, c, d), a, b, c, d, m[8], 0x6fa87e4fu, 6);
+        DSY_MD5_STEP(bop3<kMd5I>(a, b, c), d, a, b, c, m[15], 0xfe2ce6e0u, 10);
+        DSY_MD5_STEP(bop3<kMd5I>(d, a, b), c, d, a, b, m[6], 0xa3014314u, 15);
+        DSY_MD5_STEP(bop3<kMd5I>(c, d, a), b, c, d, a, m[13], 0x4e0811a1u, 21);
+        DSY_MD5_STEP(bop3<kMd5I>(b, c, d), a, b, c, d, m[4], 0xf7537e82u, 6);
+        DSY_MD5_STEP(bop3<kMd5I>(a, b, c), d, a, b, c, m[11], 0xbd3af235u, 10);
+        DSY_MD5_STEP(bop3<kMd5I>(d, a, b), c, d, a, b, m[2], 0x2ad7d2bbu, 15);
+        DSY_MD5_STEP(bop3<kMd5I>(c, d, a), b, c, d, a, m[9], 0xeb86d391u, 21);
 #undef DSY_MD5_STEP
         h[0] += a; h[1] += b; h[2] += c; h[3] += d;
     }
@@ -137,14 +155,14 @@ struct Sha1 {
             if (t < 16) {
                 x = w[t];
             } else {
-                x = rotl32(w[(t - 3) & 15] ^ w[(t - 8) & 15] ^ w[(t - 14) & 15] ^ w[t & 15], 1);
+                x = rotl32(bop3<kXor3>(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
                 w[t & 15] = x;
             }
             uint32_t f, k;
-            if (t < 20) { f = sel32(b, c, d); k = 0x5a827999u; }
-            else if (t < 40) { f = b ^ c ^ d; k = 0x6ed9eba1u; }
-            else if (t < 60) { f = (b & c) | (d & (b | c)); k = 0x8f1bbcdcu; }
-            else { f = b ^ c ^ d; k = 0xca62c1d6u; }
+            if (t < 20) { f = bop3<kCh>(b, c, d); k = 0x5a827999u; }
+            else if (t < 40) { f = bop3<kXor3>(b, c, d); k = 0x6ed9eba1u; }
+            else if (t < 60) { f = bop3<kMaj>(b, c, d); k = 0x8f1bbcdcu; }
+            else { f = bop3<kXor3>(b, c, d); k = 0xca62c1d6u; }
             uint32_t tmp = rotl32(a, 5) + f + e + k + x;
             e = d; d = c; c = rotl32(b, 30); b = a; a = tmp;
         }
@@ -191,15 +209,15 @@ struct Sha256 {
                 x = w[t];
             } else {
                 uint32_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
-                uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
-                uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
+                uint32_t s0 = bop3<kXor3>(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3);
+                uint32_t s1 = bop3<kXor3>(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10);
                 x = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
                 w[t & 15] = x;
             }
-            uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
-            uint32_t t1 = hh + S1 + sel32(e, f, g) + kSha256K[t] + x;
-            uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
-            uint32_t t2 = S0 + sel32(a ^ b, c, b);  // maj(a,b,c)
+            uint32_t S1 = bop3<kXor3>(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25));
+            uint32_t t1 = hh + S1 + bop3<kCh>(e, f, g) + kSha256K[t] + x;
+            uint32_t S0 = bop3<kXor3>(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22));
+            uint32_t t2 = S0 + bop3<kMaj>(a, b, c);
             hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
         }
         h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
@@ -266,15 +284,15 @@ struct Sha512T {
                 x = w[t];
             } else {
                 uint64_t w15 = w[(t - 15) & 15], w2 = w[(t - 2) & 15];
-                uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
-                uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
+                uint64_t s0 = bop3_64<kXor3>(rotr64(w15, 1), rotr64(w15, 8), w15 >> 7);
+                uint64_t s1 = bop3_64<kXor3>(rotr64(w2, 19), rotr64(w2, 61), w2 >> 6);
                 x = w[t & 15] + s0 + w[(t - 7) & 15] + s1;
                 w[t & 15] = x;
             }
-            uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
-            uint64_t t1 = hh + S1 + sel64(e, f, g) + kSha512K[t] + x;
-            uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
-            uint64_t t2 = S0 + sel64(a ^ b, c, b);
+            uint64_t S1 = bop3_64<kXor3>(rotr64(e, 14), rotr64(e, 18), rotr64(e, 41));
+            uint64_t t1 = hh + S1 + bop3_64<kCh>(e, f, g) + kSha512K[t] + x;
+            uint64_t S0 = bop3_64<kXor3>(rotr64(a, 28), rotr64(a, 34), rotr64(a, 39));
+            uint64_t t2 = S0 + bop3_64<kMaj>(a, b, c);
             hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
         }
         h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;

@@ -60,6 +60,17 @@ struct Plan {
     uint32_t _pad;
 };
 
+// One (claim, packet) pair as the hashing kernel consumes it, written by k_fill in hashing order (window slots
+// sorted by block count): where the packet starts in the blob, its length, and its window slot (send order).
+struct __attribute__((aligned(16))) PairTask {
+    uint64_t off;
+    uint32_t len;
+    uint32_t slot;
+};
+
+// Work counters of the responder (device u64[8], accumulated over a call's windows).
+enum { kCntPairs = 0, kCntBlocks = 1, kCntBytes = 2, kCntUseful = 3, kCntSlots = 4, kCntN = 8 };
+
 // Per-claim window state.
 struct ReqState {
     uint32_t meta;     // current meta index
@@ -97,12 +108,12 @@ struct RespondLaunch {
     ReqState* state;          // device [R]
     uint64_t* upper;          // device [R]: upper bound of selected rows per claim
     uint64_t* pair_row;       // device [R*W]
-    uint32_t* perm;           // device [R*W]: per-claim hashing order (window slots sorted by block count)
+    PairTask* task;           // device [R*W]: per-claim hashing order (window slots sorted by block count)
     uint8_t* miss;            // device [R*W]
     uint64_t* out;            // device [sum cap]
     uint32_t* flags;          // device [4]: [0] any claim still active
-    uint64_t* total_pairs;    // device [1]
-    uint64_t* total_blocks;   // device [2]: compression blocks, packet bytes hashed (nullable)
+    uint64_t* counters;       // device [kCntN]: pairs hashed, compression blocks, packet bytes, pairs the reference
+                              // would have hashed (it stops at the byte limit), lane-block slots of the hashing waves
     hipStream_t stream;
 };
 

@@ -93,7 +93,11 @@ __device__ __forceinline__ void hash_key_generic(const KeyView& kv, H& st) {
     }
 }
 
-// Fast path for prefixes of 0..3 bytes (the wire carries exactly one, conversion.py:725,769): every block is
+// Bytes 0..r-1 of a little-endian word (r = 0..4).
+__device__ __forceinline__ uint32_t low_bytes_mask(uint32_t r) { return r >= 4 ? 0xffffffffu : (1u << (8 * r)) - 1u; }
+
+// Fast path for prefixes of 0..4 bytes (the wire carries exactly one, conversion.py:725,769; BASELINE config 1
+// uses four): every block is
 // four (eight) unaligned 16-byte loads of the key; block 0 is shifted right by the prefix length with
 // v_alignbyte and the prefix OR-ed in; the final block(s) are masked in registers (0x80 terminator, zeros,
 // bit length).  Loads of block b+1 are issued before block b is compressed (one block of software prefetch).
@@ -132,7 +136,7 @@ __device__ __forceinline__ void hash_key_short_prefix(const KeyView& kv, H& st) 
         if (b == 0 && r) {
 #pragma unroll
             for (int i = NW - 1; i >= 1; --i) w[i] = __builtin_amdgcn_alignbyte(w[i], w[i - 1], 4 - r);
-            w[0] = (w[0] << (8 * r)) | preword;
+            w[0] = (r == 4 ? 0u : (w[0] << (8 * r))) | preword;
         }
         if (o0 + BLK > total) {
 #pragma unroll
@@ -169,7 +173,7 @@ __device__ __forceinline__ void hash_key_short_prefix(const KeyView& kv, H& st) 
 // instructions; every instruction moves 64/(4S) keys x S*64 contiguous bytes, so the memory system sees whole
 // 128-byte pieces instead of 64 scattered 16-byte ones.  Within a key's LDS row the 16-byte chunks are rotated by
 // (key >> SH) so the lanes' ds_read_b128 of "chunk c of my key" hit 16 distinct 4-bank groups.  NB buffers keep
-// NB-1 stages in flight (counted vmcnt).  Requires every lane's prefix to be <= 3 bytes and DSY_BLOB_GUARD
+// NB-1 stages in flight (counted vmcnt).  Requires every lane's prefix to be <= 4 bytes and DSY_BLOB_GUARD
 // readable bytes before the first and after the last key (block 0 is fetched from key - plen).
 __device__ __forceinline__ void wait_vmcnt(int k) {
     // s_waitcnt vmcnt(k), lgkm/exp counters untouched (immediates must be compile-time constants)
@@ -244,7 +248,7 @@ __device__ __forceinline__ void hash_key_dma(const KeyView& kv, H& st, uint8_t* 
             }
             if (b < nb) {
                 const uint32_t o0 = b * 64;
-                if (b == 0 && r) w[0] = (w[0] & ~((1u << (8 * r)) - 1u)) | preword;
+                if (b == 0 && r) w[0] = (w[0] & ~low_bytes_mask(r)) | preword;
                 if (o0 + 64 > total) {
 #pragma unroll
                     for (int i = 0; i < 16; ++i) {
@@ -272,7 +276,7 @@ __device__ __forceinline__ void hash_key_dma(const KeyView& kv, H& st, uint8_t* 
 
 template <class H>
 __device__ __forceinline__ void hash_key(const KeyView& kv, H& st) {
-    if (kv.plen < 4) hash_key_short_prefix<H>(kv, st);
+    if (kv.plen <= 4) hash_key_short_prefix<H>(kv, st);
     else hash_key_generic<H>(kv, st);
 }
 

@@ -231,8 +231,9 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
         if (j >= L.J) S->exhausted = 1;
     }
     // Load balance: order this window's pairs by compression-block count (counting sort in LDS) so the 64
-    // lanes of a hashing wave run the same number of blocks.  perm[i] = window slot hashed by lane-slot i; the
-    // send order (slot order) is untouched.
+    // lanes of a hashing wave run the same number of blocks.  task[i] = the pair hashed by lane-slot i (blob
+    // offset, length, window slot), so the hashing kernel reads 16 contiguous bytes per lane and then the packet;
+    // the send order (slot order) is untouched.
     __shared__ uint32_t hist[kSortBins];
     __shared__ uint16_t keyb[kMaxWindow];
     const uint32_t blk = q.hash_kind >= DSY_SHA384 ? 128u : 64u, lenb = q.hash_kind >= DSY_SHA384 ? 16u : 8u;
@@ -255,8 +256,16 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
         }
     }
     __syncthreads();
-    uint32_t* perm = L.perm + (uint64_t)r * W;
-    for (uint64_t t = threadIdx.x; t < filled; t += kFillThreads) perm[atomicAdd(&hist[keyb[t]], 1u)] = (uint32_t)t;
+    PairTask* task = L.task + (uint64_t)r * W;
+    for (uint64_t t = threadIdx.x; t < filled; t += kFillThreads) {
+        const uint64_t row = out[t];
+        const uint64_t a = L.st.offsets[row], e = L.st.offsets[row + 1];  // just read above: cache hits
+        PairTask tk;
+        tk.off = a;
+        tk.len = (uint32_t)(e - a);
+        tk.slot = (uint32_t)t;
+        task[atomicAdd(&hist[keyb[t]], 1u)] = tk;
+    }
 }
 
 // -------------------------------------------------------------------------------------- k_pair_test
@@ -271,7 +280,7 @@ __global__ void __launch_bounds__(256) k_pair_test(RespondLaunch L, const uint32
     const uint64_t wave0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     uint8_t* my_lds = dma_lds + (threadIdx.x >> 6) * DmaGeometry<2, 2>::kWaveBytes;
-    unsigned long long acc_blocks = 0, acc_bytes = 0;  // this lane's algorithmic work, reduced once per block
+    unsigned long long acc_blocks = 0, acc_bytes = 0, acc_slots = 0;  // this lane's work, reduced once per block
     // chunk-major task order: wave-task v hashes 64-pair chunk (v / n_list) of claim (v % n_list), so the
     // non-empty chunks of every claim come first and spread evenly over the grid
     for (uint64_t wv = wave0; wv < total_waves; wv += wstride) {
@@ -285,15 +294,14 @@ __global__ void __launch_bounds__(256) k_pair_test(RespondLaunch L, const uint32
         uint32_t t = 0;
         KeyView kv{L.st.blob, 0u, q.prefix, q.prefix_len};  // idle lanes hash an empty key
         if (active) {
-            t = L.perm[(uint64_t)r * W + i];
-            const uint64_t row = L.pair_row[(uint64_t)r * W + t];
-            const uint64_t a = L.st.offsets[row], e = L.st.offsets[row + 1];
-            kv.key = L.st.blob + a;
-            kv.len = (uint32_t)(e - a);
+            const PairTask tk = L.task[(uint64_t)r * W + i];
+            t = tk.slot;
+            kv.key = L.st.blob + tk.off;
+            kv.len = tk.len;
         }
         H st;
         if constexpr (DMA) {
-            if (q.prefix_len < 4) hash_key_dma<H, 2, 2>(kv, st, my_lds);
+            if (q.prefix_len <= 4) hash_key_dma<H, 2, 2>(kv, st, my_lds);
             else hash_key<H>(kv, st);
         } else {
             hash_key<H>(kv, st);
@@ -308,31 +316,39 @@ __global__ void __launch_bounds__(256) k_pair_test(RespondLaunch L, const uint32
                 ok &= (filt[pos >> 5] >> (pos & 31)) & 1u;
             }
         }
+        const uint32_t nb = active ? n_blocks(kv.plen + kv.len, H::block_bytes, H::len_bytes) : 0u;
         if (active) {
             L.miss[(uint64_t)r * W + t] = (uint8_t)(ok ^ 1u);
-            acc_blocks += n_blocks(kv.plen + kv.len, H::block_bytes, H::len_bytes);
+            acc_blocks += nb;
             acc_bytes += kv.len;
         }
-    }
-    if (L.total_blocks) {  // one pair of atomics per workgroup (a contended atomic per wave-task would stall
-                           // the next vmcnt wait of every wave behind it)
-        __shared__ unsigned long long red[2][4];
+        // lane-block slots this wave-task occupied: 64 x the longest lane (load-balance denominator)
+        uint32_t nbmax = nb;
 #pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-            acc_blocks += __shfl_xor(acc_blocks, d, 64);
-            acc_bytes += __shfl_xor(acc_bytes, d, 64);
-        }
-        if (lane == 0) {
-            red[0][threadIdx.x >> 6] = acc_blocks;
-            red[1][threadIdx.x >> 6] = acc_bytes;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned long long b = 0, y = 0;
-            for (uint32_t wv = 0; wv < blockDim.x / 64; ++wv) b += red[0][wv], y += red[1][wv];
-            if (b) atomicAdd((unsigned long long*)&L.total_blocks[0], b);
-            if (y) atomicAdd((unsigned long long*)&L.total_blocks[1], y);
-        }
+        for (int d = 32; d >= 1; d >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, d, 64));
+        if (lane == 0) acc_slots += 64ull * nbmax;
+    }
+    // one set of atomics per workgroup (a contended atomic per wave-task would stall the next vmcnt wait of
+    // every wave behind it)
+    __shared__ unsigned long long red[3][4];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        acc_blocks += __shfl_xor(acc_blocks, d, 64);
+        acc_bytes += __shfl_xor(acc_bytes, d, 64);
+        acc_slots += __shfl_xor(acc_slots, d, 64);
+    }
+    if (lane == 0) {
+        red[0][threadIdx.x >> 6] = acc_blocks;
+        red[1][threadIdx.x >> 6] = acc_bytes;
+        red[2][threadIdx.x >> 6] = acc_slots;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long b = 0, y = 0, z = 0;
+        for (uint32_t wv = 0; wv < blockDim.x / 64; ++wv) b += red[0][wv], y += red[1][wv], z += red[2][wv];
+        if (b) atomicAdd((unsigned long long*)&L.counters[kCntBlocks], b);
+        if (y) atomicAdd((unsigned long long*)&L.counters[kCntBytes], y);
+        if (z) atomicAdd((unsigned long long*)&L.counters[kCntSlots], z);
     }
 }
 
@@ -390,6 +406,7 @@ __global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
     uint64_t emitted = S->emitted;
     int64_t spent = S->spent;
     uint32_t done = 0, overflow = S->overflow;
+    uint64_t useful = n;  // pairs the reference hashes in this window: up to the packet that spends the budget
     const int64_t limit = L.byte_limit;
     for (uint64_t t0 = 0; t0 < n && !done; t0 += 64) {
         const uint64_t t = t0 + lane;
@@ -417,13 +434,17 @@ __global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
         }
         // bytes of the included prefix = inclusive scan at the last included lane
         int64_t sum_in = 0;
+        int last = -1;
         if (nin) {
-            const int last = 63 - __builtin_clzll(imask);
+            last = 63 - __builtin_clzll(imask);
             sum_in = __shfl(incl, last, 64);
         }
         emitted += nin;
         spent += sum_in;
-        if (emitted > 0 && spent >= limit) done = 1;
+        if (emitted > 0 && spent >= limit) {
+            done = 1;
+            useful = t0 + (uint64_t)last + 1;
+        }
     }
     overflow = __any(overflow) ? 1u : 0u;
     if (lane == 0) {
@@ -433,7 +454,8 @@ __global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
         if (overflow) L.flags[1] = 1;
         if (done || S->exhausted) S->done = 1;
         else L.flags[0] = 1;
-        atomicAdd((unsigned long long*)L.total_pairs, (unsigned long long)n);
+        atomicAdd((unsigned long long*)&L.counters[kCntPairs], (unsigned long long)n);
+        atomicAdd((unsigned long long*)&L.counters[kCntUseful], (unsigned long long)useful);
     }
 }
 

@@ -114,6 +114,12 @@ int dsy_ctx_set_timing(dsy_ctx* ctx, int enable);
 int dsy_ctx_kernel_time(dsy_ctx* ctx, int which, double* out_ms, uint64_t* out_launches, uint64_t* out_blocks,
                         uint64_t* out_bytes);
 int dsy_ctx_reset_timing(dsy_ctx* ctx);
+/* Algorithmic work of timer class `which` since the last reset (accumulated whether or not timing is on):
+ * out4[0] compression blocks, out4[1] key bytes hashed, out4[2] (class 0) pairs the reference would have hashed --
+ * its lazy not_filter stops at the packet that spends the byte limit (community.py:2559-2567), the GPU hashes whole
+ * windows --, out4[3] lane-block slots of the hashing waves (64 x the longest lane per wave-task): out4[0] / out4[3]
+ * is the active-lane fraction. */
+int dsy_ctx_work(dsy_ctx* ctx, int which, uint64_t* out4);
 
 /* ---------------------------------------------------------------------------------- BloomFilter kernels */
 /* Replaces BloomFilter.add / add_keys (bloomfilter.py:163-194): ORs the k bits of every key into filter_inout

@@ -184,7 +184,7 @@ __device__ __forceinline__ void hash_key_coop(const KeyView& kv, H& st, uint32_t
 // (each instruction = 8 keys x 128 contiguous bytes), double-buffered; lanes read their own 2 blocks with
 // conflict-free ds_read_b128 (chunk slot (c - lane/2) & 7 within the key's 128-B row).
 template <class H>
-__device__ __forceinline__ void hash_key_dma(const KeyView& kv, H& st, uint8_t* buf0) {
+__device__ __forceinline__ void hb_hash_key_dma(const KeyView& kv, H& st, uint8_t* buf0) {
     static_assert(H::block_bytes == 64, "64-byte blocks");
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t r = kv.plen;  // <= 3
@@ -419,7 +419,7 @@ __global__ void __launch_bounds__(256) k_hash(const uint8_t* blob, const uint64_
         hash_key_prefetch<H>(kv, st);
     } else if (V == kDma) {
         extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
-        hash_key_dma<H>(kv, st, dyn + (threadIdx.x >> 6) * 16384);
+        hb_hash_key_dma<H>(kv, st, dyn + (threadIdx.x >> 6) * 16384);
     } else if (V == kFast) {
         hash_key<H>(kv, st);
     } else if (V == kCoop) {
