@@ -1,78 +1,164 @@
 // dsy_bloom_kernels.hip -- single-filter Bloom kernels for gfx950: build (add), membership test, index dump.
 //
-// Mapping: one key per lane (Merkle-Damgard is sequential per message), 256-thread workgroups, grid-stride
-// over keys.  Small filters (the ~10 Kbit MTU filters of community.py:637-666) live in LDS for the whole
-// workgroup: the build ORs bits with ds_or_b32 and merges the LDS filter into HBM once per workgroup; the
-// test stages the filter into LDS once and probes it there.  Large filters (m = 2^20..2^24 bits, BASELINE
-// config 4) are probed/ORed in place in HBM/L2 with global atomics.
+// Mapping: one key per lane (Merkle-Damgard is sequential per message), 256-thread workgroups, a grid-stride
+// loop over 64-key wave-tasks.  Large batches are first put in length-bucketed order (k_len_* below: a counting
+// sort of the keys by compression-block count, longest first) so the 64 lanes of a wave run the same number of
+// blocks; the sort writes 16-byte task records (blob offset, length, key index) that the hashing kernel reads
+// contiguously.  Small filters (the ~10 Kbit MTU filters of community.py:637-666) live in LDS for the whole
+// workgroup: the build ORs bits with ds_or_b32 and merges the LDS filter into HBM once per workgroup; the test
+// stages the filter into LDS once and probes it there.  Large filters (m = 2^20..2^24 bits, BASELINE config 4)
+// are probed/ORed in place in L2/HBM with global atomics.  MD5 (load-bound) stages packet bytes through LDS with
+// LDS-DMA when the filter is small (dsy_message.h hash_key_dma); the SHA families load directly (compute-bound).
 #include "dsy_kernels.h"
 
 namespace dsy {
 
-template <class H, int CHUNK>
-__global__ void __launch_bounds__(256) k_bloom_add(const DevParams* __restrict__ prm, const uint8_t* __restrict__ blob,
-                                                   const uint64_t* __restrict__ offsets, const uint64_t* __restrict__ rows,
-                                                   uint64_t n, uint32_t* __restrict__ filter, uint32_t nwords, int use_lds) {
-    extern __shared__ uint32_t lds_filter[];
-    const uint64_t m = prm->m_bits;
-    const uint32_t k = prm->k;
-    if (use_lds) {
-        for (uint32_t i = threadIdx.x; i < nwords; i += blockDim.x) lds_filter[i] = 0;
-        __syncthreads();
-    }
-    uint32_t* dst = use_lds ? lds_filter : filter;
+static constexpr uint32_t kLenBins = 1024;
+static constexpr int kDmaS = 2, kDmaNB = 2;
+static constexpr size_t kDmaWaveBytes = DmaGeometry<kDmaS, kDmaNB>::kWaveBytes;
+
+__device__ __forceinline__ uint32_t len_bin(uint64_t len, const LenSort& s) {
+    return kLenBins - 1u - min(n_blocks(s.plen + (uint32_t)len, s.blk, s.lenb), kLenBins - 1u);
+}
+
+__device__ __forceinline__ void key_span(const uint64_t* __restrict__ offsets, const uint64_t* __restrict__ rows,
+                                         uint64_t i, uint64_t* off, uint32_t* len) {
+    const uint64_t row = rows ? rows[i] : i;
+    const uint64_t a = offsets[row], e = offsets[row + 1];
+    *off = a;
+    *len = (uint32_t)(e - a);
+}
+
+// ---------------------------------------------------------------------------- length-bucketed task order
+// pass 1: global histogram of bins (LDS-aggregated)
+__global__ void __launch_bounds__(256) k_len_hist(LenSort s, const uint64_t* __restrict__ offsets,
+                                                  const uint64_t* __restrict__ rows, uint64_t n,
+                                                  uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[kLenBins];
+    for (uint32_t i = threadIdx.x; i < kLenBins; i += blockDim.x) h[i] = 0;
+    __syncthreads();
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint64_t row = rows ? rows[i] : i;
-        const uint64_t a = offsets[row], e = offsets[row + 1];
-        KeyView kv{blob + a, (uint32_t)(e - a), prm->prefix, prm->prefix_len};
-        H st;
-        hash_key<H>(kv, st);
-#pragma unroll
-        for (int j = 0; j < ChunkLimit<H, CHUNK>::kmax; ++j) {
-            if (j < (int)k) {
-                const uint64_t pos = bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, j), m);
-                atomicOr(&dst[pos >> 5], 1u << (pos & 31));
-            }
-        }
+        uint64_t off;
+        uint32_t len;
+        key_span(offsets, rows, i, &off, &len);
+        atomicAdd(&h[len_bin(len, s)], 1u);
     }
-    if (use_lds) {
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < kLenBins; i += blockDim.x)
+        if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// pass 2: exclusive scan of the bins (one workgroup of kLenBins threads)
+__global__ void __launch_bounds__(kLenBins) k_len_scan(uint32_t* __restrict__ hist) {
+    __shared__ uint32_t part[kLenBins];
+    const uint32_t t = threadIdx.x;
+    const uint32_t v = hist[t];
+    part[t] = v;
+    __syncthreads();
+    for (uint32_t d = 1; d < kLenBins; d <<= 1) {
+        const uint32_t add = t >= d ? part[t - d] : 0u;
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < nwords; i += blockDim.x) {
-            const uint32_t v = lds_filter[i];
-            if (v) atomicOr(&filter[i], v);
+        part[t] += add;
+        __syncthreads();
+    }
+    hist[t] = part[t] - v;
+}
+
+// pass 3: scatter task records; each workgroup reserves its bins' ranges with one global atomic per bin
+static constexpr uint32_t kScatterChunk = 4096;
+__global__ void __launch_bounds__(256) k_len_scatter(LenSort s, const uint64_t* __restrict__ offsets,
+                                                     const uint64_t* __restrict__ rows, uint64_t n,
+                                                     uint32_t* __restrict__ base, PairTask* __restrict__ tasks) {
+    __shared__ uint32_t cnt[kLenBins];
+    __shared__ uint32_t at[kLenBins];
+    for (uint64_t c0 = (uint64_t)blockIdx.x * kScatterChunk; c0 < n; c0 += (uint64_t)gridDim.x * kScatterChunk) {
+        const uint64_t c1 = min(n, c0 + kScatterChunk);
+        for (uint32_t i = threadIdx.x; i < kLenBins; i += blockDim.x) cnt[i] = 0;
+        __syncthreads();
+        for (uint64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
+            uint64_t off;
+            uint32_t len;
+            key_span(offsets, rows, i, &off, &len);
+            atomicAdd(&cnt[len_bin(len, s)], 1u);
         }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < kLenBins; i += blockDim.x) {
+            at[i] = cnt[i] ? atomicAdd(&base[i], cnt[i]) : 0u;
+            cnt[i] = 0;
+        }
+        __syncthreads();
+        for (uint64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
+            PairTask tk;
+            key_span(offsets, rows, i, &tk.off, &tk.len);
+            tk.slot = (uint32_t)i;
+            const uint32_t b = len_bin(tk.len, s);
+            tasks[at[b] + atomicAdd(&cnt[b], 1u)] = tk;
+        }
+        __syncthreads();
     }
 }
 
-template <class H, int CHUNK>
-__global__ void __launch_bounds__(256) k_bloom_test(const DevParams* __restrict__ prm, const uint8_t* __restrict__ blob,
-                                                    const uint64_t* __restrict__ offsets, uint64_t n,
-                                                    const uint32_t* __restrict__ filter, uint32_t nwords, int use_lds,
-                                                    uint8_t* __restrict__ present) {
-    extern __shared__ uint32_t lds_filter[];
+// ------------------------------------------------------------------------------------- hash + probe / set
+// OP 0: add (OR k bits per key into the filter), OP 1: test (present[key] = all k bits set).
+template <class H, int CHUNK, int OP, bool DMA>
+__global__ void __launch_bounds__(256) k_bloom(const DevParams* __restrict__ prm, const uint8_t* __restrict__ blob,
+                                               const uint64_t* __restrict__ offsets, const uint64_t* __restrict__ rows,
+                                               const PairTask* __restrict__ tasks, uint64_t n,
+                                               uint32_t* __restrict__ filter, uint32_t nwords, int use_lds,
+                                               uint8_t* __restrict__ present) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+    uint8_t* my_dma = dyn_lds + (threadIdx.x >> 6) * kDmaWaveBytes;
+    uint32_t* lds_filter = (uint32_t*)(dyn_lds + (DMA ? 4 * kDmaWaveBytes : 0));
     const uint64_t m = prm->m_bits;
     const uint32_t k = prm->k;
     if (use_lds) {
-        for (uint32_t i = threadIdx.x; i < nwords; i += blockDim.x) lds_filter[i] = filter[i];
+        for (uint32_t i = threadIdx.x; i < nwords; i += blockDim.x) lds_filter[i] = OP == 0 ? 0u : filter[i];
         __syncthreads();
     }
-    const uint32_t* src = use_lds ? lds_filter : filter;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint64_t a = offsets[i], e = offsets[i + 1];
-        KeyView kv{blob + a, (uint32_t)(e - a), prm->prefix, prm->prefix_len};
-        H st;
-        hash_key<H>(kv, st);
-        uint32_t ok = 1;
-#pragma unroll
-        for (int j = 0; j < ChunkLimit<H, CHUNK>::kmax; ++j) {
-            if (j < (int)k) {
-                const uint64_t pos = bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, j), m);
-                ok &= (src[pos >> 5] >> (pos & 31)) & 1u;
+    uint32_t* fbits = use_lds ? lds_filter : filter;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t waves = (n + 63) / 64;
+    const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t v = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; v < waves; v += wstride) {
+        const uint64_t i = v * 64 + lane;
+        const bool active = i < n;
+        KeyView kv{blob, 0u, prm->prefix, prm->prefix_len};  // idle lanes hash an empty key
+        uint64_t slot = i;
+        if (active) {
+            if (tasks) {
+                const PairTask tk = tasks[i];
+                kv.key = blob + tk.off;
+                kv.len = tk.len;
+                slot = tk.slot;
+            } else {
+                uint64_t off;
+                key_span(offsets, rows, i, &off, &kv.len);
+                kv.key = blob + off;
             }
         }
-        present[i] = (uint8_t)ok;
+        H st;
+        if constexpr (DMA) hash_key_dma<H, kDmaS, kDmaNB>(kv, st, my_dma);
+        else hash_key<H>(kv, st);
+        if (active) {
+            uint32_t ok = 1;
+#pragma unroll
+            for (int j = 0; j < ChunkLimit<H, CHUNK>::kmax; ++j) {
+                if (j < (int)k) {
+                    const uint64_t pos = bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, j), m);
+                    if (OP == 0) atomicOr(&fbits[pos >> 5], 1u << (pos & 31));
+                    else ok &= (fbits[pos >> 5] >> (pos & 31)) & 1u;
+                }
+            }
+            if (OP == 1) present[slot] = (uint8_t)ok;
+        }
+    }
+    if (OP == 0 && use_lds) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < nwords; i += blockDim.x) {
+            const uint32_t val = lds_filter[i];
+            if (val) atomicOr(&filter[i], val);
+        }
     }
 }
 
@@ -95,27 +181,50 @@ __global__ void __launch_bounds__(256) k_bloom_indices(const DevParams* __restri
 }
 
 // ------------------------------------------------------------------------------------------ dispatch
+hipError_t launch_len_sort(const LenSort& s, const uint64_t* offsets, const uint64_t* rows, uint64_t n,
+                           uint32_t* d_bins, PairTask* d_tasks, uint32_t max_grid, hipStream_t stream) {
+    hipError_t e = hipMemsetAsync(d_bins, 0, kLenBins * 4, stream);
+    if (e != hipSuccess) return e;
+    const uint64_t want = (n + 255) / 256;
+    const uint32_t grid = (uint32_t)(want < max_grid ? (want ? want : 1) : max_grid);
+    hipLaunchKernelGGL(k_len_hist, dim3(grid), dim3(256), 0, stream, s, offsets, rows, n, d_bins);
+    hipLaunchKernelGGL(k_len_scan, dim3(1), dim3(kLenBins), 0, stream, d_bins);
+    const uint64_t chunks = (n + kScatterChunk - 1) / kScatterChunk;
+    const uint32_t sgrid = (uint32_t)(chunks < max_grid ? (chunks ? chunks : 1) : max_grid);
+    hipLaunchKernelGGL(k_len_scatter, dim3(sgrid), dim3(256), 0, stream, s, offsets, rows, n, d_bins, d_tasks);
+    return hipGetLastError();
+}
+
+template <class H, int CHUNK, int OP>
+static hipError_t launch_op(const BloomLaunch& L, uint32_t grid) {
+    // LDS-DMA staging for MD5 whenever the filter is small enough to leave room for it (2 workgroups per CU)
+    const bool dma = H::kind == DSY_MD5 && L.prm_prefix_len <= 4 && (!L.use_lds || L.nwords * 4 <= 16 * 1024);
+    const size_t lds = (dma ? 4 * kDmaWaveBytes : 0) + (L.use_lds ? (size_t)L.nwords * 4 : 0);
+    if (dma) {
+        if constexpr (H::block_bytes == 64)
+            hipLaunchKernelGGL((k_bloom<H, CHUNK, OP, true>), dim3(grid), dim3(256), lds, L.stream, L.prm, L.blob,
+                               L.offsets, L.rows, L.tasks, L.n, L.filter, L.nwords, L.use_lds, L.present);
+    } else {
+        hipLaunchKernelGGL((k_bloom<H, CHUNK, OP, false>), dim3(grid), dim3(256), lds, L.stream, L.prm, L.blob,
+                           L.offsets, L.rows, L.tasks, L.n, L.filter, L.nwords, L.use_lds, L.present);
+    }
+    return hipGetLastError();
+}
+
 template <class H, int CHUNK>
 static hipError_t launch_family(const BloomLaunch& L) {
     const uint32_t block = 256;
     const uint64_t want = (L.n + block - 1) / block;
     const uint32_t grid = (uint32_t)(want < L.max_grid ? (want ? want : 1) : L.max_grid);
-    const size_t lds = L.use_lds ? (size_t)L.nwords * 4 : 0;
     switch (L.op) {
-        case BloomOp::Add:
-            hipLaunchKernelGGL((k_bloom_add<H, CHUNK>), dim3(grid), dim3(block), lds, L.stream, L.prm, L.blob, L.offsets,
-                               L.rows, L.n, L.filter, L.nwords, L.use_lds);
-            break;
-        case BloomOp::Test:
-            hipLaunchKernelGGL((k_bloom_test<H, CHUNK>), dim3(grid), dim3(block), lds, L.stream, L.prm, L.blob,
-                               L.offsets, L.n, (const uint32_t*)L.filter, L.nwords, L.use_lds, L.present);
-            break;
+        case BloomOp::Add: return launch_op<H, CHUNK, 0>(L, grid);
+        case BloomOp::Test: return launch_op<H, CHUNK, 1>(L, grid);
         case BloomOp::Indices:
             hipLaunchKernelGGL((k_bloom_indices<H, CHUNK>), dim3(grid), dim3(block), 0, L.stream, L.prm, L.blob,
                                L.offsets, L.n, L.indices);
-            break;
+            return hipGetLastError();
     }
-    return hipGetLastError();
+    return hipErrorInvalidValue;
 }
 
 template <class H>

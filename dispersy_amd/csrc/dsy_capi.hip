@@ -168,6 +168,9 @@ int check_params(const dsy_bloom_params* p) {
 
 uint64_t filter_words(uint64_t m) { return (m + 31) / 32; }
 
+// batches of at least this many keys are hashed in length-bucketed order
+const uint64_t kLenSortMin = 1 << 15;
+
 int upload_params(dsy_ctx* c, const dsy_bloom_params* p, DevParams** out) {
     DevParams hp{};
     hp.m_bits = p->m_bits;
@@ -221,6 +224,7 @@ int run_bloom(dsy_ctx* c, BloomOp op, const dsy_bloom_params* p, const uint8_t* 
     L.kind = p->hash_kind;
     L.chunk = p->chunk_bytes;
     L.prm = dp;
+    L.prm_prefix_len = p->prefix_len;
     L.blob = d_blob;
     L.offsets = d_off;
     L.rows = d_rows;
@@ -232,6 +236,18 @@ int run_bloom(dsy_ctx* c, BloomOp op, const dsy_bloom_params* p, const uint8_t* 
     L.indices = d_idx;
     L.max_grid = c->max_grid;
     L.stream = c->stream;
+    // Large batches hash in length-bucketed order (a wave's 64 lanes then run the same number of blocks); the
+    // sort costs ~40 B of traffic per key next to the key bytes themselves.
+    if (op != BloomOp::Indices && n >= kLenSortMin) {
+        void *bins, *tasks;
+        int rc2;
+        if ((rc2 = ws_get(c, "len_bins", 1024 * 4, &bins))) return rc2;
+        if ((rc2 = ws_get(c, "len_tasks", n * sizeof(PairTask), &tasks))) return rc2;
+        const bool wide = p->hash_kind >= DSY_SHA384;
+        LenSort ls{p->prefix_len, wide ? 128u : 64u, wide ? 16u : 8u};
+        HIP_TRY(launch_len_sort(ls, d_off, d_rows, n, (uint32_t*)bins, (PairTask*)tasks, c->max_grid, c->stream));
+        L.tasks = (const PairTask*)tasks;
+    }
     PendingTimer t;
     timer_begin(c, &t, kTimeBuild);
     HIP_TRY(launch_bloom(L));
@@ -599,7 +615,13 @@ int dsy_bloom_add_rows(dsy_ctx* c, const dsy_bloom_params* p, const dsy_store* s
 }
 
 // -------------------------------------------------------------------------------------------- responder
+// The window pool holds kWindow pairs per claim of the call, and at least kMinSlots claims' worth (16 M pairs,
+// 400 MB of workspace); each window the active claims share it evenly, from kWindow up to kMaxWindow pairs each.
+// Few long-running claims then take a handful of big windows: every window costs at least the serial digest of
+// its longest packet on one lane (~1 ms for a 64 KB packet), so their number matters.
 static const uint64_t kWindow = 4096;
+static const uint64_t kMaxWindow = 1 << 18;
+static const uint64_t kMinSlots = 4096;
 
 static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, uint32_t R, const uint8_t* d_filters,
                         uint64_t filters_len, const dsy_meta* metas, uint32_t J, uint64_t responder_gt,
@@ -633,34 +655,35 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
         sm[j].has_pruning = metas[j].has_pruning;
         sm[j].inactive = metas[j].inactive_threshold;
     }
-    const uint64_t W = kWindow;
+    const uint64_t pool = kWindow * std::max<uint64_t>(R, kMinSlots);
     int rc;
     void *d_reqs, *d_metas, *d_plans, *d_state, *d_upper, *d_pairs, *d_miss, *d_flags, *d_total, *d_lists;
+    void *d_act, *d_act_done;
     if ((rc = ws_get(c, "reqs", std::max<size_t>(R, 1) * sizeof(dsy_request), &d_reqs))) return rc;
     if ((rc = ws_get(c, "metas", std::max<size_t>(J, 1) * sizeof(SegMeta), &d_metas))) return rc;
     if ((rc = ws_get(c, "plans", std::max<size_t>((size_t)R * J, 1) * sizeof(Plan), &d_plans))) return rc;
     if ((rc = ws_get(c, "state", std::max<size_t>(R, 1) * sizeof(ReqState), &d_state))) return rc;
     if ((rc = ws_get(c, "upper", std::max<size_t>(R, 1) * 8, &d_upper))) return rc;
-    if ((rc = ws_get(c, "pairs", std::max<size_t>((size_t)R * W, 1) * 8, &d_pairs))) return rc;
-    if ((rc = ws_get(c, "miss", std::max<size_t>((size_t)R * W, 1), &d_miss))) return rc;
+    if ((rc = ws_get(c, "pairs", pool * 8, &d_pairs))) return rc;
+    if ((rc = ws_get(c, "miss", pool, &d_miss))) return rc;
     void* d_task;
-    if ((rc = ws_get(c, "task", std::max<size_t>((size_t)R * W, 1) * sizeof(PairTask), &d_task))) return rc;
+    if ((rc = ws_get(c, "task", pool * sizeof(PairTask), &d_task))) return rc;
     if ((rc = ws_get(c, "flags", 64, &d_flags))) return rc;
     if ((rc = ws_get(c, "total", 64, &d_total))) return rc;
     if ((rc = ws_get(c, "lists", std::max<size_t>(R, 1) * 4, &d_lists))) return rc;
+    if ((rc = ws_get(c, "act", std::max<size_t>(R, 1) * 4, &d_act))) return rc;
+    if ((rc = ws_get(c, "act_done", std::max<size_t>(R, 1), &d_act_done))) return rc;
 
     if (R) HIP_TRY(hipMemcpyAsync(d_reqs, reqs, (size_t)R * sizeof(dsy_request), hipMemcpyHostToDevice, c->stream));
     if (J) HIP_TRY(hipMemcpyAsync(d_metas, sm.data(), (size_t)J * sizeof(SegMeta), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemsetAsync(d_upper, 0, std::max<size_t>(R, 1) * 8, c->stream));
     HIP_TRY(hipMemsetAsync(d_total, 0, 64, c->stream));
-    std::vector<uint32_t> lists;
-    std::vector<std::pair<std::pair<int, uint32_t>, std::pair<size_t, size_t>>> fam_ranges;
-    for (auto& kv : families) {
-        fam_ranges.push_back({kv.first, {lists.size(), kv.second.size()}});
-        lists.insert(lists.end(), kv.second.begin(), kv.second.end());
-    }
-    if (!lists.empty())
-        HIP_TRY(hipMemcpyAsync(d_lists, lists.data(), lists.size() * 4, hipMemcpyHostToDevice, c->stream));
+    // window slots 0..R-1 (a family's active claims occupy a contiguous run of slots in every window)
+    std::vector<uint32_t> slots(R);
+    for (uint32_t i = 0; i < R; ++i) slots[i] = i;
+    if (R) HIP_TRY(hipMemcpyAsync(d_lists, slots.data(), (size_t)R * 4, hipMemcpyHostToDevice, c->stream));
+    std::vector<std::pair<std::pair<int, uint32_t>, std::vector<uint32_t>>> fam_active;  // per family: active claims
+    for (auto& kv : families) fam_active.push_back({kv.first, kv.second});
 
     RespondLaunch L{};
     L.st.blob = s->d_blob;
@@ -677,7 +700,9 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     L.include_inactive = include_inactive;
     L.byte_limit = byte_limit;
     L.seed = seed;
-    L.window = W;
+    L.window = kWindow;
+    L.act = (const uint32_t*)d_act;
+    L.act_done = (uint8_t*)d_act_done;
     L.plans = (Plan*)d_plans;
     L.state = (ReqState*)d_state;
     L.upper = (uint64_t*)d_upper;
@@ -720,29 +745,54 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
         if (R) HIP_TRY(hipMemcpyAsync(d_state, st.data(), (size_t)R * sizeof(ReqState), hipMemcpyHostToDevice, c->stream));
     }
 
-    // ---- windows: fill -> hash/test (one launch per hash family) -> compact; one host sync per window
+    // ---- windows: fill -> hash/test (one launch per hash family) -> compact; one host sync per window.  Only
+    // the active claims take part; as they finish, the rest share the pool in bigger windows.
     uint32_t* h_flags = (uint32_t*)c->pinned;
     uint64_t* h_tot = (uint64_t*)c->pinned + 8;
+    std::vector<uint32_t> act;
+    std::vector<uint8_t> act_done;
     for (;;) {
+        act.clear();
+        std::vector<std::pair<size_t, size_t>> runs;  // per family: (first slot, slots)
+        for (auto& fa : fam_active) {
+            runs.push_back({act.size(), fa.second.size()});
+            act.insert(act.end(), fa.second.begin(), fa.second.end());
+        }
+        const uint32_t n_act = (uint32_t)act.size();
+        if (!n_act) break;
+        uint64_t W = pool / n_act / 64 * 64;
+        W = std::min<uint64_t>(std::max<uint64_t>(W, kWindow), kMaxWindow);
+        L.window = W;
+        L.n_act = n_act;
+        HIP_TRY(hipMemcpyAsync(d_act, act.data(), (size_t)n_act * 4, hipMemcpyHostToDevice, c->stream));
         HIP_TRY(hipMemsetAsync(d_flags, 0, 64, c->stream));
         timer_begin(c, &t, kTimeSelect);
         HIP_TRY(launch_fill(L));
         timer_end(c, &t);
-        for (auto& fr : fam_ranges) {
+        for (size_t f = 0; f < fam_active.size(); ++f) {
+            if (!runs[f].second) continue;
             timer_begin(c, &t, kTimePairTest);
-            HIP_TRY(launch_pair_test_list(L, fr.first.first, fr.first.second, (const uint32_t*)d_lists + fr.second.first,
-                                          (uint32_t)fr.second.second));
+            HIP_TRY(launch_pair_test_list(L, fam_active[f].first.first, fam_active[f].first.second,
+                                          (const uint32_t*)d_lists + runs[f].first, (uint32_t)runs[f].second));
             timer_end(c, &t);
         }
         timer_begin(c, &t, kTimeCompact);
         HIP_TRY(launch_compact(L));
         timer_end(c, &t);
+        act_done.resize(n_act);
+        HIP_TRY(hipMemcpyAsync(act_done.data(), d_act_done, n_act, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipMemcpyAsync(h_flags, d_flags, 8, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipMemcpyAsync(h_tot, d_total, kCntN * 8, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
         // capacity overflow can only come from a wrong min_len bound; report it loudly
         if (h_flags[1]) return fail(DSY_ECAPACITY, "internal: a claim overflowed its output capacity");
-        if (!h_flags[0]) break;
+        size_t a = 0;
+        for (auto& fa : fam_active) {
+            std::vector<uint32_t> keep;
+            for (uint32_t r : fa.second)
+                if (!act_done[a++]) keep.push_back(r);
+            fa.second.swap(keep);
+        }
     }
     void *d_packed_v, *d_packed_off_v;
     if ((rc = ws_get(c, "packed", std::max<uint64_t>(cap_total, 1) * 8, &d_packed_v))) return rc;

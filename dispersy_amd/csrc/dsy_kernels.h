@@ -18,14 +18,25 @@ struct DevParams {
 
 enum class BloomOp { Add, Test, Indices };
 
+// One (claim, packet) pair -- or one key of a single-filter batch -- as a hashing kernel consumes it, written in
+// hashing order (sorted by block count): where the packet starts in the blob, its length, and its slot (the
+// window slot / key index whose result it produces).
+struct __attribute__((aligned(16))) PairTask {
+    uint64_t off;
+    uint32_t len;
+    uint32_t slot;
+};
+
 struct BloomLaunch {
     BloomOp op;
     int kind;
     uint32_t chunk;
     const DevParams* prm;
+    uint32_t prm_prefix_len;  // host copy of prm->prefix_len (kernel choice)
     const uint8_t* blob;
     const uint64_t* offsets;
-    const uint64_t* rows;  // optional indirection (add by store row)
+    const uint64_t* rows;     // optional indirection (add by store row)
+    const PairTask* tasks;    // optional length-bucketed order of the n keys (launch_len_sort)
     uint64_t n;
     uint32_t* filter;
     uint32_t nwords;
@@ -37,6 +48,13 @@ struct BloomLaunch {
 };
 
 hipError_t launch_bloom(const BloomLaunch& L);
+
+// Length-bucketed order of a key batch: tasks[0..n) sorted by compression-block count, longest first.
+struct LenSort {
+    uint32_t plen, blk, lenb;
+};
+hipError_t launch_len_sort(const LenSort& s, const uint64_t* offsets, const uint64_t* rows, uint64_t n,
+                           uint32_t* d_bins /* 1024 */, PairTask* d_tasks, uint32_t max_grid, hipStream_t stream);
 
 // ------------------------------------------------------------------------------------------ responder
 // Store view the responder kernels read.  `live` rows are the rows with undone == 0, in index order.
@@ -58,14 +76,6 @@ struct Plan {
     uint64_t perm_key; // RANDOM: permutation key
     uint32_t perm_bits;// RANDOM: Feistel half-width
     uint32_t _pad;
-};
-
-// One (claim, packet) pair as the hashing kernel consumes it, written by k_fill in hashing order (window slots
-// sorted by block count): where the packet starts in the blob, its length, and its window slot (send order).
-struct __attribute__((aligned(16))) PairTask {
-    uint64_t off;
-    uint32_t len;
-    uint32_t slot;
 };
 
 // Work counters of the responder (device u64[8], accumulated over a call's windows).
@@ -103,7 +113,10 @@ struct RespondLaunch {
     int include_inactive;
     int64_t byte_limit;
     uint64_t seed;
-    uint64_t window;          // W pairs per claim per window
+    uint64_t window;          // W pairs per claim in this window
+    const uint32_t* act;      // device [n_act]: window slot a serves claim act[a]
+    uint32_t n_act;
+    uint8_t* act_done;        // device [n_act]: written by k_compact, 1 once claim act[a] is done
     Plan* plans;              // device [R*J]
     ReqState* state;          // device [R]
     uint64_t* upper;          // device [R]: upper bound of selected rows per claim
@@ -111,7 +124,7 @@ struct RespondLaunch {
     PairTask* task;           // device [R*W]: per-claim hashing order (window slots sorted by block count)
     uint8_t* miss;            // device [R*W]
     uint64_t* out;            // device [sum cap]
-    uint32_t* flags;          // device [4]: [0] any claim still active
+    uint32_t* flags;          // device [4]: [1] an output capacity overflowed
     uint64_t* counters;       // device [kCntN]: pairs hashed, compression blocks, packet bytes, pairs the reference
                               // would have hashed (it stops at the byte limit), lane-block slots of the hashing waves
     hipStream_t stream;
@@ -119,7 +132,7 @@ struct RespondLaunch {
 
 hipError_t launch_plan(const RespondLaunch& L);
 hipError_t launch_fill(const RespondLaunch& L);
-// hash + test the window's pairs of the listed claims, all of one (hash kind, chunk) family
+// hash + test the window's pairs of the listed window slots, all of one (hash kind, chunk) family
 hipError_t launch_pair_test_list(const RespondLaunch& L, int kind, uint32_t chunk, const uint32_t* d_list, uint32_t n);
 hipError_t launch_compact(const RespondLaunch& L);
 hipError_t launch_caps(const RespondLaunch& L, uint64_t per_claim_cap);

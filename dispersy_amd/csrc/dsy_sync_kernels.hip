@@ -3,7 +3,10 @@
 // Work is windowed per claim, mirroring the reference's lazy cursor + lazy not_filter: each window selects at
 // most W (claim, packet) pairs per claim in send order, hashes and tests them, and emits missing packets until
 // the claim's byte budget is spent.  A claim whose budget is spent after its first window never selects more,
-// exactly as the reference stops pulling rows from SQLite.
+// exactly as the reference stops pulling rows from SQLite.  Only the claims still active take part in a window
+// (L.act: window slot a serves claim act[a]); the host grows W as claims finish, so the few claims that walk huge
+// ranges (a filter that covers everything, a global time shared by 10^5 rows) take big windows instead of
+// hundreds of small ones.
 //
 //   k_plan        one lane per (claim, meta): binary-search the live-row span of [time_low', time_high] in the
 //                 meta's global_time-sorted segment; choose scan (every row) or enumerate (every global time
@@ -134,7 +137,6 @@ __global__ void k_plan(RespondLaunch L) {
 // ------------------------------------------------------------------------------------------- k_fill
 static constexpr int kFillThreads = 256;
 static constexpr uint32_t kSortBins = 1024;
-static constexpr uint32_t kMaxWindow = 4096;
 
 __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* lds, uint64_t* total) {
     // lds: kFillThreads + 1 words.  Simple Hillis-Steele over LDS (one per window step; not the hot loop).
@@ -156,7 +158,8 @@ __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* l
 __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
     __shared__ uint64_t scan[kFillThreads + 1];
     __shared__ uint32_t first_cross;
-    const uint32_t r = blockIdx.x;
+    const uint32_t a_slot = blockIdx.x;
+    const uint32_t r = L.act[a_slot];
     ReqState* S = &L.state[r];
     if (S->done) {
         if (threadIdx.x == 0) S->n_window = 0;
@@ -164,7 +167,7 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
     }
     const dsy_request& q = L.reqs[r];
     const uint64_t W = L.window;
-    uint64_t* out = L.pair_row + (uint64_t)r * W;
+    uint64_t* out = L.pair_row + (uint64_t)a_slot * W;
     uint32_t j = S->meta;
     uint64_t c = S->cand, s = S->sub, filled = 0;
     const uint64_t mod = q.modulo, off = q.offset;
@@ -234,29 +237,38 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
     // lanes of a hashing wave run the same number of blocks.  task[i] = the pair hashed by lane-slot i (blob
     // offset, length, window slot), so the hashing kernel reads 16 contiguous bytes per lane and then the packet;
     // the send order (slot order) is untouched.
+    // Bins run from the most blocks down, so the longest packets start first (they set the window's tail).
     __shared__ uint32_t hist[kSortBins];
-    __shared__ uint16_t keyb[kMaxWindow];
     const uint32_t blk = q.hash_kind >= DSY_SHA384 ? 128u : 64u, lenb = q.hash_kind >= DSY_SHA384 ? 16u : 8u;
+    auto bin_of = [&](uint64_t len) {
+        return (uint32_t)kSortBins - 1u - min(n_blocks(q.prefix_len + (uint32_t)len, blk, lenb), (uint32_t)kSortBins - 1);
+    };
     for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads) hist[i] = 0;
     __syncthreads();
     for (uint64_t t = threadIdx.x; t < filled; t += kFillThreads) {
         const uint64_t row = out[t];
-        const uint32_t len = (uint32_t)(L.st.offsets[row + 1] - L.st.offsets[row]);
-        const uint32_t nb = min(n_blocks(q.prefix_len + len, blk, lenb), (uint32_t)kSortBins - 1);
-        keyb[t] = (uint16_t)nb;
-        atomicAdd(&hist[nb], 1u);
+        atomicAdd(&hist[bin_of(L.st.offsets[row + 1] - L.st.offsets[row])], 1u);
     }
     __syncthreads();
-    if (threadIdx.x == 0) {  // exclusive scan of kSortBins counters (cheap next to the fill itself)
-        uint32_t run = 0;
-        for (uint32_t i = 0; i < kSortBins; ++i) {
-            const uint32_t h = hist[i];
-            hist[i] = run;
+    if (threadIdx.x < 64) {  // exclusive scan of the kSortBins counters by one wave
+        const uint32_t per = kSortBins / 64, lane = threadIdx.x;
+        uint32_t sum = 0;
+        for (uint32_t i = 0; i < per; ++i) sum += hist[lane * per + i];
+        uint32_t incl = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(incl, d, 64);
+            if ((int)lane >= d) incl += o;
+        }
+        uint32_t run = incl - sum;
+        for (uint32_t i = 0; i < per; ++i) {
+            const uint32_t h = hist[lane * per + i];
+            hist[lane * per + i] = run;
             run += h;
         }
     }
     __syncthreads();
-    PairTask* task = L.task + (uint64_t)r * W;
+    PairTask* task = L.task + (uint64_t)a_slot * W;
     for (uint64_t t = threadIdx.x; t < filled; t += kFillThreads) {
         const uint64_t row = out[t];
         const uint64_t a = L.st.offsets[row], e = L.st.offsets[row + 1];  // just read above: cache hits
@@ -264,7 +276,7 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
         tk.off = a;
         tk.len = (uint32_t)(e - a);
         tk.slot = (uint32_t)t;
-        task[atomicAdd(&hist[keyb[t]], 1u)] = tk;
+        task[atomicAdd(&hist[bin_of(e - a)], 1u)] = tk;
     }
 }
 
@@ -284,7 +296,8 @@ __global__ void __launch_bounds__(256) k_pair_test(RespondLaunch L, const uint32
     // chunk-major task order: wave-task v hashes 64-pair chunk (v / n_list) of claim (v % n_list), so the
     // non-empty chunks of every claim come first and spread evenly over the grid
     for (uint64_t wv = wave0; wv < total_waves; wv += wstride) {
-        const uint32_t r = req_list[wv % n_list];
+        const uint32_t a_slot = req_list[wv % n_list];
+        const uint32_t r = L.act[a_slot];
         const uint64_t i0 = (wv / n_list) * 64;
         const uint64_t n = L.state[r].n_window;
         if (i0 >= n) continue;  // wave-uniform: past this claim's window
@@ -294,7 +307,7 @@ __global__ void __launch_bounds__(256) k_pair_test(RespondLaunch L, const uint32
         uint32_t t = 0;
         KeyView kv{L.st.blob, 0u, q.prefix, q.prefix_len};  // idle lanes hash an empty key
         if (active) {
-            const PairTask tk = L.task[(uint64_t)r * W + i];
+            const PairTask tk = L.task[(uint64_t)a_slot * W + i];
             t = tk.slot;
             kv.key = L.st.blob + tk.off;
             kv.len = tk.len;
@@ -318,7 +331,7 @@ __global__ void __launch_bounds__(256) k_pair_test(RespondLaunch L, const uint32
         }
         const uint32_t nb = active ? n_blocks(kv.plen + kv.len, H::block_bytes, H::len_bytes) : 0u;
         if (active) {
-            L.miss[(uint64_t)r * W + t] = (uint8_t)(ok ^ 1u);
+            L.miss[(uint64_t)a_slot * W + t] = (uint8_t)(ok ^ 1u);
             acc_blocks += nb;
             acc_bytes += kv.len;
         }
@@ -397,9 +410,13 @@ __device__ __forceinline__ int64_t wave_inclusive_scan(int64_t v) {
 }
 
 __global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
-    const uint32_t r = blockIdx.x;
+    const uint32_t a_slot = blockIdx.x;
+    const uint32_t r = L.act[a_slot];
     ReqState* S = &L.state[r];
-    if (S->done) return;
+    if (S->done) {
+        if (threadIdx.x == 0) L.act_done[a_slot] = 1;
+        return;
+    }
     const uint64_t W = L.window;
     const uint64_t n = S->n_window;
     const uint32_t lane = threadIdx.x;
@@ -411,11 +428,11 @@ __global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
     for (uint64_t t0 = 0; t0 < n && !done; t0 += 64) {
         const uint64_t t = t0 + lane;
         const bool valid = t < n;
-        const bool miss = valid && L.miss[(uint64_t)r * W + t];
+        const bool miss = valid && L.miss[(uint64_t)a_slot * W + t];
         uint64_t row = 0;
         int64_t len = 0;
         if (miss) {
-            row = L.pair_row[(uint64_t)r * W + t];
+            row = L.pair_row[(uint64_t)a_slot * W + t];
             len = (int64_t)(L.st.offsets[row + 1] - L.st.offsets[row]);
         }
         const int64_t incl = wave_inclusive_scan(len);
@@ -453,7 +470,7 @@ __global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
         S->overflow = overflow;
         if (overflow) L.flags[1] = 1;
         if (done || S->exhausted) S->done = 1;
-        else L.flags[0] = 1;
+        L.act_done[a_slot] = (uint8_t)S->done;
         atomicAdd((unsigned long long*)&L.counters[kCntPairs], (unsigned long long)n);
         atomicAdd((unsigned long long*)&L.counters[kCntUseful], (unsigned long long)useful);
     }
@@ -542,14 +559,14 @@ hipError_t launch_plan(const RespondLaunch& L) {
 }
 
 hipError_t launch_fill(const RespondLaunch& L) {
-    if (!L.R) return hipSuccess;
-    hipLaunchKernelGGL(k_fill, dim3(L.R), dim3(kFillThreads), 0, L.stream, L);
+    if (!L.n_act) return hipSuccess;
+    hipLaunchKernelGGL(k_fill, dim3(L.n_act), dim3(kFillThreads), 0, L.stream, L);
     return hipGetLastError();
 }
 
 hipError_t launch_compact(const RespondLaunch& L) {
-    if (!L.R) return hipSuccess;
-    hipLaunchKernelGGL(k_compact, dim3(L.R), dim3(64), 0, L.stream, L);
+    if (!L.n_act) return hipSuccess;
+    hipLaunchKernelGGL(k_compact, dim3(L.n_act), dim3(64), 0, L.stream, L);
     return hipGetLastError();
 }
 

@@ -137,3 +137,22 @@ def test_ref_false_positives():
                 assert bloom.contains_many([str(i).encode() for i in range(n)]).all()
                 fp = int(bloom.contains_many([str(i).encode() for i in range(n, n + 10000)]).sum())
                 assert abs(fp / 10000.0 - f) <= 0.05
+
+
+@pytest.mark.parametrize("m,f,prefix", [(10160, 0.01, b""), (10160, 0.01, b"\x05\x06\x07\x08"), (4096, 0.001, b"x"),
+                                        (1 << 20, 0.01, b"\x07"), (1 << 16, 0.0001, b"abcde"),
+                                        (1 << 15, 0.001, b"\x01\x02")])
+def test_length_sorted_batches_against_oracle(m, f, prefix):
+    """Batches above the sort threshold (dsy_capi kLenSortMin) hash in length-bucketed order, with LDS-DMA staging
+    for MD5: adds and tests of 40 k heavy-tailed keys in every family against the oracle, outputs in key order."""
+    rng = np.random.Generator(np.random.PCG64(m ^ len(prefix)))
+    lengths = np.minimum((rng.pareto(1.2, 40_000) + 1) * 60, 20_000).astype(np.int64)
+    lengths[:6] = [0, 1, 55, 56, 63, 64]
+    keys = [rng.bytes(int(n)) for n in lengths]
+    bf, ref = BloomFilter(m, f, prefix), OracleBloom.from_m_f(m, f, prefix)
+    bf.add_keys(keys[:35_000])
+    ref.add_keys(keys[:35_000])
+    assert bf.bytes == ref.to_bytes()
+    blob, off = pack_keys(keys)
+    got = _native.default_context().bloom_test(bf.params, blob, off, bf.bytes)
+    assert got.astype(bool).tolist() == [k in ref for k in keys]
