@@ -215,7 +215,7 @@ def main():
     if rank == 0 and world == 1 and args.cpu_claims > 0:
         cpu = cpu_baseline(args, ctx, lib, store, reqs, claims, blob, offsets, total_bytes, N, fblob)
 
-    extra = set(x for x in args.extra.split(",") if x)
+    extra = set(x for x in args.extra.split(",") if x and x != "none")
 
     gossip = None
     if "3" in extra and args.sim_peers > 0:

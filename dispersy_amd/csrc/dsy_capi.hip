@@ -941,6 +941,10 @@ int dsy_sim_build_claims(dsy_ctx* c, const dsy_sim_config* cfg, uint32_t round, 
     L.bits = (uint32_t*)d_bits;
     L.out = d_out;
     if ((rc = sim_cursor(c, h_offsets, n_ranks, &L.cursor))) return rc;
+    void* ds;
+    if ((rc = ws_get(c, "sim_slots", 4 * std::max<uint64_t>(cfg->peer_end - cfg->peer_begin, 1), &ds))) return rc;
+    L.slots = (uint32_t*)ds;
+    HIP_TRY(launch_sim(kSimClaimSlots, L));
     PendingTimer t;
     timer_begin(c, &t, kTimeBuild);
     HIP_TRY(launch_sim(kSimBuild, L));
@@ -978,19 +982,25 @@ int dsy_sim_respond(dsy_ctx* c, const dsy_sim_config* cfg, const uint8_t* d_ublo
     L.n_in = n_claims;
     L.out = d_out;
     void* dt;
-    if ((rc = ws_get(c, "sim_tested", 16, &dt))) return rc;
-    HIP_TRY(hipMemsetAsync(dt, 0, 16, c->stream));
+    if ((rc = ws_get(c, "sim_tested", 8 * kSimTestedSlots, &dt))) return rc;
+    HIP_TRY(hipMemsetAsync(dt, 0, 8 * kSimTestedSlots, c->stream));
     L.tested = (unsigned long long*)dt;
     if ((rc = sim_cursor(c, h_offsets, n_ranks, &L.cursor))) return rc;
+    void* ds;
+    if ((rc = ws_get(c, "sim_slots", 4 * std::max<uint64_t>(n_claims, 1), &ds))) return rc;
+    L.slots = (uint32_t*)ds;
+    HIP_TRY(launch_sim(kSimRespSlots, L));
     PendingTimer t;
     timer_begin(c, &t, kTimePairTest);
     HIP_TRY(launch_sim(kSimRespond, L));
     timer_end(c, &t);
-    uint64_t* h = (uint64_t*)c->pinned + 16;
-    HIP_TRY(hipMemcpyAsync(h, dt, 8, hipMemcpyDeviceToHost, c->stream));
+    uint64_t* h = (uint64_t*)c->pinned + 128;
+    HIP_TRY(hipMemcpyAsync(h, dt, 8 * kSimTestedSlots, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     timers_collect(c);
-    if (out_tested) *out_tested = h[0];
+    uint64_t tested = 0;
+    for (uint32_t i = 0; i < kSimTestedSlots; ++i) tested += h[i];
+    if (out_tested) *out_tested = tested;
     return DSY_OK;
 }
 

@@ -141,7 +141,9 @@ hipError_t launch_pack(const RespondLaunch& L, uint64_t* packed, uint64_t* packe
 // ---------------------------------------------------------------------------------------- simulator
 static constexpr uint32_t kSimFilterWordsMax = 2048;  // m <= 65536 bits
 static constexpr uint32_t kSimRespMax = DSY_SIM_RESP_MAX;
-enum { kSimSeed = 0, kSimClaimCounts, kSimBuild, kSimRespCounts, kSimRespond, kSimMerge, kSimStats };
+enum { kSimSeed = 0, kSimClaimCounts, kSimBuild, kSimRespCounts, kSimRespond, kSimMerge, kSimStats, kSimClaimSlots,
+       kSimRespSlots };
+static constexpr uint32_t kSimTestedSlots = 64;  // k_sim_respond spreads its tested-pair counter over 64 words
 
 struct SimLaunch {
     dsy_sim_config cfg;
@@ -154,6 +156,7 @@ struct SimLaunch {
     uint64_t n_in;
     uint8_t* out;
     uint32_t* cursor;
+    uint32_t* slots;
     uint32_t* counts;
     unsigned long long* tested;
     unsigned long long* stats;

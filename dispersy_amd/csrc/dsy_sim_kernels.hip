@@ -34,6 +34,27 @@ __device__ __forceinline__ uint32_t sim_owner(const dsy_sim_config& c, uint64_t 
     return (uint32_t)(p / c.peers_per_rank);
 }
 
+// counts[key] += 1 for every active lane, with one atomic per distinct key in the wave (a million lanes adding to
+// the same rank counter one by one serialise on one address); returns the lane's old value + its rank among the
+// wave's lanes with the same key, i.e. a unique slot when counts holds running cursors
+__device__ __forceinline__ uint32_t wave_count(uint32_t* counts, uint32_t key, bool active) {
+    uint64_t pending = __ballot(active);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    uint32_t mine = 0;
+    while (pending) {
+        const int leader = __builtin_ctzll(pending);
+        const uint32_t k = __shfl(key, leader, 64);
+        const uint64_t same = __ballot(active && key == k) & pending;
+        uint32_t base = 0;
+        if (lane == (uint32_t)leader) base = atomicAdd(&counts[k], (uint32_t)__popcll(same));
+        base = __shfl(base, leader, 64);
+        if ((same >> lane) & 1) mine = base + (uint32_t)__popcll(same & below);
+        pending &= ~same;
+    }
+    return mine;
+}
+
 // ------------------------------------------------------------------------------------------ seeding
 __global__ void k_sim_seed(dsy_sim_config c, uint32_t* __restrict__ bits, uint32_t initial) {
     const uint64_t lp = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -83,50 +104,106 @@ __device__ __forceinline__ uint32_t wave_list_ids(const uint32_t* __restrict__ b
 // --------------------------------------------------------------------------------------- claims
 __global__ void k_sim_claim_counts(dsy_sim_config c, uint32_t round, uint32_t* __restrict__ counts) {
     const uint64_t lp = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (lp >= c.peer_end - c.peer_begin) return;
-    atomicAdd(&counts[sim_owner(c, sim_partner(c, round, c.peer_begin + lp))], 1u);
+    const bool active = lp < c.peer_end - c.peer_begin;
+    wave_count(counts, active ? sim_owner(c, sim_partner(c, round, c.peer_begin + lp)) : 0u, active);
+}
+
+// slot of every local requester's claim record: cursor[dest] starts at the destination's first record
+__global__ void k_sim_claim_slots(dsy_sim_config c, uint32_t round, uint32_t* __restrict__ cursor,
+                                  uint32_t* __restrict__ slots) {
+    const uint64_t lp = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool active = lp < c.peer_end - c.peer_begin;
+    const uint32_t s = wave_count(cursor, active ? sim_owner(c, sim_partner(c, round, c.peer_begin + lp)) : 0u, active);
+    if (active) slots[lp] = s;
+}
+
+// slot of every received claim's response record (grouped by the requester's rank)
+__global__ void k_sim_resp_slots(dsy_sim_config c, const uint8_t* __restrict__ claims, uint64_t n_claims,
+                                 uint32_t* __restrict__ cursor, uint32_t* __restrict__ slots) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool active = i < n_claims;
+    uint32_t owner = 0;
+    if (active) owner = sim_owner(c, ((const dsy_sim_claim_header*)(claims + i * c.claim_bytes))->requester);
+    const uint32_t s = wave_count(cursor, owner, active);
+    if (active) slots[i] = s;
 }
 
 static constexpr uint32_t kSimListCap = 2048;
 
-// one wave per local requester: list its packets, hash them into an LDS-resident filter (ds_or_b32; lanes that
-// hit the same word in one instruction are merged by the LDS atomic unit), write the claim record
+// LDS of one requester wave in k_sim_build_claims: id list, the same ids sorted by block count, a 64-bin
+// histogram, the prefix byte and the filter (sized by m at launch)
+__host__ __device__ constexpr uint32_t sim_build_wave_lds(uint32_t nwords) {
+    return (4 * kSimListCap + 256 + 16 + nwords * 4 + 15) / 16 * 16;
+}
+
+// one wave per local requester: list its packets, put the claimed ones in block-count order (a counting sort in
+// LDS: the filter is an OR, so the hashing order is free, and equal-length lanes finish together), hash them into
+// an LDS-resident filter (ds_or_b32; lanes that hit the same word in one instruction are merged by the LDS atomic
+// unit), write the claim record
 template <class H, int CHUNK>
 __global__ void __launch_bounds__(256) k_sim_build_claims(dsy_sim_config c, uint32_t round, const uint8_t* __restrict__ ublob,
                                                           const uint64_t* __restrict__ uoff, const uint32_t* __restrict__ bits,
-                                                          uint8_t* __restrict__ out, uint32_t* __restrict__ cursor) {
-    __shared__ uint16_t lists[4][kSimListCap];
-    __shared__ uint32_t filt[4][kSimFilterWordsMax];
-    __shared__ uint8_t pre[4][4];
+                                                          uint8_t* __restrict__ out, const uint32_t* __restrict__ slots) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t sim_lds[];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t lp = (uint64_t)blockIdx.x * 4 + wv;
     if (lp >= c.peer_end - c.peer_begin) return;  // wave-uniform
-    const uint64_t p = c.peer_begin + lp;
     const uint32_t nwords = (uint32_t)((c.m_bits + 31) / 32);
-    for (uint32_t i = lane; i < nwords; i += 64) filt[wv][i] = 0;
-    uint32_t n = wave_list_ids(bits + lp * c.words, c.words, lists[wv], kSimListCap);
+    uint8_t* mine = sim_lds + wv * sim_build_wave_lds(nwords);
+    uint16_t* list = (uint16_t*)mine;
+    uint16_t* sorted = list + kSimListCap;
+    uint32_t* hist = (uint32_t*)(sorted + kSimListCap);
+    uint8_t* pre = (uint8_t*)(hist + 64);
+    uint32_t* filt = (uint32_t*)(pre + 16);
+    const uint64_t p = c.peer_begin + lp;
+    for (uint32_t i = lane; i < nwords; i += 64) filt[i] = 0;
+    hist[lane] = 0;
+    uint32_t n = wave_list_ids(bits + lp * c.words, c.words, list, kSimListCap);
     // _select_and_fix(..., 0, capacity, True): the first capacity packets; over-full drops the (capacity+1)-th
     // global time (global times are distinct here) and the range ends at the last kept one
     uint64_t time_high = 0x7fffffffffffffffull;
     if (n > c.capacity) {
         n = c.capacity;
-        time_high = (uint64_t)lists[wv][n - 1] + 1;
+        time_high = (uint64_t)list[n - 1] + 1;
     }
     const uint32_t prefix = sim_prefix(c, round, p);
-    if (lane == 0) pre[wv][0] = (uint8_t)prefix;
+    if (lane == 0) pre[0] = (uint8_t)prefix;
+    const uint32_t blk = H::block_bytes, lenb = H::len_bytes;
+    auto bin_of = [&](uint32_t id) { return 63u - min(n_blocks(1 + (uint32_t)(uoff[id + 1] - uoff[id]), blk, lenb), 63u); };
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t i = lane; i < n; i += 64) atomicAdd(&hist[bin_of(list[i])], 1u);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    {
+        const uint32_t h = hist[lane];
+        uint32_t incl = h;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(incl, d, 64);
+            if ((int)lane >= d) incl += o;
+        }
+        hist[lane] = incl - h;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t i = lane; i < n; i += 64) {
+        const uint32_t id = list[i];
+        sorted[atomicAdd(&hist[bin_of(id)], 1u)] = (uint16_t)id;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
     for (uint32_t i0 = 0; i0 < n; i0 += 64) {
         const uint32_t i = i0 + lane;
         if (i < n) {
-            const uint32_t id = lists[wv][i];
-            KeyView kv{ublob + uoff[id], (uint32_t)(uoff[id + 1] - uoff[id]), pre[wv], 1};
+            const uint32_t id = sorted[i];
+            KeyView kv{ublob + uoff[id], (uint32_t)(uoff[id + 1] - uoff[id]), pre, 1};
             H st;
             hash_key<H>(kv, st);
 #pragma unroll
             for (int j = 0; j < ChunkLimit<H, CHUNK>::kmax; ++j) {
                 if (j < (int)c.k) {
                     const uint64_t pos = bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, j), c.m_bits);
-                    atomicOr(&filt[wv][pos >> 5], 1u << (pos & 31));
+                    atomicOr(&filt[pos >> 5], 1u << (pos & 31));
                 }
             }
         }
@@ -134,10 +211,7 @@ __global__ void __launch_bounds__(256) k_sim_build_claims(dsy_sim_config c, uint
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
     const uint64_t q = sim_partner(c, round, p);
-    uint32_t slot = 0;
-    if (lane == 0) slot = atomicAdd(&cursor[sim_owner(c, q)], 1u);
-    slot = __shfl(slot, 0, 64);
-    uint8_t* rec = out + (uint64_t)slot * c.claim_bytes;
+    uint8_t* rec = out + (uint64_t)slots[lp] * c.claim_bytes;
     if (lane == 0) {
         dsy_sim_claim_header h;
         h.requester = p;
@@ -148,16 +222,17 @@ __global__ void __launch_bounds__(256) k_sim_build_claims(dsy_sim_config c, uint
         *(dsy_sim_claim_header*)rec = h;
     }
     uint32_t* fw = (uint32_t*)(rec + sizeof(dsy_sim_claim_header));
-    for (uint32_t i = lane; i < nwords; i += 64) fw[i] = filt[wv][i];
+    for (uint32_t i = lane; i < nwords; i += 64) fw[i] = filt[i];
 }
 
 // -------------------------------------------------------------------------------------- responses
 __global__ void k_sim_resp_counts(dsy_sim_config c, const uint8_t* __restrict__ claims, uint64_t n_claims,
                                   uint32_t* __restrict__ counts) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_claims) return;
-    const dsy_sim_claim_header* h = (const dsy_sim_claim_header*)(claims + i * c.claim_bytes);
-    atomicAdd(&counts[sim_owner(c, h->requester)], 1u);
+    const bool active = i < n_claims;
+    uint32_t owner = 0;
+    if (active) owner = sim_owner(c, ((const dsy_sim_claim_header*)(claims + i * c.claim_bytes))->requester);
+    wave_count(counts, owner, active);
 }
 
 // one wave per incoming claim: the responder's packets in global-time order, 64 at a time; hash + probe; send the
@@ -167,7 +242,7 @@ template <class H, int CHUNK>
 __global__ void __launch_bounds__(256) k_sim_respond(dsy_sim_config c, const uint8_t* __restrict__ ublob,
                                                      const uint64_t* __restrict__ uoff, const uint32_t* __restrict__ bits,
                                                      const uint8_t* __restrict__ claims, uint64_t n_claims,
-                                                     uint8_t* __restrict__ out, uint32_t* __restrict__ cursor,
+                                                     uint8_t* __restrict__ out, const uint32_t* __restrict__ slots,
                                                      unsigned long long* __restrict__ tested) {
     __shared__ uint16_t lists[4][kSimListCap];
     __shared__ uint32_t filt[4][kSimFilterWordsMax];
@@ -231,18 +306,14 @@ __global__ void __launch_bounds__(256) k_sim_respond(dsy_sim_config c, const uin
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
-    const uint32_t q_owner = sim_owner(c, h.requester);
-    uint32_t slot = 0;
-    if (lane == 0) slot = atomicAdd(&cursor[q_owner], 1u);
-    slot = __shfl(slot, 0, 64);
-    uint8_t* o = out + (uint64_t)slot * c.resp_bytes;
+    uint8_t* o = out + (uint64_t)slots[ci] * c.resp_bytes;
     dsy_sim_resp_header* oh = (dsy_sim_resp_header*)o;
     const uint32_t cnt = min(sent, (uint32_t)kSimRespMax);
     if (lane == 0) {
         oh->requester = h.requester;
         oh->count = cnt;
         oh->overflow = sent > kSimRespMax;
-        atomicAdd(tested, (unsigned long long)ntested);
+        atomicAdd(&tested[blockIdx.x & (kSimTestedSlots - 1)], (unsigned long long)ntested);  // spread
     }
     uint16_t* ids = (uint16_t*)(o + sizeof(dsy_sim_resp_header));
     if (lane < cnt) ids[lane] = outl[wv][lane];
@@ -281,12 +352,13 @@ static hipError_t sim_family(int op, const SimLaunch& L) {
     const uint64_t local = L.cfg.peer_end - L.cfg.peer_begin;
     if (op == 0) {
         if (!local) return hipSuccess;
-        hipLaunchKernelGGL((k_sim_build_claims<H, CHUNK>), dim3((uint32_t)((local + 3) / 4)), dim3(256), 0, L.stream, L.cfg,
-                           L.round, L.ublob, L.uoff, L.bits, L.out, L.cursor);
+        const size_t lds = 4 * (size_t)sim_build_wave_lds((uint32_t)((L.cfg.m_bits + 31) / 32));
+        hipLaunchKernelGGL((k_sim_build_claims<H, CHUNK>), dim3((uint32_t)((local + 3) / 4)), dim3(256), lds, L.stream, L.cfg,
+                           L.round, L.ublob, L.uoff, L.bits, L.out, L.slots);
     } else {
         if (!L.n_in) return hipSuccess;
         hipLaunchKernelGGL((k_sim_respond<H, CHUNK>), dim3((uint32_t)((L.n_in + 3) / 4)), dim3(256), 0, L.stream, L.cfg,
-                           L.ublob, L.uoff, L.bits, L.in, L.n_in, L.out, L.cursor, L.tested);
+                           L.ublob, L.uoff, L.bits, L.in, L.n_in, L.out, L.slots, L.tested);
     }
     return hipGetLastError();
 }
@@ -300,6 +372,12 @@ hipError_t launch_sim(int op, const SimLaunch& L) {
             return hipGetLastError();
         case kSimClaimCounts:
             if (local) hipLaunchKernelGGL(k_sim_claim_counts, dim3((uint32_t)((local + 255) / 256)), dim3(256), 0, L.stream, c, L.round, L.counts);
+            return hipGetLastError();
+        case kSimClaimSlots:
+            if (local) hipLaunchKernelGGL(k_sim_claim_slots, dim3((uint32_t)((local + 255) / 256)), dim3(256), 0, L.stream, c, L.round, L.cursor, L.slots);
+            return hipGetLastError();
+        case kSimRespSlots:
+            if (L.n_in) hipLaunchKernelGGL(k_sim_resp_slots, dim3((uint32_t)((L.n_in + 255) / 256)), dim3(256), 0, L.stream, c, L.in, L.n_in, L.cursor, L.slots);
             return hipGetLastError();
         case kSimRespCounts:
             if (L.n_in) hipLaunchKernelGGL(k_sim_resp_counts, dim3((uint32_t)((L.n_in + 255) / 256)), dim3(256), 0, L.stream, c, L.in, L.n_in, L.counts);

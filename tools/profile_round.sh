@@ -1,10 +1,11 @@
 #!/bin/bash
-# Profile bench.py on the GPU box: kernel trace + stats, then separate PMC passes (FETCH_SIZE, WRITE_SIZE, SQ).
-# Run through gpurun from the repo root.  Each step has its own time limit; steps are chained with &&.
+# Profile bench.py on the GPU box: kernel trace + stats of the full bench (every config), then separate PMC passes
+# (FETCH_SIZE, WRITE_SIZE, SQ) over the headline (config 2) only.  Run through gpurun from the repo root; each step
+# has its own time limit and the steps are chained with &&.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 ARGS="--cpu-claims 0 ${BENCH_ARGS:-}"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- python bench.py --steps 20 $ARGS > gpurun_out/prof.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o p --output-format csv -- python bench.py --steps 5 --warmup 1 $ARGS > gpurun_out/pmc_fetch.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o p --output-format csv -- python bench.py --steps 5 --warmup 1 $ARGS > gpurun_out/pmc_write.log 2>&1 &&
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_LDS -d gpurun_out/pmc_sq -o p --output-format csv -- python bench.py --steps 5 --warmup 1 $ARGS > gpurun_out/pmc_sq.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o bench --output-format csv -- python bench.py --steps 20 $ARGS > gpurun_out/prof.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o p --output-format csv -- python bench.py --steps 5 --warmup 1 --extra none $ARGS > gpurun_out/pmc_fetch.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o p --output-format csv -- python bench.py --steps 5 --warmup 1 --extra none $ARGS > gpurun_out/pmc_write.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_LDS -d gpurun_out/pmc_sq -o p --output-format csv -- python bench.py --steps 5 --warmup 1 --extra none $ARGS > gpurun_out/pmc_sq.log 2>&1
