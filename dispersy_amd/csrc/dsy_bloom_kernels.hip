@@ -7,15 +7,15 @@
 // contiguously.  Small filters (the ~10 Kbit MTU filters of community.py:637-666) live in LDS for the whole
 // workgroup: the build ORs bits with ds_or_b32 and merges the LDS filter into HBM once per workgroup; the test
 // stages the filter into LDS once and probes it there.  Large filters (m = 2^20..2^24 bits, BASELINE config 4)
-// are probed/ORed in place in L2/HBM with global atomics.  MD5 (load-bound) stages packet bytes through LDS with
-// LDS-DMA when the filter is small (dsy_message.h hash_key_dma); the SHA families load directly (compute-bound).
+// are probed/ORed in place in L2/HBM with global atomics.  MD5 and SHA-1 stage packet bytes through LDS with
+// LDS-DMA when the filter is small (dsy_message.h hash_key_dma_reg); SHA-2 loads directly.
 #include "dsy_kernels.h"
 
 namespace dsy {
 
 static constexpr uint32_t kLenBins = 1024;
-static constexpr int kDmaS = 2, kDmaNB = 2;
-static constexpr size_t kDmaWaveBytes = DmaGeometry<kDmaS, kDmaNB>::kWaveBytes;
+static constexpr int kDmaS = 2;
+static constexpr size_t kDmaWaveBytes = DmaGeometry<kDmaS, 1>::kWaveBytes;
 
 __device__ __forceinline__ uint32_t len_bin(uint64_t len, const LenSort& s) {
     return kLenBins - 1u - min(n_blocks(s.plen + (uint32_t)len, s.blk, s.lenb), kLenBins - 1u);
@@ -138,7 +138,7 @@ __global__ void __launch_bounds__(256) k_bloom(const DevParams* __restrict__ prm
             }
         }
         H st;
-        if constexpr (DMA) hash_key_dma<H, kDmaS, kDmaNB>(kv, st, my_dma);
+        if constexpr (DMA) hash_key_dma_reg<H, kDmaS>(kv, st, my_dma);
         else hash_key<H>(kv, st);
         if (active) {
             uint32_t ok = 1;
@@ -197,8 +197,9 @@ hipError_t launch_len_sort(const LenSort& s, const uint64_t* offsets, const uint
 
 template <class H, int CHUNK, int OP>
 static hipError_t launch_op(const BloomLaunch& L, uint32_t grid) {
-    // LDS-DMA staging for MD5 whenever the filter is small enough to leave room for it (2 workgroups per CU)
-    const bool dma = H::kind == DSY_MD5 && L.prm_prefix_len <= 4 && (!L.use_lds || L.nwords * 4 <= 16 * 1024);
+    // LDS-DMA staging for MD5 / SHA-1 whenever the filter is small enough to leave room for it
+    const bool dma = (H::kind == DSY_MD5 || H::kind == DSY_SHA1) && L.prm_prefix_len <= 4 &&
+                     (!L.use_lds || L.nwords * 4 <= 16 * 1024);
     const size_t lds = (dma ? 4 * kDmaWaveBytes : 0) + (L.use_lds ? (size_t)L.nwords * 4 : 0);
     if (dma) {
         if constexpr (H::block_bytes == 64)

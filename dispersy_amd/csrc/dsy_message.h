@@ -195,7 +195,11 @@ struct DmaGeometry {
     static constexpr int kWaveBytes = NB * kStageBytes;
 };
 
-template <class H, int S = 2, int NB = 2>
+// Flags: kDmaSkipDead -- (NB == 2 only, where every wait is vmcnt(0)) lanes whose key has ended issue no load;
+// kDmaPrio -- raise the wave's issue priority while it issues a stage's loads.
+enum { kDmaSkipDead = 1, kDmaPrio = 2 };
+
+template <class H, int S = 2, int NB = 2, int FLAGS = 0>
 __device__ __forceinline__ void hash_key_dma(const KeyView& kv, H& st, uint8_t* lds_wave) {
     static_assert(H::block_bytes == 64, "LDS-DMA staging is for 64-byte blocks");
     using G = DmaGeometry<S, NB>;
@@ -212,6 +216,7 @@ __device__ __forceinline__ void hash_key_dma(const KeyView& kv, H& st, uint8_t* 
     const uint64_t base = (uint64_t)(uintptr_t)kv.key - r;  // window of block b starts at base + 64 b
     auto issue = [&](uint32_t s) {
         uint8_t* buf = lds_wave + (s % NB) * G::kStageBytes;
+        if (FLAGS & kDmaPrio) __builtin_amdgcn_s_setprio(3);
 #pragma unroll
         for (int i = 0; i < G::kInsts; ++i) {
             const int p = G::kKeysPerInst * i + (int)(lane / G::kChunks);
@@ -219,11 +224,19 @@ __device__ __forceinline__ void hash_key_dma(const KeyView& kv, H& st, uint8_t* 
             const uint32_t pend = __shfl((int)total, p, 64);
             const uint32_t c = ((lane % G::kChunks) + ((uint32_t)p >> G::kShift)) % G::kChunks;
             const uint64_t b64 = ((uint64_t)bhi << 32) | blo;
-            // always issue (the vmcnt accounting counts instructions); stages past the key re-read its start
-            const uint64_t a = (s * (S * 64) < pend) ? b64 + s * (S * 64) + 16 * c : b64;
-            __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)a,
-                                             (__attribute__((address_space(3))) void*)(buf + i * 1024), 16, 0, 0);
+            const bool live = s * (S * 64) < pend;
+            if ((FLAGS & kDmaSkipDead) && NB == 2) {
+                if (live)
+                    __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)(b64 + s * (S * 64) + 16 * c),
+                                                     (__attribute__((address_space(3))) void*)(buf + i * 1024), 16, 0, 0);
+            } else {
+                // always issue (the vmcnt accounting counts instructions); stages past the key re-read its start
+                const uint64_t a = live ? b64 + s * (S * 64) + 16 * c : b64;
+                __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)a,
+                                                 (__attribute__((address_space(3))) void*)(buf + i * 1024), 16, 0, 0);
+            }
         }
+        if (FLAGS & kDmaPrio) __builtin_amdgcn_s_setprio(0);
     };
     st.init();
 #pragma unroll
@@ -271,6 +284,88 @@ __device__ __forceinline__ void hash_key_dma(const KeyView& kv, H& st, uint8_t* 
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this stage's reads retire before its buffer refills
         __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// Single-buffer variant of hash_key_dma: one S*64-byte stage per key in LDS (S*4 KiB per wave); the stage is
+// copied to registers as soon as it lands, and the next stage's DMA into the same buffer is issued before the
+// blocks are compressed from the registers.  Half the LDS of the double-buffered form for the same amount in
+// flight, so twice the waves fit a CU.  Dead lanes (key already ended) issue nothing; every wait is vmcnt(0).
+template <class H, int S = 1>
+__device__ __forceinline__ void hash_key_dma_reg(const KeyView& kv, H& st, uint8_t* lds_wave) {
+    static_assert(H::block_bytes == 64, "LDS-DMA staging is for 64-byte blocks");
+    using G = DmaGeometry<S, 1>;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t r = kv.plen;
+    const uint32_t total = r + kv.len;
+    const uint32_t nb = n_blocks(total, 64, H::len_bytes);
+    uint32_t nbmax = nb;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, d, 64));
+    const uint32_t nst = (nbmax + S - 1) / S;
+    uint32_t preword = 0;
+    for (uint32_t j = 0; j < r; ++j) preword |= (uint32_t)kv.pre[j] << (8 * j);
+    const uint64_t base = (uint64_t)(uintptr_t)kv.key - r;
+    auto issue = [&](uint32_t s) {
+#pragma unroll
+        for (int i = 0; i < G::kInsts; ++i) {
+            const int p = G::kKeysPerInst * i + (int)(lane / G::kChunks);
+            const uint32_t blo = __shfl((int)(uint32_t)base, p, 64), bhi = __shfl((int)(uint32_t)(base >> 32), p, 64);
+            const uint32_t pend = __shfl((int)total, p, 64);
+            const uint32_t c = ((lane % G::kChunks) + ((uint32_t)p >> G::kShift)) % G::kChunks;
+            const uint64_t b64 = ((uint64_t)bhi << 32) | blo;
+            if (s * (S * 64) < pend)
+                __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)(b64 + s * (S * 64) + 16 * c),
+                                                 (__attribute__((address_space(3))) void*)(lds_wave + i * 1024), 16, 0, 0);
+        }
+    };
+    st.init();
+    if (nst) issue(0);
+    for (uint32_t s = 0; s < nst; ++s) {
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): stage s has landed
+        __builtin_amdgcn_wave_barrier();
+        uint32_t w[S][16];
+#pragma unroll
+        for (int bb = 0; bb < S; ++bb) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t c = 4 * bb + q;
+                const uint32_t slot = (c - (lane >> G::kShift)) % G::kChunks;
+                const uint4 v = *(const uint4*)(lds_wave + (lane / G::kKeysPerInst) * 1024 +
+                                                16 * (G::kChunks * (lane % G::kKeysPerInst) + slot));
+                w[bb][4 * q] = v.x; w[bb][4 * q + 1] = v.y; w[bb][4 * q + 2] = v.z; w[bb][4 * q + 3] = v.w;
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the buffer is free again
+        __builtin_amdgcn_wave_barrier();
+        if (s + 1 < nst) issue(s + 1);
+#pragma unroll
+        for (int bb = 0; bb < S; ++bb) {
+            const uint32_t b = S * s + bb;
+            if (b < nb) {
+                uint32_t* x = w[bb];
+                const uint32_t o0 = b * 64;
+                if (b == 0 && r) x[0] = (x[0] & ~low_bytes_mask(r)) | preword;
+                if (o0 + 64 > total) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int rel = (int)total - (int)o0 - 4 * i;
+                        if (rel <= 0) x[i] = rel == 0 ? 0x80u : 0u;
+                        else if (rel < 4) x[i] = (x[i] & ((1u << (8 * rel)) - 1u)) | (0x80u << (8 * rel));
+                    }
+                }
+                if (H::big_endian) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) x[i] = bswap32(x[i]);
+                }
+                if (b + 1 == nb) {
+                    const uint64_t bits = (uint64_t)total * 8u;
+                    if (H::big_endian) { x[14] = (uint32_t)(bits >> 32); x[15] = (uint32_t)bits; }
+                    else { x[14] = (uint32_t)bits; x[15] = (uint32_t)(bits >> 32); }
+                }
+                st.compress(x);
+            }
+        }
     }
 }
 

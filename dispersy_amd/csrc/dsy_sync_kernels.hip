@@ -291,7 +291,7 @@ __global__ void __launch_bounds__(256) k_pair_test(RespondLaunch L, const uint32
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t wave0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    uint8_t* my_lds = dma_lds + (threadIdx.x >> 6) * DmaGeometry<2, 2>::kWaveBytes;
+    uint8_t* my_lds = dma_lds + (threadIdx.x >> 6) * DmaGeometry<2, 1>::kWaveBytes;
     unsigned long long acc_blocks = 0, acc_bytes = 0, acc_slots = 0;  // this lane's work, reduced once per block
     // chunk-major task order: wave-task v hashes 64-pair chunk (v / n_list) of claim (v % n_list), so the
     // non-empty chunks of every claim come first and spread evenly over the grid
@@ -314,7 +314,7 @@ __global__ void __launch_bounds__(256) k_pair_test(RespondLaunch L, const uint32
         }
         H st;
         if constexpr (DMA) {
-            if (q.prefix_len <= 4) hash_key_dma<H, 2, 2>(kv, st, my_lds);
+            if (q.prefix_len <= 4) hash_key_dma_reg<H, 2>(kv, st, my_lds);
             else hash_key<H>(kv, st);
         } else {
             hash_key<H>(kv, st);
@@ -371,10 +371,11 @@ static hipError_t pair_test_family(const RespondLaunch& L, const uint32_t* list,
     uint64_t blocks = (waves + 3) / 4;
     if (blocks > 256 * 16) blocks = 256 * 16;
     if (blocks == 0) return hipSuccess;
-    // MD5 is load-bound: stage its blocks through LDS with DMA; the SHA families are compute-bound and keep the
-    // direct per-lane loads (higher occupancy)
-    constexpr bool dma = H::kind == DSY_MD5;
-    const size_t lds = dma ? 4 * DmaGeometry<2, 2>::kWaveBytes : 0;
+    // MD5 and SHA-1 stage their 64-byte blocks through LDS with DMA (8 keys x 128 contiguous bytes per wave
+    // instruction, single LDS buffer, next stage in flight while the current one is compressed from registers:
+    // tools/hashbench, profiles/hashbench_r1_dmareg.txt); SHA-2 is compute-bound enough that direct loads match it
+    constexpr bool dma = H::kind == DSY_MD5 || H::kind == DSY_SHA1;
+    const size_t lds = dma ? 4 * DmaGeometry<2, 1>::kWaveBytes : 0;
     hipLaunchKernelGGL((k_pair_test<H, CHUNK, dma>), dim3((uint32_t)blocks), dim3(256), lds, L.stream, L, list, n_list);
     return hipGetLastError();
 }

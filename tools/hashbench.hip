@@ -480,6 +480,95 @@ float run(const uint8_t* blob, const uint64_t* off, const uint32_t* order, uint3
     return ms / reps;
 }
 
+// the product's hash_key_dma (dsy_message.h) in WG-thread workgroups, one 64-key wave-task per wave
+template <class H, int S, int WG>
+__global__ void __launch_bounds__(WG) k_hash_dma_r(const uint8_t* blob, const uint64_t* off, const uint32_t* order,
+                                                   uint32_t n, const uint8_t* pre, uint32_t plen, uint32_t* out) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    const uint32_t i = blockIdx.x * WG + threadIdx.x;
+    const uint32_t key = order ? order[min(i, n - 1)] : min(i, n - 1);
+    const uint64_t a = off[key], e = off[key + 1];
+    KeyView kv{blob + a, i < n ? (uint32_t)(e - a) : 0u, pre, plen};
+    H st;
+    hash_key_dma_reg<H, S>(kv, st, dyn + (threadIdx.x >> 6) * DmaGeometry<S, 1>::kWaveBytes);
+    uint32_t x = 0;
+#pragma unroll
+    for (int j = 0; j < H::digest_bytes / 4; ++j) x ^= st.be_word(j);
+    if (i < n) out[i] = x;
+}
+
+template <class H, int S, int WG>
+float run_dma_r(const uint8_t* blob, const uint64_t* off, const uint32_t* order, uint32_t n, const uint8_t* pre,
+                uint32_t plen, uint32_t* out, int reps) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    dim3 grid((n + WG - 1) / WG);
+    const size_t dl = (size_t)(WG / 64) * DmaGeometry<S, 1>::kWaveBytes;
+    hipLaunchKernelGGL((k_hash_dma_r<H, S, WG>), grid, dim3(WG), dl, 0, blob, off, order, n, pre, plen, out);
+    CK(hipEventRecord(a));
+    for (int r = 0; r < reps; ++r)
+        hipLaunchKernelGGL((k_hash_dma_r<H, S, WG>), grid, dim3(WG), dl, 0, blob, off, order, n, pre, plen, out);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    std::vector<uint32_t> h(n), ord(n), byk(n);
+    CK(hipMemcpy(h.data(), out, n * 4, hipMemcpyDeviceToHost));
+    if (order) {
+        CK(hipMemcpy(ord.data(), order, n * 4, hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < n; ++i) byk[ord[i]] = h[i];
+    } else byk = h;
+    uint64_t cs = 0;
+    for (uint32_t i = 0; i < n; ++i) cs = cs * 1000003u + byk[i];
+    g_checksum = cs;
+    return ms / reps;
+}
+
+template <class H, int S, int NB, int WG, int FLAGS>
+__global__ void __launch_bounds__(WG) k_hash_dma_p(const uint8_t* blob, const uint64_t* off, const uint32_t* order,
+                                                   uint32_t n, const uint8_t* pre, uint32_t plen, uint32_t* out) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    const uint32_t i = blockIdx.x * WG + threadIdx.x;
+    const uint32_t key = order ? order[min(i, n - 1)] : min(i, n - 1);
+    const uint64_t a = off[key], e = off[key + 1];
+    KeyView kv{blob + a, i < n ? (uint32_t)(e - a) : 0u, pre, plen};
+    H st;
+    hash_key_dma<H, S, NB, FLAGS>(kv, st, dyn + (threadIdx.x >> 6) * DmaGeometry<S, NB>::kWaveBytes);
+    uint32_t x = 0;
+#pragma unroll
+    for (int j = 0; j < H::digest_bytes / 4; ++j) x ^= st.be_word(j);
+    if (i < n) out[i] = x;
+}
+
+template <class H, int S, int NB, int WG, int FLAGS>
+float run_dma_p(const uint8_t* blob, const uint64_t* off, const uint32_t* order, uint32_t n, const uint8_t* pre,
+                uint32_t plen, uint32_t* out, int reps) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    dim3 grid((n + WG - 1) / WG);
+    const size_t dl = (size_t)(WG / 64) * DmaGeometry<S, NB>::kWaveBytes;
+    hipLaunchKernelGGL((k_hash_dma_p<H, S, NB, WG, FLAGS>), grid, dim3(WG), dl, 0, blob, off, order, n, pre, plen, out);
+    CK(hipEventRecord(a));
+    for (int r = 0; r < reps; ++r)
+        hipLaunchKernelGGL((k_hash_dma_p<H, S, NB, WG, FLAGS>), grid, dim3(WG), dl, 0, blob, off, order, n, pre, plen, out);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    std::vector<uint32_t> h(n), ord(n), byk(n);
+    CK(hipMemcpy(h.data(), out, n * 4, hipMemcpyDeviceToHost));
+    if (order) {
+        CK(hipMemcpy(ord.data(), order, n * 4, hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < n; ++i) byk[ord[i]] = h[i];
+    } else byk = h;
+    uint64_t cs = 0;
+    for (uint32_t i = 0; i < n; ++i) cs = cs * 1000003u + byk[i];
+    g_checksum = cs;
+    return ms / reps;
+}
+
 int main(int argc, char** argv) {
     const uint32_t n = argc > 1 ? atoi(argv[1]) : 1000000;
     const int reps = argc > 2 ? atoi(argv[2]) : 10;
@@ -523,28 +612,23 @@ int main(int argc, char** argv) {
     for (int round = 0; round < 2; ++round) {
         struct R { const char* name; float ms; uint64_t cs = 0; };
         std::vector<R> rs;
-        { float ms_ = run<Md5, kFast>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"md5 fast sorted", ms_, g_checksum}); }
-        { float ms_ = run<Md5, kDma>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"md5 dma(2,2,wg256) sorted", ms_, g_checksum}); }
-        { float ms_ = run_dma<Md5, 1, 2>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"md5 dma(1,2) sorted", ms_, g_checksum}); }
-        { float ms_ = run_dma<Md5, 1, 3>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"md5 dma(1,3) sorted", ms_, g_checksum}); }
-        { float ms_ = run_dma<Md5, 1, 4>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"md5 dma(1,4) sorted", ms_, g_checksum}); }
-        { float ms_ = run_dma<Md5, 2, 2>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"md5 dma(2,2) sorted", ms_, g_checksum}); }
-        { float ms_ = run_dma<Md5, 2, 3>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"md5 dma(2,3) sorted", ms_, g_checksum}); }
-        { float ms_ = run_dma<Md5, 4, 2>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"md5 dma(4,2) sorted", ms_, g_checksum}); }
-        { float ms_ = run_dma<Md5, 2, 3>(d_blob, d_off, d_scat_sorted, n, d_pre, 1, d_out, reps); rs.push_back({"md5 dma(2,3) scat-sorted", ms_, g_checksum}); }
-        { float ms_ = run<Md5, kPure>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"md5 pure sorted", ms_, g_checksum}); }
-        { float ms_ = run<NullHash, kFast>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"null fast sorted", ms_, g_checksum}); }
-        { float ms_ = run<NullHash, kFast>(d_blob, d_off, nullptr, n, d_pre, 1, d_out, reps); rs.push_back({"null fast natural", ms_, g_checksum}); }
-        { float ms_ = run_dma<NullHash, 1, 3>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"null dma(1,3) sorted", ms_, g_checksum}); }
-        { float ms_ = run_dma<NullHash, 2, 2>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"null dma(2,2) sorted", ms_, g_checksum}); }
-        { float ms_ = run_dma<NullHash, 4, 2>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"null dma(4,2) sorted", ms_, g_checksum}); }
-        { float ms_ = run_dma<NullHash, 2, 2>(d_blob, d_off, nullptr, n, d_pre, 1, d_out, reps); rs.push_back({"null dma(2,2) natural", ms_, g_checksum}); }
-        { float ms_ = run<Sha1, kFast>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"sha1 fast sorted", ms_, g_checksum}); }
-        { float ms_ = run_dma<Sha1, 1, 3>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"sha1 dma(1,3) sorted", ms_, g_checksum}); }
-        { float ms_ = run_dma<Sha1, 2, 3>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"sha1 dma(2,3) sorted", ms_, g_checksum}); }
-        { float ms_ = run<Sha1, kPure>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"sha1 pure sorted", ms_, g_checksum}); }
-        { float ms_ = run<Sha256, kFast>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"sha256 fast sorted", ms_, g_checksum}); }
-        { float ms_ = run<Sha256, kPure>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps); rs.push_back({"sha256 pure sorted", ms_, g_checksum}); }
+#define V(NAME, CALL) { float ms_ = CALL; rs.push_back({NAME, ms_, g_checksum}); }
+        V("md5 dma(2,2) wg256", (run_dma_p<Md5, 2, 2, 256, 0>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+        V("md5 dmareg(1) wg256", (run_dma_r<Md5, 1, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+        V("md5 dmareg(2) wg256", (run_dma_r<Md5, 2, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+        V("md5 dmareg(2) wg128", (run_dma_r<Md5, 2, 128>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+        V("md5 dmareg(4) wg256", (run_dma_r<Md5, 4, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+        V("md5 dmareg(2) wg256 scat", (run_dma_r<Md5, 2, 256>(d_blob, d_off, d_scat_sorted, n, d_pre, 1, d_out, reps)));
+        V("null dma(2,2) wg256", (run_dma_p<NullHash, 2, 2, 256, 0>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+        V("null dmareg(2) wg256", (run_dma_r<NullHash, 2, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+        V("null dmareg(4) wg256", (run_dma_r<NullHash, 4, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+        V("sha1 fast sorted", (run<Sha1, kFast>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+        V("sha1 dmareg(1) wg256", (run_dma_r<Sha1, 1, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+        V("sha1 dmareg(2) wg256", (run_dma_r<Sha1, 2, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+        V("sha1 pure sorted", (run<Sha1, kPure>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+        V("sha256 fast sorted", (run<Sha256, kFast>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+        V("sha256 dmareg(1) wg256", (run_dma_r<Sha256, 1, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+#undef V
         for (auto& r : rs) (void)0;
         for (auto& r : rs)
             printf("round %d  %-26s %8.3f ms  %7.1f GB/s  %6.2f Gblk/s  cs=%016llx\n", round, r.name, r.ms,
