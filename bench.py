@@ -230,7 +230,7 @@ def main():
         store = None
         del blob_full, blob, offsets, gt, meta, d_filters
         torch.cuda.empty_cache()
-        large = large_filter(args, ctx, lib, dev, rank, world)
+        large = large_filter(args, ctx, lib, dev, rank, world, dist)
 
 
     if rank == 0:
@@ -398,10 +398,13 @@ def single_filter_cpu(blob, offsets):
             "results": res}
 
 
-def large_filter(args, ctx, lib, dev, rank, world):
+def large_filter(args, ctx, lib, dev, rank, world, dist=None):
     """BASELINE config 4: BloomFilter(2**b, 0.01, b"\x07") for b in (20, 22, 24) -- SHA-256, 'L' chunks, k=7 --
     filled with --large-keys packets (100-1500 B, seed 99, generated in HBM) and probed with --large-tests other
-    packets.  The filters (128 KB - 2 MB) exceed LDS: the build ORs bits into the L2/HBM-resident array."""
+    packets.  The filters (128 KB - 2 MB) exceed LDS: the build ORs bits into the L2/HBM-resident array.
+    With N ranks every rank adds its own --large-keys packets (weak scaling); the partial filters are all-gathered
+    over RCCL and OR-ed on the GPU (dsy_filter_or_reduce) into the filter of all N x keys, which every
+    rank then probes with its own test packets."""
     import torch
     from dispersy_amd.bloomfilter import BloomFilter
     G = _native.BLOB_GUARD
@@ -431,8 +434,34 @@ def large_filter(args, ctx, lib, dev, rank, world):
                                                             present.data_ptr()))
         filt.zero_()
         k_add, _ = _timed_bloom(ctx, add, 1)
+        union = None
+        if dist is not None and world > 1:
+            # the whole build as a job: every rank adds its shard, then all-gather + OR of the partial filters
+            words = filt.numel()
+            parts = torch.empty(world * words, dtype=torch.int32, device=dev)
+            union = torch.empty_like(filt)
+            filt.zero_()
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            add()
+            ctx.synchronize()
+            dist.all_gather_into_tensor(parts, filt)
+            torch.cuda.synchronize()
+            _native.check(lib.dsy_filter_or_reduce(ctx.handle, parts.data_ptr(), world, words, union.data_ptr()))
+            ctx.synchronize()
+            t_job = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+            dist.all_reduce(t_job, op=dist.ReduceOp.MAX)
+            filt.copy_(union)
+            torch.cuda.synchronize()
         k_test, _ = _timed_bloom(ctx, test, 3)
         ones = int(torch.bitwise_count(filt).sum().item()) if hasattr(torch, "bitwise_count") else None
+        if union is not None:
+            out.setdefault("sharded_build", {})["2^%d" % bits] = {
+                "ranks": world, "keys_all_ranks": world * n_add, "job_s": round(float(t_job.item()), 4),
+                "add_keys_per_s_all_ranks": round(world * n_add / float(t_job.item()), 1),
+                "exchange": "RCCL all_gather_into_tensor of %d x %d B partial filters + dsy_filter_or_reduce"
+                            % (world, 4 * filt.numel())}
         out["filters"]["2^%d" % bits] = {
             "hash": "%s k=%d chunk=%d" % (bf.hash_name, bf.functions, bf.chunk_bytes),
             "add_keys_per_s": round(n_add / k_add, 1), "add_ms": round(k_add * 1e3, 2),

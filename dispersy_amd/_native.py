@@ -19,6 +19,7 @@ HASH_KINDS = {"md5": DSY_MD5, "sha1": DSY_SHA1, "sha256": DSY_SHA256, "sha384": 
 DSY_ASC, DSY_DESC, DSY_RANDOM = 0, 1, 2
 DIRECTIONS = {"ASC": DSY_ASC, "DESC": DSY_DESC, "RANDOM": DSY_RANDOM}
 BLOB_GUARD = 256
+SYNC_HEADER = 24  # DSY_SYNC_HEADER: '>QQHHBH' + the 1-byte prefix (conversion.py:727-728)
 
 # the ctx timer classes of dsy_ctx_kernel_time
 TIME_PAIR_TEST, TIME_BLOOM, TIME_SELECT, TIME_COMPACT = 0, 1, 2, 3
@@ -86,6 +87,9 @@ SIGNATURES = {
     "dsy_sync_respond_dev": (ctypes.c_int, [_P, _P, ctypes.POINTER(Request), _U32, _P, ctypes.POINTER(Meta), _U32,
                                             _U64, ctypes.c_int, ctypes.c_int64, _U64, ctypes.POINTER(_P),
                                             ctypes.POINTER(_P), _PU64]),
+    "dsy_filter_or_reduce": (ctypes.c_int, [_P, _P, _U32, _U64, _P]),
+    "dsy_sync_decode": (ctypes.c_int, [_P, _P, _U32, _U64, ctypes.POINTER(Request), _P, _U64, _PU64, _P]),
+    "dsy_sync_encode": (ctypes.c_int, [ctypes.POINTER(Request), _U32, _P, _P, _U64, _P]),
     "dsy_sim_setup": (ctypes.c_int, [_P]),
     "dsy_sim_seed": (ctypes.c_int, [_P, _P, _P, _U32]),
     "dsy_sim_claim_counts": (ctypes.c_int, [_P, _P, _U32, _P, _U32]),

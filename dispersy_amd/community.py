@@ -358,11 +358,6 @@ class SyncCommunity(object):
     def respond(self, requests, include_inactive=False, byte_limit=None, random_seed=None):
         """Batched responder (community.py:2531-2572): for each ClaimRequest (time_high already resolved), the store
         rows the reference would send, in send order.  One call into the HIP library for the whole batch."""
-        byte_limit = self.dispersy_sync_response_limit if byte_limit is None else byte_limit
-        seed = self._random.getrandbits(64) if random_seed is None else random_seed
-        st = self._store
-        ctx = st.ctx
-        metas = self._served_metas()
         R = len(requests)
         reqs = (_native.Request * max(R, 1))()
         filters, off = [], 0
@@ -380,6 +375,29 @@ class SyncCommunity(object):
             ctypes.memmove(r.prefix, bf.prefix, len(bf.prefix))
             filters.append(raw)
             off += len(raw)
+        return self._respond_requests(reqs, R, b"".join(filters), include_inactive, byte_limit, random_seed)
+
+    def respond_wire(self, blocks, include_inactive=False, byte_limit=None, random_seed=None):
+        """on_introduction_request's sync half for a receive batch of raw sync blocks: decode (conversion.py:732-799,
+        time_high 0 resolved to this community's global time, community.py:2545-2553) and answer every good claim
+        in one responder call.  Returns, per block, a DropPacket (the decoder's verdict) or the store rows to send."""
+        from .conversion import DROP_REASONS, DropPacket, decode_sync_blocks
+        batch = decode_sync_blocks(blocks, responder_global_time=self.global_time)
+        good = np.flatnonzero(batch.status == 0)
+        sub = (_native.Request * max(len(good), 1))(*[batch.requests[int(i)] for i in good])
+        rows = self._respond_requests(sub, len(good), batch.filters, include_inactive, byte_limit, random_seed)
+        out = [DropPacket(DROP_REASONS.get(int(st), "Invalid sync block")) for st in batch.status]
+        for i, r in zip(good, rows):
+            out[int(i)] = r
+        return out
+
+    def _respond_requests(self, reqs, R, blob, include_inactive, byte_limit, random_seed):
+        """One dsy_sync_respond call for R dsy_request records whose filters sit in `blob`."""
+        byte_limit = self.dispersy_sync_response_limit if byte_limit is None else byte_limit
+        seed = self._random.getrandbits(64) if random_seed is None else random_seed
+        st = self._store
+        ctx = st.ctx
+        metas = self._served_metas()
         mt = (_native.Meta * max(len(metas), 1))()
         for j, m in enumerate(metas):
             mt[j].meta_id = m.database_id
@@ -387,7 +405,6 @@ class SyncCommunity(object):
             pr = m.distribution.pruning
             mt[j].has_pruning = 1 if isinstance(pr, GlobalTimePruning) else 0
             mt[j].inactive_threshold = pr.inactive_threshold if isinstance(pr, GlobalTimePruning) else 0
-        blob = b"".join(filters)
         out_off = np.zeros(R + 1, dtype=np.uint64)
         cap = 1 << 16
         while True:

@@ -180,6 +180,50 @@ __global__ void __launch_bounds__(256) k_bloom_indices(const DevParams* __restri
     }
 }
 
+// ------------------------------------------------------------------------------ union of partial filters
+__global__ void __launch_bounds__(256) k_or_reduce(const uint4* __restrict__ parts, uint32_t n_parts, uint64_t vecs,
+                                                   uint64_t stride_vecs, uint4* __restrict__ out) {
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < vecs; i += step) {
+        uint4 acc = parts[i];
+        for (uint32_t g = 1; g < n_parts; ++g) {
+            const uint4 v = parts[g * stride_vecs + i];
+            acc.x |= v.x; acc.y |= v.y; acc.z |= v.z; acc.w |= v.w;
+        }
+        out[i] = acc;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_or_reduce_tail(const uint32_t* __restrict__ parts, uint32_t n_parts,
+                                                        uint64_t first, uint64_t words, uint32_t* __restrict__ out) {
+    const uint64_t w = first + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= words) return;
+    uint32_t acc = 0;
+    for (uint32_t g = 0; g < n_parts; ++g) acc |= parts[g * words + w];
+    out[w] = acc;
+}
+
+hipError_t launch_or_reduce(const uint32_t* parts, uint32_t n_parts, uint64_t words, uint32_t* out, uint32_t max_grid,
+                            hipStream_t stream) {
+    // 16-byte vectors when every part starts 16-byte aligned (words % 4 == 0 and aligned base pointers)
+    const bool vec = words % 4 == 0 && ((uintptr_t)parts % 16) == 0 && ((uintptr_t)out % 16) == 0;
+    uint64_t done = 0;
+    if (vec && words) {
+        const uint64_t vecs = words / 4;
+        const uint64_t want = (vecs + 255) / 256;
+        const uint32_t grid = (uint32_t)(want < max_grid ? want : max_grid);
+        hipLaunchKernelGGL(k_or_reduce, dim3(grid), dim3(256), 0, stream, (const uint4*)parts, n_parts, vecs, vecs,
+                           (uint4*)out);
+        done = words;
+    }
+    if (done < words) {
+        const uint64_t rest = words - done;
+        hipLaunchKernelGGL(k_or_reduce_tail, dim3((uint32_t)((rest + 255) / 256)), dim3(256), 0, stream, parts, n_parts,
+                           done, words, out);
+    }
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------------------ dispatch
 hipError_t launch_len_sort(const LenSort& s, const uint64_t* offsets, const uint64_t* rows, uint64_t n,
                            uint32_t* d_bins, PairTask* d_tasks, uint32_t max_grid, hipStream_t stream) {

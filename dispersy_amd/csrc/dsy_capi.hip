@@ -446,6 +446,13 @@ int dsy_bloom_test_dev(dsy_ctx* c, const dsy_bloom_params* p, const uint8_t* d_b
     return run_bloom(c, BloomOp::Test, p, d_blob, d_offsets, nullptr, n, (uint32_t*)d_filter, d_present, nullptr);
 }
 
+int dsy_filter_or_reduce(dsy_ctx* c, const uint32_t* d_parts, uint32_t n_parts, uint64_t words, uint32_t* d_out) {
+    if (!c || !d_out || (n_parts && !d_parts) || !n_parts) return fail(DSY_EINVAL, "NULL argument or no parts");
+    Guard g(c);
+    HIP_TRY(launch_or_reduce(d_parts, n_parts, words, d_out, c->max_grid, c->stream));
+    return DSY_OK;
+}
+
 // ------------------------------------------------------------------------------------------------ store
 static int store_index(dsy_store* s, const uint64_t* offsets, const uint64_t* gt, const uint32_t* meta,
                        const uint8_t* undone, std::vector<uint64_t>* live_gt, std::vector<uint64_t>* live_row,

@@ -48,6 +48,8 @@ struct BloomLaunch {
 };
 
 hipError_t launch_bloom(const BloomLaunch& L);
+hipError_t launch_or_reduce(const uint32_t* parts, uint32_t n_parts, uint64_t words, uint32_t* out, uint32_t max_grid,
+                            hipStream_t stream);
 
 // Length-bucketed order of a key batch: tasks[0..n) sorted by compression-block count, longest first.
 struct LenSort {

@@ -190,6 +190,42 @@ int dsy_sync_respond_dev(dsy_ctx* ctx, const dsy_store* store, const dsy_request
                          uint64_t random_seed, const uint64_t** d_out_idx, const uint64_t** d_out_offsets,
                          uint64_t* out_total_pairs);
 
+/* Union of G partial filters of one (m, k, prefix) built over disjoint key shards (the large-filter
+ * build shards keys over GPUs; RCCL reduces only sum/prod/min/max, so the partials are all-gathered over xGMI and
+ * OR-ed here): d_out[w] = OR_g d_parts[g * words + w].  Device pointers; enqueued on the ctx stream. */
+int dsy_filter_or_reduce(dsy_ctx* ctx, const uint32_t* d_parts, uint32_t n_parts, uint64_t words, uint32_t* d_out);
+
+/* ------------------------------------------------------------------------------- sync block wire codec */
+/* The sync part of an introduction-request payload (conversion.py:712-730 encode, :732-799 decode): struct
+ * '>QQHHBH' (time_low, time_high, modulo, offset, functions, size in bits), the 1-byte prefix, then size/8 filter
+ * bytes up to the end of the payload.  DSY_SYNC_HEADER = 23 + 1.  Decoding a batch gives per-item status codes
+ * (the reference's DropPacket reasons, checked in its order) and, for the good items, dsy_request records whose
+ * filters are packed 4-byte aligned into out_filters -- exactly what dsy_sync_respond takes. */
+#define DSY_SYNC_HEADER 24
+#define DSY_DROP_OK 0
+#define DSY_DROP_SIZE 1        /* "Insufficient packet size"                 conversion.py:763-764 */
+#define DSY_DROP_TIME_LOW 2    /* "Invalid time_low value"                   :772-773 */
+#define DSY_DROP_TIME_HIGH 3   /* "Invalid time_high value"                  :774-775 */
+#define DSY_DROP_MODULO 4      /* "Invalid modulo value"                     :776-777 */
+#define DSY_DROP_OFFSET 5      /* "Invalid offset value"                     :778-779 */
+#define DSY_DROP_FUNCTIONS 6   /* "Invalid functions value"                  :780-781 */
+#define DSY_DROP_SIZE_VALUE 7  /* "Invalid size value"                       :782-783 */
+#define DSY_DROP_SIZE_MULT8 8  /* "Invalid size value, must be a multiple of eight"  :784-785 */
+#define DSY_DROP_LENGTH 9      /* "Invalid number of bytes available"        :787-789 */
+#define DSY_DROP_FAMILY 10     /* BloomFilter(bytes, k) would assert: (m, k) needs > 512 digest bits or k > m
+                                  (bloomfilter.py:128-156) */
+/* blob + offsets[n+1]: each item is one sync block (from its first byte to the end of the payload).  When
+ * responder_global_time != 0, time_high == 0 is resolved to it and both bounds are clamped to 2^63-1 as
+ * on_introduction_request does (community.py:2545-2553).  If out_filters is too small, DSY_ECAPACITY is returned
+ * with the space needed so far in *out_filters_len (at most 8 KiB per item). */
+int dsy_sync_decode(const uint8_t* blob, const uint64_t* offsets, uint32_t n, uint64_t responder_global_time,
+                    dsy_request* out_reqs, uint8_t* out_filters, uint64_t filters_cap, uint64_t* out_filters_len,
+                    int32_t* out_status);
+/* Encode n claims (prefix_len 1, 0 < k < 256, m % 8 == 0, m < 2^16 -- the wire's field widths and the asserts of
+ * conversion.py:723-726) into out; out_offsets[n+1] delimit the blocks. */
+int dsy_sync_encode(const dsy_request* reqs, uint32_t n, const uint8_t* filters, uint8_t* out, uint64_t out_cap,
+                    uint64_t* out_offsets);
+
 /* ------------------------------------------------------------------ epidemic-sync simulator (config 3) */
 /* Simulated peers run the reference protocol once per round (see dispersy_amd/csrc/dsy_sim_kernels.hip):
  * requester claim = _dispersy_claim_sync_bloom_filter_largest's below-capacity branch (community.py:808-821),

@@ -156,3 +156,32 @@ def test_length_sorted_batches_against_oracle(m, f, prefix):
     blob, off = pack_keys(keys)
     got = _native.default_context().bloom_test(bf.params, blob, off, bf.bytes)
     assert got.astype(bool).tolist() == [k in ref for k in keys]
+
+
+def test_filter_or_reduce_is_the_union_of_shards():
+    """Sharded large-filter build: per-shard filters OR-ed by dsy_filter_or_reduce == one filter over
+    all keys (and == the oracle), for word counts with and without a 16-byte-vector tail."""
+    import torch
+    ctx = _native.default_context()
+    dev = torch.device("cuda", 0)
+    for m, f in ((1 << 20, 0.01), (10160, 0.01), (4104, 0.001)):
+        blob, off = random_packets(m & 0xFFFF, 6000, 60, 700)
+        keys = [blob[int(off[i]):int(off[i + 1])] for i in range(len(off) - 1)]
+        shards = [keys[i::3] for i in range(3)]
+        parts = []
+        for sh in shards:
+            bf = BloomFilter(m, f, b"\x07")
+            bf.add_keys(sh)
+            raw = bf.bytes + b"\x00" * ((-len(bf.bytes)) % 4)
+            parts.append(np.frombuffer(raw, dtype=np.int32))
+        words = len(parts[0])
+        d_parts = torch.from_numpy(np.concatenate(parts)).to(dev)
+        d_out = torch.full((words,), -1, dtype=torch.int32, device=dev)
+        _native.check(ctx.lib.dsy_filter_or_reduce(ctx.handle, d_parts.data_ptr(), 3, words, d_out.data_ptr()))
+        ctx.synchronize()
+        whole = BloomFilter(m, f, b"\x07")
+        whole.add_keys(keys)
+        ref = OracleBloom.from_m_f(m, f, b"\x07")
+        ref.add_keys(keys)
+        got = d_out.cpu().numpy().tobytes()[:m // 8]
+        assert got == whole.bytes == ref.to_bytes()

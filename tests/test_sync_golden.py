@@ -172,3 +172,31 @@ def test_claim_state_machine_matches_reference():
         assert [st.sync_bloom_new, st.sync_bloom_reuse, st.sync_bloom_send, st.sync_bloom_skip] == ev["stats"]
         assert com._sync_cache_skip_count == ev["skip_count"]
     assert not draws.log
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("sc", [s for s in SYNC["respond"] if not s["random_directions"]],
+                         ids=[s["name"] for s in SYNC["respond"] if not s["random_directions"]])
+def test_respond_wire_matches_reference(sc):
+    """Claims that fit the wire (1-byte prefix, m < 2^16, k < 256) encoded as introduction-request sync blocks
+    (conversion.py:712-730), decoded and answered in one call (respond_wire): the reference's response; a corrupt
+    block in the same batch is dropped with the decoder's reason and does not disturb the others."""
+    from dispersy_amd.conversion import DropPacket, encode_sync_blocks
+    store = store_of(sc["rows"])
+    n = 0
+    for req, res in zip(sc["requests"], sc["results"]):
+        bf = claim_of(req)
+        if len(bf.prefix) != 1 or bf.size >= 1 << 16 or req["time_low"] >= 1 << 63 or req["time_high"] >= 1 << 63:
+            continue
+        gt = req["responder_global_time"]
+        com = SyncCommunity(store, metas_of(sc["metas"]), global_time=gt)
+        if com.global_time != gt:
+            continue
+        [blk] = encode_sync_blocks([(req["time_low"], req["time_high"], req["modulo"], req["offset"], bf)])
+        bad = blk[:-1]
+        out = com.respond_wire([bad, blk, bad], include_inactive=req["include_inactive"], byte_limit=req["byte_limit"])
+        assert isinstance(out[0], DropPacket) and str(out[0]) == "Invalid number of bytes available"
+        assert isinstance(out[2], DropPacket)
+        assert store.rowid[out[1]].tolist() == res["response"], req
+        n += 1
+    assert n > 0
