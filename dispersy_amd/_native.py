@@ -72,6 +72,7 @@ SIGNATURES = {
     "dsy_ctx_kernel_time": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), _PU64, _PU64, _PU64]),
     "dsy_ctx_reset_timing": (ctypes.c_int, [_P]),
     "dsy_ctx_work": (ctypes.c_int, [_P, ctypes.c_int, _PU64]),
+    "dsy_ctx_set_window": (ctypes.c_int, [_P, _U64]),
     "dsy_bloom_add": (ctypes.c_int, [_P, ctypes.POINTER(BloomParams), _P, _U64, _P, _U64, _P]),
     "dsy_bloom_test": (ctypes.c_int, [_P, ctypes.POINTER(BloomParams), _P, _U64, _P, _U64, _P, _P]),
     "dsy_bloom_indices": (ctypes.c_int, [_P, ctypes.POINTER(BloomParams), _P, _U64, _P, _U64, _P]),
@@ -187,6 +188,10 @@ class Context(object):
         check(self.lib.dsy_ctx_kernel_time(self.handle, which, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(blocks),
                                            ctypes.byref(nbytes)))
         return dict(ms=ms.value, launches=n.value, blocks=blocks.value, bytes=nbytes.value)
+
+    def set_window(self, max_pairs):
+        """Cap the responder window (0: default); results are independent of it."""
+        check(self.lib.dsy_ctx_set_window(self.handle, max_pairs))
 
     def work(self, which):
         """Algorithmic work counters of a timer class (dsy_ctx_work)."""

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -67,6 +68,9 @@ struct dsy_ctx {
     uint64_t useful[kTimeClasses] = {0, 0, 0, 0};  // pairs the reference would have hashed (responder)
     uint64_t slots[kTimeClasses] = {0, 0, 0, 0};   // lane-block slots of the hashing waves (load balance)
     void* pinned = nullptr;  // small pinned staging for flags/counters
+    uint64_t window_cap = 0; // dsy_ctx_set_window: upper bound on the responder's window (0: the default 2^18)
+    void* stage = nullptr;   // grow-only pinned staging of the responder's uploads and status read-backs
+    size_t stage_bytes = 0;
 };
 
 struct dsy_store {
@@ -100,6 +104,23 @@ int ws_get(dsy_ctx* c, const char* name, size_t bytes, void** out) {
     return DSY_OK;
 }
 
+// grow-only pinned host staging (one H2D upload and one D2H status read per responder window)
+int stage_get(dsy_ctx* c, size_t bytes, uint8_t** out) {
+    if (c->stage_bytes < bytes) {
+        if (c->stage) hipHostFree(c->stage);
+        c->stage = nullptr;
+        c->stage_bytes = 0;
+        const size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
+        if (hipHostMalloc(&c->stage, want, hipHostMallocDefault) != hipSuccess) {
+            c->stage = nullptr;
+            return fail(DSY_ENOMEM, "hipHostMalloc(%zu) for the staging buffer failed", want);
+        }
+        c->stage_bytes = want;
+    }
+    *out = (uint8_t*)c->stage;
+    return DSY_OK;
+}
+
 hipEvent_t take_event(dsy_ctx* c) {
     if (!c->event_pool.empty()) {
         hipEvent_t e = c->event_pool.back();
@@ -126,18 +147,30 @@ void timer_end(dsy_ctx* c, PendingTimer* t) {
     c->pending.push_back(*t);
 }
 
-// fold completed timers (call after a stream synchronisation)
+// fold completed timers; timers whose events have not completed yet stay pending
 void timers_collect(dsy_ctx* c) {
+    size_t keep = 0;
     for (auto& t : c->pending) {
         float ms = 0;
-        if (hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) {
+        const hipError_t e = hipEventElapsedTime(&ms, t.a, t.b);
+        if (e == hipErrorNotReady) {
+            c->pending[keep++] = t;
+            continue;
+        }
+        if (e == hipSuccess) {
             c->time_ms[t.cls] += ms;
             c->launches[t.cls] += 1;
         }
         c->event_pool.push_back(t.a);
         c->event_pool.push_back(t.b);
     }
-    c->pending.clear();
+    c->pending.resize(keep);
+}
+
+// entry points fold their timers lazily (hipEventElapsedTime costs host time per event pair); the
+// synchronising accessors (dsy_ctx_kernel_time, _synchronize, _reset_timing) fold everything
+void timers_collect_lazy(dsy_ctx* c) {
+    if (c->pending.size() >= 512) timers_collect(c);
 }
 
 int check_family(uint64_t m, uint32_t k, int32_t* kind, uint32_t* chunk) {
@@ -310,6 +343,7 @@ int dsy_ctx_destroy(dsy_ctx* c) {
         for (auto& kv : c->ws) if (kv.second.ptr) hipFree(kv.second.ptr);
         for (auto e : c->event_pool) hipEventDestroy(e);
         if (c->pinned) hipHostFree(c->pinned);
+        if (c->stage) hipHostFree(c->stage);
         hipStreamDestroy(c->stream);
     }
     delete c;
@@ -356,6 +390,13 @@ int dsy_ctx_reset_timing(dsy_ctx* c) {
     return DSY_OK;
 }
 
+int dsy_ctx_set_window(dsy_ctx* c, uint64_t max_pairs) {
+    if (!c || (max_pairs && (max_pairs < 64 || max_pairs % 64))) return fail(DSY_EINVAL, "window must be 0 or a multiple of 64");
+    Guard g(c);
+    c->window_cap = max_pairs;
+    return DSY_OK;
+}
+
 int dsy_ctx_work(dsy_ctx* c, int which, uint64_t* out4) {
     if (!c || !out4 || which < 0 || which >= kTimeClasses) return fail(DSY_EINVAL, "bad ctx, output or class");
     Guard g(c);
@@ -384,7 +425,7 @@ int dsy_bloom_add(dsy_ctx* c, const dsy_bloom_params* p, const uint8_t* blob, ui
     if ((rc = run_bloom(c, BloomOp::Add, p, db, dof, nullptr, n, (uint32_t*)df, nullptr, nullptr))) return rc;
     HIP_TRY(hipMemcpyAsync(filter_inout, df, nbytes, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    timers_collect(c);
+    timers_collect_lazy(c);
     return DSY_OK;
 }
 
@@ -406,7 +447,7 @@ int dsy_bloom_test(dsy_ctx* c, const dsy_bloom_params* p, const uint8_t* blob, u
     if ((rc = run_bloom(c, BloomOp::Test, p, db, dof, nullptr, n, (uint32_t*)df, (uint8_t*)dp, nullptr))) return rc;
     if (n) HIP_TRY(hipMemcpyAsync(out_present, dp, n, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    timers_collect(c);
+    timers_collect_lazy(c);
     return DSY_OK;
 }
 
@@ -424,7 +465,7 @@ int dsy_bloom_indices(dsy_ctx* c, const dsy_bloom_params* p, const uint8_t* blob
     if ((rc = run_bloom(c, BloomOp::Indices, p, db, dof, nullptr, n, nullptr, nullptr, (uint64_t*)di))) return rc;
     if (n) HIP_TRY(hipMemcpyAsync(out_idx, di, n * p->k * 8, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    timers_collect(c);
+    timers_collect_lazy(c);
     return DSY_OK;
 }
 
@@ -617,7 +658,7 @@ int dsy_bloom_add_rows(dsy_ctx* c, const dsy_bloom_params* p, const dsy_store* s
         return rc;
     HIP_TRY(hipMemcpyAsync(filter_inout, df, nbytes, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    timers_collect(c);
+    timers_collect_lazy(c);
     return DSY_OK;
 }
 
@@ -634,8 +675,10 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
                         uint64_t filters_len, const dsy_meta* metas, uint32_t J, uint64_t responder_gt,
                         int include_inactive, int64_t byte_limit, uint64_t seed, uint64_t** d_packed,
                         uint64_t** d_packed_off, uint64_t* total_pairs) {
-    // ---- validate claims (payload.py:89-101, conversion.py:772-789) and their filters
-    std::map<std::pair<int, uint32_t>, std::vector<uint32_t>> families;
+    // ---- validate claims (payload.py:89-101, conversion.py:772-789) and their filters; group them by hash family
+    // (kind x chunk width: one pair-test launch per family)
+    constexpr int kFamilies = 5 * 3;
+    std::vector<uint32_t> fam_members[kFamilies];
     for (uint32_t r = 0; r < R; ++r) {
         const dsy_request& q = reqs[r];
         if (q.modulo == 0 || q.offset >= q.modulo)
@@ -649,48 +692,90 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
         if (q.filter_offset % 4) return fail(DSY_EINVAL, "claim %u: filter_offset must be a multiple of 4", r);
         if (filters_len && q.filter_offset + filter_words(q.m_bits) * 4 > filters_len)
             return fail(DSY_EINVAL, "claim %u: filter beyond the filters buffer", r);
-        families[{kind, chunk}].push_back(r);
+        fam_members[kind * 3 + (chunk == 2 ? 0 : chunk == 4 ? 1 : 2)].push_back(r);
     }
-    std::vector<SegMeta> sm(J);
+    const uint64_t pool = kWindow * std::max<uint64_t>(R, kMinSlots);
+    // ---- device layout: one upload region [claims | metas | window slots 0..R-1 | first active list] and one
+    // status region [counters kCntSpread x 64 B | flags 64 B | act_done R B | upper R x u64] zeroed once, read
+    // back (up to act_done) per window
+    size_t prefix_b = 0;
+    for (uint32_t r = 0; r < R; ++r) prefix_b += reqs[r].prefix_len;
+    const size_t reqs_b = (size_t)R * sizeof(DevRequest), metas_b = (size_t)J * sizeof(SegMeta);
+    const size_t in_b = reqs_b + metas_b + (size_t)R * 8 + (prefix_b + 15) / 16 * 16 + 64;
+    const size_t act_done_b = ((size_t)R + 15) / 16 * 16;
+    const size_t cnt_b = kCntSpread * kCntN * 8, head_b = cnt_b + 64;
+    const size_t io_b = head_b + act_done_b + (size_t)R * 8;
+    int rc;
+    void *d_in, *d_io, *d_plans, *d_state, *d_pairs, *d_off, *d_len, *d_miss, *d_task;
+    if ((rc = ws_get(c, "resp_in", in_b, &d_in))) return rc;
+    if ((rc = ws_get(c, "resp_io", io_b, &d_io))) return rc;
+    if ((rc = ws_get(c, "plans", std::max<size_t>((size_t)R * J, 1) * sizeof(Plan), &d_plans))) return rc;
+    if ((rc = ws_get(c, "state", std::max<size_t>(R, 1) * sizeof(ReqState), &d_state))) return rc;
+    if ((rc = ws_get(c, "pairs", pool * 8, &d_pairs))) return rc;
+    if ((rc = ws_get(c, "pair_off", pool * 8, &d_off))) return rc;
+    if ((rc = ws_get(c, "pair_len", pool * 4, &d_len))) return rc;
+    if ((rc = ws_get(c, "miss", pool, &d_miss))) return rc;
+    if ((rc = ws_get(c, "task", pool * sizeof(PairTask), &d_task))) return rc;
+    uint8_t* h_in;
+    if ((rc = stage_get(c, in_b + io_b, &h_in))) return rc;
+    uint8_t* h_io = h_in + in_b;  // the status region's host mirror
+    std::memset(h_io, 0, head_b);  // counters stay zero if no window runs (R == 0)
+    {
+        DevRequest* dq = (DevRequest*)h_in;
+        uint8_t* h_pre = h_in + reqs_b + metas_b + (size_t)R * 8;
+        const uint8_t* d_pre = (const uint8_t*)d_in + reqs_b + metas_b + (size_t)R * 8;
+        size_t at = 0;
+        for (uint32_t r = 0; r < R; ++r) {
+            const dsy_request& q = reqs[r];
+            DevRequest d;
+            d.time_low = q.time_low;
+            d.time_high = q.time_high;
+            d.filter_offset = q.filter_offset;
+            d.m_bits = q.m_bits;
+            d.modulo = q.modulo;
+            d.offset = q.offset;
+            d.k = q.k;
+            d.hash_kind = (uint32_t)q.hash_kind;
+            d.chunk_bytes = q.chunk_bytes;
+            d.prefix_len = q.prefix_len;
+            d.prefix = d_pre + at;
+            std::memcpy(h_pre + at, q.prefix, q.prefix_len);
+            at += q.prefix_len;
+            dq[r] = d;
+        }
+    }
+    SegMeta* sm = (SegMeta*)(h_in + reqs_b);
     for (uint32_t j = 0; j < J; ++j) {
         if (metas[j].direction < DSY_ASC || metas[j].direction > DSY_RANDOM)
             return fail(DSY_EINVAL, "meta %u: unknown synchronization direction %d", j, metas[j].direction);
         auto it = s->segs.find(metas[j].meta_id);
-        sm[j].seg_a = it == s->segs.end() ? 0 : it->second.first;
-        sm[j].seg_b = it == s->segs.end() ? 0 : it->second.second;
-        sm[j].dir = (uint32_t)metas[j].direction;
-        sm[j].has_pruning = metas[j].has_pruning;
-        sm[j].inactive = metas[j].inactive_threshold;
+        SegMeta m{};
+        m.seg_a = it == s->segs.end() ? 0 : it->second.first;
+        m.seg_b = it == s->segs.end() ? 0 : it->second.second;
+        m.dir = (uint32_t)metas[j].direction;
+        m.has_pruning = metas[j].has_pruning;
+        m.inactive = metas[j].inactive_threshold;
+        sm[j] = m;
     }
-    const uint64_t pool = kWindow * std::max<uint64_t>(R, kMinSlots);
-    int rc;
-    void *d_reqs, *d_metas, *d_plans, *d_state, *d_upper, *d_pairs, *d_miss, *d_flags, *d_total, *d_lists;
-    void *d_act, *d_act_done;
-    if ((rc = ws_get(c, "reqs", std::max<size_t>(R, 1) * sizeof(dsy_request), &d_reqs))) return rc;
-    if ((rc = ws_get(c, "metas", std::max<size_t>(J, 1) * sizeof(SegMeta), &d_metas))) return rc;
-    if ((rc = ws_get(c, "plans", std::max<size_t>((size_t)R * J, 1) * sizeof(Plan), &d_plans))) return rc;
-    if ((rc = ws_get(c, "state", std::max<size_t>(R, 1) * sizeof(ReqState), &d_state))) return rc;
-    if ((rc = ws_get(c, "upper", std::max<size_t>(R, 1) * 8, &d_upper))) return rc;
-    if ((rc = ws_get(c, "pairs", pool * 8, &d_pairs))) return rc;
-    if ((rc = ws_get(c, "miss", pool, &d_miss))) return rc;
-    void* d_task;
-    if ((rc = ws_get(c, "task", pool * sizeof(PairTask), &d_task))) return rc;
-    if ((rc = ws_get(c, "flags", 64, &d_flags))) return rc;
-    if ((rc = ws_get(c, "total", 64, &d_total))) return rc;
-    if ((rc = ws_get(c, "lists", std::max<size_t>(R, 1) * 4, &d_lists))) return rc;
-    if ((rc = ws_get(c, "act", std::max<size_t>(R, 1) * 4, &d_act))) return rc;
-    if ((rc = ws_get(c, "act_done", std::max<size_t>(R, 1), &d_act_done))) return rc;
-
-    if (R) HIP_TRY(hipMemcpyAsync(d_reqs, reqs, (size_t)R * sizeof(dsy_request), hipMemcpyHostToDevice, c->stream));
-    if (J) HIP_TRY(hipMemcpyAsync(d_metas, sm.data(), (size_t)J * sizeof(SegMeta), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemsetAsync(d_upper, 0, std::max<size_t>(R, 1) * 8, c->stream));
-    HIP_TRY(hipMemsetAsync(d_total, 0, 64, c->stream));
-    // window slots 0..R-1 (a family's active claims occupy a contiguous run of slots in every window)
-    std::vector<uint32_t> slots(R);
-    for (uint32_t i = 0; i < R; ++i) slots[i] = i;
-    if (R) HIP_TRY(hipMemcpyAsync(d_lists, slots.data(), (size_t)R * 4, hipMemcpyHostToDevice, c->stream));
-    std::vector<std::pair<std::pair<int, uint32_t>, std::vector<uint32_t>>> fam_active;  // per family: active claims
-    for (auto& kv : families) fam_active.push_back({kv.first, kv.second});
+    uint32_t* h_slots = (uint32_t*)(h_in + reqs_b + metas_b);
+    uint32_t* h_act0 = h_slots + R;
+    // the active list, family by family (a family's active claims occupy a contiguous run of slots)
+    std::vector<std::vector<uint32_t>> fam_active;
+    std::vector<int> fam_id;
+    for (int f = 0; f < kFamilies; ++f)
+        if (!fam_members[f].empty()) {
+            fam_active.push_back(fam_members[f]);
+            fam_id.push_back(f);
+        }
+    {
+        uint32_t a = 0;
+        for (uint32_t i = 0; i < R; ++i) h_slots[i] = i;
+        for (auto& fa : fam_active)
+            for (uint32_t r : fa) h_act0[a++] = r;
+    }
+    HIP_TRY(hipMemcpyAsync(d_in, h_in, in_b, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(d_io, 0, io_b, c->stream));
+    uint8_t* io = (uint8_t*)d_io;
 
     RespondLaunch L{};
     L.st.blob = s->d_blob;
@@ -698,8 +783,10 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     L.st.live_gt = s->d_live_gt;
     L.st.live_row = s->d_live_row;
     L.st.n_live = s->n_live;
-    L.reqs = (const dsy_request*)d_reqs;
-    L.metas = (const SegMeta*)d_metas;
+    L.reqs = (const DevRequest*)d_in;
+    L.metas = (const SegMeta*)((uint8_t*)d_in + reqs_b);
+    const uint32_t* d_slots = (const uint32_t*)((uint8_t*)d_in + reqs_b + metas_b);
+    uint32_t* d_act = (uint32_t*)(d_slots + R);
     L.R = R;
     L.J = J;
     L.filters = d_filters;
@@ -708,16 +795,18 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     L.byte_limit = byte_limit;
     L.seed = seed;
     L.window = kWindow;
-    L.act = (const uint32_t*)d_act;
-    L.act_done = (uint8_t*)d_act_done;
+    L.act = d_act;
+    L.act_done = io + head_b;
     L.plans = (Plan*)d_plans;
     L.state = (ReqState*)d_state;
-    L.upper = (uint64_t*)d_upper;
+    L.upper = (uint64_t*)(io + head_b + act_done_b);
     L.pair_row = (uint64_t*)d_pairs;
+    L.pair_off = (uint64_t*)d_off;
+    L.pair_len = (uint32_t*)d_len;
     L.miss = (uint8_t*)d_miss;
     L.task = (PairTask*)d_task;
-    L.flags = (uint32_t*)d_flags;
-    L.counters = (uint64_t*)d_total;
+    L.flags = (uint32_t*)(io + cnt_b);
+    L.counters = (uint64_t*)io;
     L.stream = c->stream;
 
     PendingTimer t;
@@ -737,7 +826,7 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
         HIP_TRY(launch_caps(L, per_claim));
     } else {
         std::vector<uint64_t> upper(R);
-        if (R) HIP_TRY(hipMemcpyAsync(upper.data(), d_upper, (size_t)R * 8, hipMemcpyDeviceToHost, c->stream));
+        if (R) HIP_TRY(hipMemcpyAsync(upper.data(), L.upper, (size_t)R * 8, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
         std::vector<ReqState> st(R);
         for (uint32_t r = 0; r < R; ++r) {
@@ -749,63 +838,96 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
         }
         if ((rc = ws_get(c, "out", std::max<uint64_t>(cap_total, 1) * 8, &d_out))) return rc;
         L.out = (uint64_t*)d_out;
-        if (R) HIP_TRY(hipMemcpyAsync(d_state, st.data(), (size_t)R * sizeof(ReqState), hipMemcpyHostToDevice, c->stream));
+        if (R) HIP_TRY(hipMemcpy(d_state, st.data(), (size_t)R * sizeof(ReqState), hipMemcpyHostToDevice));
     }
 
     // ---- windows: fill -> hash/test (one launch per hash family) -> compact; one host sync per window.  Only
     // the active claims take part; as they finish, the rest share the pool in bigger windows.
-    uint32_t* h_flags = (uint32_t*)c->pinned;
-    uint64_t* h_tot = (uint64_t*)c->pinned + 8;
     std::vector<uint32_t> act;
-    std::vector<uint8_t> act_done;
+    bool first = true;
     for (;;) {
-        act.clear();
         std::vector<std::pair<size_t, size_t>> runs;  // per family: (first slot, slots)
+        size_t n_act = 0;
         for (auto& fa : fam_active) {
-            runs.push_back({act.size(), fa.second.size()});
-            act.insert(act.end(), fa.second.begin(), fa.second.end());
+            runs.push_back({n_act, fa.size()});
+            n_act += fa.size();
         }
-        const uint32_t n_act = (uint32_t)act.size();
         if (!n_act) break;
         uint64_t W = pool / n_act / 64 * 64;
         W = std::min<uint64_t>(std::max<uint64_t>(W, kWindow), kMaxWindow);
+        if (c->window_cap) W = std::min<uint64_t>(W, c->window_cap);
         L.window = W;
-        L.n_act = n_act;
-        HIP_TRY(hipMemcpyAsync(d_act, act.data(), (size_t)n_act * 4, hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(hipMemsetAsync(d_flags, 0, 64, c->stream));
+        L.n_act = (uint32_t)n_act;
+        if (!first) {  // the first window's list went up with the claims
+            uint32_t* h_act = (uint32_t*)h_in;  // the staged claims are on the device already: reuse the space
+            size_t a = 0;
+            for (auto& fa : fam_active)
+                for (uint32_t r : fa) h_act[a++] = r;
+            HIP_TRY(hipMemcpyAsync(d_act, h_act, n_act * 4, hipMemcpyHostToDevice, c->stream));
+        }
+        first = false;
+        static const bool fill_profile = getenv("DSY_FILL_PROFILE") != nullptr;
+        void* d_fc = nullptr;
+        if (fill_profile) {
+            if ((rc = ws_get(c, "fill_clock", n_act * 32 + 32, &d_fc))) return rc;
+            HIP_TRY(hipMemsetAsync(d_fc, 0, n_act * 32, c->stream));
+            L.fill_clock = (uint64_t*)d_fc;
+        }
         timer_begin(c, &t, kTimeSelect);
         HIP_TRY(launch_fill(L));
         timer_end(c, &t);
+        if (fill_profile) {  // per-window stderr line: k_fill phase durations over the workgroups (s_memtime ticks)
+            std::vector<uint64_t> fc(n_act * 4);
+            HIP_TRY(hipMemcpyAsync(fc.data(), d_fc, n_act * 32, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            uint64_t t0 = ~0ull, t2 = 0, sel = 0, srt = 0, mx_sel = 0, mx_srt = 0, n = 0;
+            for (size_t a = 0; a < n_act; ++a) {
+                if (!fc[a * 4]) continue;
+                t0 = std::min(t0, fc[a * 4]);
+                t2 = std::max(t2, fc[a * 4 + 2]);
+                sel += fc[a * 4 + 1] - fc[a * 4];
+                srt += fc[a * 4 + 2] - fc[a * 4 + 1];
+                mx_sel = std::max(mx_sel, fc[a * 4 + 1] - fc[a * 4]);
+                mx_srt = std::max(mx_srt, fc[a * 4 + 2] - fc[a * 4 + 1]);
+                ++n;
+            }
+            if (n) fprintf(stderr, "fill_profile n=%llu span=%llu select avg=%llu max=%llu sort avg=%llu max=%llu\n",
+                           (unsigned long long)n, (unsigned long long)(t2 - t0), (unsigned long long)(sel / n),
+                           (unsigned long long)mx_sel, (unsigned long long)(srt / n), (unsigned long long)mx_srt);
+            L.fill_clock = nullptr;
+        }
         for (size_t f = 0; f < fam_active.size(); ++f) {
             if (!runs[f].second) continue;
+            const int fid = fam_id[f];
             timer_begin(c, &t, kTimePairTest);
-            HIP_TRY(launch_pair_test_list(L, fam_active[f].first.first, fam_active[f].first.second,
-                                          (const uint32_t*)d_lists + runs[f].first, (uint32_t)runs[f].second));
+            HIP_TRY(launch_pair_test_list(L, fid / 3, fid % 3 == 0 ? 2 : fid % 3 == 1 ? 4 : 8, d_slots + runs[f].first,
+                                          (uint32_t)runs[f].second));
             timer_end(c, &t);
         }
         timer_begin(c, &t, kTimeCompact);
         HIP_TRY(launch_compact(L));
         timer_end(c, &t);
-        act_done.resize(n_act);
-        HIP_TRY(hipMemcpyAsync(act_done.data(), d_act_done, n_act, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipMemcpyAsync(h_flags, d_flags, 8, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipMemcpyAsync(h_tot, d_total, kCntN * 8, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(h_io, d_io, head_b + n_act, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
         // capacity overflow can only come from a wrong min_len bound; report it loudly
-        if (h_flags[1]) return fail(DSY_ECAPACITY, "internal: a claim overflowed its output capacity");
+        if (((uint32_t*)(h_io + cnt_b))[1]) return fail(DSY_ECAPACITY, "internal: a claim overflowed its output capacity");
+        const uint8_t* done = h_io + head_b;
         size_t a = 0;
         for (auto& fa : fam_active) {
-            std::vector<uint32_t> keep;
-            for (uint32_t r : fa.second)
-                if (!act_done[a++]) keep.push_back(r);
-            fa.second.swap(keep);
+            size_t keep = 0;
+            for (uint32_t r : fa)
+                if (!done[a++]) fa[keep++] = r;
+            fa.resize(keep);
         }
     }
+    uint64_t h_tot[kCntN] = {0};
+    for (uint32_t i = 0; i < kCntSpread; ++i)
+        for (uint32_t k = 0; k < kCntN; ++k) h_tot[k] += ((const uint64_t*)h_io)[i * kCntN + k];
     void *d_packed_v, *d_packed_off_v;
     if ((rc = ws_get(c, "packed", std::max<uint64_t>(cap_total, 1) * 8, &d_packed_v))) return rc;
     if ((rc = ws_get(c, "packed_off", ((size_t)R + 1) * 8, &d_packed_off_v))) return rc;
     HIP_TRY(launch_pack(L, (uint64_t*)d_packed_v, (uint64_t*)d_packed_off_v, nullptr));
-    timers_collect(c);
+    timers_collect_lazy(c);
     c->blocks[kTimePairTest] += h_tot[kCntBlocks];
     c->bytes[kTimePairTest] += h_tot[kCntBytes];
     c->useful[kTimePairTest] += h_tot[kCntUseful];
@@ -957,7 +1079,7 @@ int dsy_sim_build_claims(dsy_ctx* c, const dsy_sim_config* cfg, uint32_t round, 
     HIP_TRY(launch_sim(kSimBuild, L));
     timer_end(c, &t);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    timers_collect(c);
+    timers_collect_lazy(c);
     return DSY_OK;
 }
 
@@ -1004,7 +1126,7 @@ int dsy_sim_respond(dsy_ctx* c, const dsy_sim_config* cfg, const uint8_t* d_ublo
     uint64_t* h = (uint64_t*)c->pinned + 128;
     HIP_TRY(hipMemcpyAsync(h, dt, 8 * kSimTestedSlots, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    timers_collect(c);
+    timers_collect_lazy(c);
     uint64_t tested = 0;
     for (uint32_t i = 0; i < kSimTestedSlots; ++i) tested += h[i];
     if (out_tested) *out_tested = tested;

@@ -77,11 +77,18 @@ struct Plan {
     uint32_t dir;      // DSY_ASC / DSY_DESC / DSY_RANDOM
     uint64_t perm_key; // RANDOM: permutation key
     uint32_t perm_bits;// RANDOM: Feistel half-width
-    uint32_t _pad;
+    uint32_t dense;    // the span's global times are exactly g_lo..g_hi, one row each (row = a + g - g_lo)
+    uint64_t g_lo, g_hi; // global_time at the span's ends (enumerate mode's one-round position guess)
 };
 
 // Work counters of the responder (device u64[8], accumulated over a call's windows).
+// Spread over kCntSpread copies (a workgroup adds into copy blockIdx % kCntSpread): thousands of same-address
+// atomics at the end of a launch serialise into its tail; the host sums the copies.
 enum { kCntPairs = 0, kCntBlocks = 1, kCntBytes = 2, kCntUseful = 3, kCntSlots = 4, kCntN = 8 };
+static constexpr uint32_t kCntSpread = 64;
+__device__ __forceinline__ unsigned long long* counter(uint64_t* counters, uint32_t which) {
+    return (unsigned long long*)&counters[(blockIdx.x % kCntSpread) * kCntN + which];
+}
 
 // Per-claim window state.
 struct ReqState {
@@ -98,6 +105,14 @@ struct ReqState {
     uint32_t overflow; // output capacity exceeded (host retries with a larger capacity)
 };
 
+// Device copy of one claim: the fields of dsy_request the kernels read, with the prefix bytes moved to a side
+// buffer (a dsy_request is 296 B because of its 256-byte prefix array; claims carry 1 byte on the wire).
+struct DevRequest {
+    uint64_t time_low, time_high, filter_offset, m_bits;
+    uint32_t modulo, offset, k, hash_kind, chunk_bytes, prefix_len;
+    const uint8_t* prefix;  // device pointer into the call's prefix buffer
+};
+
 struct SegMeta {          // one syncable meta in serving order, resolved against the store
     uint64_t seg_a, seg_b; // live-row segment of this meta id
     uint32_t dir;
@@ -107,7 +122,7 @@ struct SegMeta {          // one syncable meta in serving order, resolved agains
 
 struct RespondLaunch {
     StoreView st;
-    const dsy_request* reqs;  // device [R]
+    const DevRequest* reqs;   // device [R]
     const SegMeta* metas;     // device [J]
     uint32_t R, J;
     const uint8_t* filters;   // device
@@ -122,12 +137,15 @@ struct RespondLaunch {
     Plan* plans;              // device [R*J]
     ReqState* state;          // device [R]
     uint64_t* upper;          // device [R]: upper bound of selected rows per claim
-    uint64_t* pair_row;       // device [R*W]
+    uint64_t* pair_row;       // device [pool]: store row of window slot t
+    uint64_t* pair_off;       // device [pool]: its packet's blob offset
+    uint32_t* pair_len;       // device [pool]: its packet's length
     PairTask* task;           // device [R*W]: per-claim hashing order (window slots sorted by block count)
     uint8_t* miss;            // device [R*W]
     uint64_t* out;            // device [sum cap]
     uint32_t* flags;          // device [4]: [1] an output capacity overflowed
-    uint64_t* counters;       // device [kCntN]: pairs hashed, compression blocks, packet bytes, pairs the reference
+    uint64_t* fill_clock;     // optional [n_act][4] s_memtime stamps of k_fill phases (DSY_FILL_PROFILE)
+    uint64_t* counters;       // device [kCntSpread][kCntN]: pairs hashed, compression blocks, packet bytes, pairs the reference
                               // would have hashed (it stops at the byte limit), lane-block slots of the hashing waves
     hipStream_t stream;
 };

@@ -89,7 +89,7 @@ __global__ void k_plan(RespondLaunch L) {
     const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= L.R * L.J) return;
     const uint32_t r = idx / L.J, j = idx % L.J;
-    const dsy_request& q = L.reqs[r];
+    const DevRequest& q = L.reqs[r];
     const SegMeta& mt = L.metas[j];
     uint64_t lo = q.time_low, hi = q.time_high;
     if (!L.include_inactive && mt.has_pruning) {
@@ -108,6 +108,11 @@ __global__ void k_plan(RespondLaunch L) {
         p.b = hi >= kMaxGt ? mt.seg_b : lower_bound_interp(L.st.live_gt, p.a, mt.seg_b, hi + 1);
     }
     const uint64_t span = p.b - p.a;
+    if (span) {
+        p.g_lo = L.st.live_gt[p.a];
+        p.g_hi = L.st.live_gt[p.b - 1];
+        p.dense = p.g_hi - p.g_lo == span - 1;
+    }
     const uint64_t mod = q.modulo;
     p.mode = 0;
     p.ncand = span;
@@ -136,92 +141,254 @@ __global__ void k_plan(RespondLaunch L) {
 
 // ------------------------------------------------------------------------------------------- k_fill
 static constexpr int kFillThreads = 256;
+static constexpr int kFillWaves = kFillThreads / 64;
+
+// Live-row range [x, y) of global time g inside the plan's span.  One round of three independent loads when the
+// span's global times are dense or evenly spread (the position interpolated from the span's end values is exact);
+// otherwise the interpolation / binary search of lower_bound_interp.
+__device__ __forceinline__ void enum_range(const uint64_t* __restrict__ gt, const Plan& p, uint64_t g, uint64_t* x,
+                                           uint64_t* y) {
+    if (p.a >= p.b || g < p.g_lo || g > p.g_hi) {
+        *x = *y = g < p.g_lo ? p.a : p.b;
+        return;
+    }
+    const uint64_t span = p.b - p.a;
+    uint64_t guess = p.a;
+    if (p.g_hi > p.g_lo)
+        guess = p.a + (uint64_t)((double)(g - p.g_lo) / (double)(p.g_hi - p.g_lo) * (double)(span - 1) + 0.5);
+    if (guess >= p.b) guess = p.b - 1;
+    const uint64_t gp = gt[guess];
+    const uint64_t gq = guess > p.a ? gt[guess - 1] : 0;
+    const uint64_t gn = guess + 1 < p.b ? gt[guess + 1] : ~0ull;
+    if (gp == g && (guess == p.a || gq < g)) {
+        *x = guess;
+        *y = gn != g ? guess + 1 : upper_bound_gt(gt, guess + 1, p.b, g);
+        return;
+    }
+    const uint64_t lx = lower_bound_interp(gt, p.a, p.b, g);
+    uint64_t ly = lx;
+    if (lx < p.b && gt[lx] == g) ly = (lx + 1 < p.b && gt[lx + 1] == g) ? upper_bound_gt(gt, lx + 1, p.b, g) : lx + 1;
+    *x = lx;
+    *y = ly;
+}
 static constexpr uint32_t kSortBins = 1024;
 
 __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* lds, uint64_t* total) {
-    // lds: kFillThreads + 1 words.  Simple Hillis-Steele over LDS (one per window step; not the hot loop).
-    const int t = threadIdx.x;
-    lds[t] = v;
-    __syncthreads();
-    for (int d = 1; d < kFillThreads; d <<= 1) {
-        const uint64_t add = t >= d ? lds[t - d] : 0;
-        __syncthreads();
-        lds[t] += add;
-        __syncthreads();
+    // lds: kFillWaves + 1 words.  Wave-level inclusive scans (no barrier), one LDS round for the wave totals.
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    uint64_t incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += o;
     }
-    const uint64_t incl = lds[t];
-    *total = lds[kFillThreads - 1];
+    if (lane == 63) lds[wv] = incl;
     __syncthreads();
-    return incl - v;
+    uint64_t before = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < kFillWaves; ++w) {
+        const uint64_t x = lds[w];
+        before += w < wv ? x : 0;
+        all += x;
+    }
+    *total = all;
+    __syncthreads();  // lds is reused by the next call
+    return before + incl - v;
 }
 
 __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
-    __shared__ uint64_t scan[kFillThreads + 1];
+    __shared__ uint64_t scan[kFillWaves + 2];
     __shared__ uint32_t first_cross;
     const uint32_t a_slot = blockIdx.x;
+    const uint64_t clk0 = L.fill_clock ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t r = L.act[a_slot];
     ReqState* S = &L.state[r];
     if (S->done) {
         if (threadIdx.x == 0) S->n_window = 0;
         return;
     }
-    const dsy_request& q = L.reqs[r];
+    const DevRequest& q = L.reqs[r];
     const uint64_t W = L.window;
     uint64_t* out = L.pair_row + (uint64_t)a_slot * W;
+    uint64_t* out_off = L.pair_off + (uint64_t)a_slot * W;
+    uint32_t* out_len = L.pair_len + (uint64_t)a_slot * W;
     uint32_t j = S->meta;
     uint64_t c = S->cand, s = S->sub, filled = 0;
     const uint64_t mod = q.modulo, off = q.offset;
+    // each thread takes kCand consecutive candidates, so one round of independent lookups covers
+    // kFillThreads * kCand candidates (the fill is latency-bound: fewer, wider rounds)
+    constexpr int kCand = 4;
+    constexpr uint64_t kBatch = (uint64_t)kFillThreads * kCand;
     while (j < L.J && filled < W) {
         const Plan p = L.plans[(uint64_t)r * L.J + j];
         if (c >= p.ncand) { ++j; c = 0; s = 0; continue; }
-        const uint64_t ci = c + threadIdx.x;
-        const bool valid = ci < p.ncand;
-        uint64_t x = 0, y = 0;  // live-row range of this candidate
-        if (valid) {
-            uint64_t cand = ci;
-            if (p.dir == DSY_DESC) cand = p.ncand - 1 - ci;
-            else if (p.dir == DSY_RANDOM && p.ncand > 1) cand = permute(ci, p.ncand, p.perm_bits, p.perm_key);
+        if (p.dense && p.dir != DSY_RANDOM && (p.mode == 1 || mod <= 1)) {
+            // One row per global time, consecutive: candidate -> row is arithmetic, no lookup and no scan.
+            // Candidates (ascending) whose global time lies in [g_lo, g_hi] are [i0, i1); the others have no row.
+            uint64_t i0 = 0, i1 = p.ncand;
+            if (p.mode == 1) {
+                i0 = p.g_lo > p.g0 ? (p.g_lo - p.g0 + mod - 1) / mod : 0;
+                i1 = p.g_hi >= p.g0 ? (p.g_hi - p.g0) / mod + 1 : 0;
+                if (i1 > p.ncand) i1 = p.ncand;
+                if (i0 > i1) i0 = i1;
+            }
+            // iteration order: ASC visits candidates i0..i1-1, DESC i1-1..i0
+            const uint64_t it0 = p.dir == DSY_DESC ? p.ncand - i1 : i0, it1 = p.dir == DSY_DESC ? p.ncand - i0 : i1;
+            const uint64_t cs = c > it0 ? c : it0;
+            const uint64_t avail = cs < it1 ? it1 - cs : 0;
+            const uint64_t take = avail < W - filled ? avail : W - filled;
+            const uint64_t* __restrict__ offs = L.st.offsets;
+            for (uint64_t i = threadIdx.x; i < take; i += kFillThreads) {
+                const uint64_t ci = cs + i;
+                const uint64_t cd = p.dir == DSY_DESC ? p.ncand - 1 - ci : ci;
+                const uint64_t lr = p.a + (p.mode == 1 ? p.g0 + cd * mod - p.g_lo : cd);
+                const uint64_t row = L.st.live_row ? L.st.live_row[lr] : lr;
+                const uint64_t a0 = offs[row], a1 = offs[row + 1];
+                out[filled + i] = row;
+                out_off[filled + i] = a0;
+                out_len[filled + i] = (uint32_t)(a1 - a0);
+            }
+            filled += take;
+            c = cs + take;
+            if (c >= it1) c = p.ncand;  // the remaining candidates have no row
+            s = 0;
+            continue;
+        }
+        uint64_t xs[kCand], cnts[kCand], sks[kCand];
+        uint64_t tcnt = 0;
+        const uint64_t* __restrict__ gt = L.st.live_gt;
+        // phase A: every candidate's probe addresses, and ALL the loads issued before any is consumed (a branch
+        // between them would serialise kCand memory round-trips)
+        uint64_t cand[kCand], pa[kCand], ga[kCand], gb[kCand], gc[kCand];
+        bool ok[kCand];
+#pragma unroll
+        for (int u = 0; u < kCand; ++u) {
+            const uint64_t ci = c + (uint64_t)threadIdx.x * kCand + u;
+            ok[u] = ci < p.ncand;
+            uint64_t cd = ci;
+            if (p.dir == DSY_DESC) cd = p.ncand - 1 - ci;
+            else if (p.dir == DSY_RANDOM && p.ncand > 1 && ok[u]) cd = permute(ci, p.ncand, p.perm_bits, p.perm_key);
+            cand[u] = cd;
             if (p.mode == 0) {
-                x = p.a + cand;
-                const bool match = mod <= 1 || ((L.st.live_gt[x] + off) % mod) == 0;
-                y = match ? x + 1 : x;
+                pa[u] = p.a + cd;
             } else {
-                const uint64_t g = p.g0 + cand * mod;
-                x = lower_bound_interp(L.st.live_gt, p.a, p.b, g);
-                y = x;
-                if (x < p.b && L.st.live_gt[x] == g) {  // equal range: usually a single row
-                    y = (x + 1 < p.b && L.st.live_gt[x + 1] == g) ? upper_bound_gt(L.st.live_gt, x + 1, p.b, g) : x + 1;
-                }
+                const uint64_t g = p.g0 + cd * mod;
+                uint64_t guess = p.a;
+                if (p.g_hi > p.g_lo && g > p.g_lo)
+                    guess = p.a + (uint64_t)((double)(g - p.g_lo) / (double)(p.g_hi - p.g_lo) * (double)(p.b - p.a - 1) + 0.5);
+                pa[u] = guess < p.b ? guess : p.b - 1;
             }
         }
-        uint64_t cnt = y - x;
-        const uint64_t skip = (threadIdx.x == 0) ? s : 0;
-        cnt = cnt > skip ? cnt - skip : 0;
-        uint64_t total;
-        const uint64_t pos = block_exclusive_scan(cnt, scan, &total);
-        // emit rows of this candidate that still fit in the window
-        for (uint64_t e = 0; e < cnt; ++e) {
-            const uint64_t dst = filled + pos + e;
-            if (dst >= W) break;
-            const uint64_t lr = (p.dir == DSY_DESC) ? (y - 1 - skip - e) : (x + skip + e);
-            out[dst] = L.st.live_row ? L.st.live_row[lr] : lr;
+#pragma unroll
+        for (int u = 0; u < kCand; ++u) {
+            const bool need = ok[u] && p.b > p.a && (p.mode == 1 || mod > 1);
+            ga[u] = need ? gt[pa[u]] : 0;
+            gb[u] = (need && p.mode == 1 && pa[u] > p.a) ? gt[pa[u] - 1] : 0;
+            gc[u] = (need && p.mode == 1 && pa[u] + 1 < p.b) ? gt[pa[u] + 1] : ~0ull;
         }
-        const uint64_t batch = (p.ncand - c) < (uint64_t)kFillThreads ? (p.ncand - c) : (uint64_t)kFillThreads;
+        // phase B: ranges (the enumerate fallback -- a guess that missed -- is rare on dense or even global times)
+#pragma unroll
+        for (int u = 0; u < kCand; ++u) {
+            uint64_t x = 0, y = 0;  // live-row range of this candidate
+            if (ok[u]) {
+                if (p.mode == 0) {
+                    x = pa[u];
+                    y = (mod <= 1 || ((ga[u] + off) % mod) == 0) ? x + 1 : x;
+                } else {
+                    const uint64_t g = p.g0 + cand[u] * mod;
+                    if (p.a >= p.b || g < p.g_lo || g > p.g_hi) {
+                        x = y = g < p.g_lo ? p.a : p.b;
+                    } else if (ga[u] == g && (pa[u] == p.a || gb[u] < g)) {
+                        x = pa[u];
+                        y = gc[u] != g ? x + 1 : upper_bound_gt(gt, x + 1, p.b, g);
+                    } else {
+                        enum_range(gt, p, g, &x, &y);
+                    }
+                }
+            }
+            const uint64_t sk = (threadIdx.x == 0 && u == 0) ? s : 0;  // rows of a resumed candidate already sent
+            uint64_t n = y - x;
+            n = n > sk ? n - sk : 0;
+            // DESC walks the range from its top: the first row emitted is y - 1 - sk
+            xs[u] = p.dir == DSY_DESC ? y - 1 - sk : x + sk;
+            cnts[u] = n;
+            sks[u] = sk;
+            tcnt += n;
+        }
+        uint64_t total;
+        const uint64_t pos = block_exclusive_scan(tcnt, scan, &total);
+        // emit the rows of these candidates that still fit in the window, in candidate order: first every
+        // candidate's first row with all loads issued together, then the rare extra rows of shared global times
+        const uint64_t* __restrict__ offs = L.st.offsets;
+        uint64_t row0[kCand], o0[kCand], o1[kCand];
+#pragma unroll
+        for (int u = 0; u < kCand; ++u) {
+            const uint64_t lr = xs[u];
+            row0[u] = (cnts[u] && L.st.live_row) ? L.st.live_row[lr] : lr;
+        }
+#pragma unroll
+        for (int u = 0; u < kCand; ++u) {
+            o0[u] = cnts[u] ? offs[row0[u]] : 0;
+            o1[u] = cnts[u] ? offs[row0[u] + 1] : 0;
+        }
+        uint64_t at = pos;
+#pragma unroll
+        for (int u = 0; u < kCand; ++u) {
+            const uint64_t dst = filled + at;
+            if (cnts[u] && dst < W) {
+                out[dst] = row0[u];
+                out_off[dst] = o0[u];
+                out_len[dst] = (uint32_t)(o1[u] - o0[u]);
+            }
+            at += cnts[u];
+        }
+        at = pos;
+#pragma unroll
+        for (int u = 0; u < kCand; ++u) {
+            for (uint64_t e = 1; e < cnts[u]; ++e) {
+                const uint64_t dst = filled + at + e;
+                if (dst >= W) break;
+                const uint64_t lr = p.dir == DSY_DESC ? xs[u] - e : xs[u] + e;
+                const uint64_t row = L.st.live_row ? L.st.live_row[lr] : lr;
+                const uint64_t a0 = offs[row], a1 = offs[row + 1];
+                out[dst] = row;
+                out_off[dst] = a0;
+                out_len[dst] = (uint32_t)(a1 - a0);
+            }
+            at += cnts[u];
+        }
+        const uint64_t batch = (p.ncand - c) < kBatch ? (p.ncand - c) : kBatch;
         if (filled + total <= W) {
             filled += total;
             c += batch;
             s = 0;
         } else {
+            // the window ends inside candidate `key`: resume there next window with its rows already sent
             if (threadIdx.x == 0) first_cross = 0xffffffffu;
             __syncthreads();
-            if (valid && filled + pos + cnt > W) atomicMin(&first_cross, threadIdx.x);
+            uint64_t acc = pos, acc_mine = 0;
+            int mine = -1;
+#pragma unroll
+            for (int u = 0; u < kCand; ++u) {
+                if (mine < 0 && cnts[u] > 0 && filled + acc + cnts[u] > W) {
+                    mine = u;
+                    acc_mine = acc;
+                }
+                acc += cnts[u];
+            }
+            if (mine >= 0) atomicMin(&first_cross, threadIdx.x * kCand + (uint32_t)mine);
             __syncthreads();
-            const uint32_t t = first_cross;
-            // broadcast the crossing candidate's position through LDS
-            if (threadIdx.x == t) scan[kFillThreads] = W - filled - pos + skip;
+            const uint32_t key = first_cross;
+            if (threadIdx.x == key / kCand) {
+                uint64_t skm = 0;
+#pragma unroll
+                for (int u = 0; u < kCand; ++u)
+                    if (u == (int)(key % kCand)) skm = sks[u];
+                scan[kFillWaves + 1] = W - filled - acc_mine + skm;
+            }
             __syncthreads();
-            s = scan[kFillThreads];
-            c = c + t;
+            s = scan[kFillWaves + 1];
+            c = c + key;
             filled = W;
             __syncthreads();
         }
@@ -233,6 +400,7 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
         S->n_window = filled;
         if (j >= L.J) S->exhausted = 1;
     }
+    const uint64_t clk1 = L.fill_clock ? __builtin_amdgcn_s_memtime() : 0;
     // Load balance: order this window's pairs by compression-block count (counting sort in LDS) so the 64
     // lanes of a hashing wave run the same number of blocks.  task[i] = the pair hashed by lane-slot i (blob
     // offset, length, window slot), so the hashing kernel reads 16 contiguous bytes per lane and then the packet;
@@ -245,10 +413,7 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
     };
     for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads) hist[i] = 0;
     __syncthreads();
-    for (uint64_t t = threadIdx.x; t < filled; t += kFillThreads) {
-        const uint64_t row = out[t];
-        atomicAdd(&hist[bin_of(L.st.offsets[row + 1] - L.st.offsets[row])], 1u);
-    }
+    for (uint64_t t = threadIdx.x; t < filled; t += kFillThreads) atomicAdd(&hist[bin_of(out_len[t])], 1u);
     __syncthreads();
     if (threadIdx.x < 64) {  // exclusive scan of the kSortBins counters by one wave
         const uint32_t per = kSortBins / 64, lane = threadIdx.x;
@@ -270,13 +435,18 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
     __syncthreads();
     PairTask* task = L.task + (uint64_t)a_slot * W;
     for (uint64_t t = threadIdx.x; t < filled; t += kFillThreads) {
-        const uint64_t row = out[t];
-        const uint64_t a = L.st.offsets[row], e = L.st.offsets[row + 1];  // just read above: cache hits
         PairTask tk;
-        tk.off = a;
-        tk.len = (uint32_t)(e - a);
+        tk.off = out_off[t];
+        tk.len = out_len[t];
         tk.slot = (uint32_t)t;
-        task[atomicAdd(&hist[bin_of(e - a)], 1u)] = tk;
+        task[atomicAdd(&hist[bin_of(tk.len)], 1u)] = tk;
+    }
+    if (L.fill_clock && threadIdx.x == 0) {
+        uint64_t* fc = L.fill_clock + (uint64_t)a_slot * 4;
+        fc[0] = clk0;
+        fc[1] = clk1;
+        fc[2] = __builtin_amdgcn_s_memtime();
+        fc[3] = filled;
     }
 }
 
@@ -303,7 +473,7 @@ __global__ void __launch_bounds__(256) k_pair_test(RespondLaunch L, const uint32
         if (i0 >= n) continue;  // wave-uniform: past this claim's window
         const uint64_t i = i0 + lane;
         const bool active = i < n;
-        const dsy_request& q = L.reqs[r];
+        const DevRequest& q = L.reqs[r];
         uint32_t t = 0;
         KeyView kv{L.st.blob, 0u, q.prefix, q.prefix_len};  // idle lanes hash an empty key
         if (active) {
@@ -359,9 +529,9 @@ __global__ void __launch_bounds__(256) k_pair_test(RespondLaunch L, const uint32
     if (threadIdx.x == 0) {
         unsigned long long b = 0, y = 0, z = 0;
         for (uint32_t wv = 0; wv < blockDim.x / 64; ++wv) b += red[0][wv], y += red[1][wv], z += red[2][wv];
-        if (b) atomicAdd((unsigned long long*)&L.counters[kCntBlocks], b);
-        if (y) atomicAdd((unsigned long long*)&L.counters[kCntBytes], y);
-        if (z) atomicAdd((unsigned long long*)&L.counters[kCntSlots], z);
+        if (b) atomicAdd(counter(L.counters, kCntBlocks), b);
+        if (y) atomicAdd(counter(L.counters, kCntBytes), y);
+        if (z) atomicAdd(counter(L.counters, kCntSlots), z);
     }
 }
 
@@ -426,42 +596,53 @@ __global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
     uint32_t done = 0, overflow = S->overflow;
     uint64_t useful = n;  // pairs the reference hashes in this window: up to the packet that spends the budget
     const int64_t limit = L.byte_limit;
-    for (uint64_t t0 = 0; t0 < n && !done; t0 += 64) {
-        const uint64_t t = t0 + lane;
-        const bool valid = t < n;
-        const bool miss = valid && L.miss[(uint64_t)a_slot * W + t];
-        uint64_t row = 0;
-        int64_t len = 0;
-        if (miss) {
-            row = L.pair_row[(uint64_t)a_slot * W + t];
-            len = (int64_t)(L.st.offsets[row + 1] - L.st.offsets[row]);
+    const uint8_t* miss_w = L.miss + (uint64_t)a_slot * W;
+    const uint32_t* len_w = L.pair_len + (uint64_t)a_slot * W;
+    const uint64_t* row_w = L.pair_row + (uint64_t)a_slot * W;
+    // groups of 4 chunks: their flags and lengths are fetched together (one memory round-trip per 256 pairs
+    // instead of one per 64), then the chunks are compacted in order
+    constexpr int kGroup = 4;
+    for (uint64_t g0 = 0; g0 < n && !done; g0 += 64 * kGroup) {
+        uint32_t lens[kGroup];
+#pragma unroll
+        for (int u = 0; u < kGroup; ++u) {
+            const uint64_t t = g0 + 64 * u + lane;
+            lens[u] = (t < n && miss_w[t]) ? len_w[t] : 0u;
         }
-        const int64_t incl = wave_inclusive_scan(len);
-        const int64_t excl = incl - len;
-        const uint64_t mmask = __ballot(miss);
-        const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-        const uint32_t rank = __popcll(mmask & lt);
-        // send while the budget before this packet is positive; the first packet is always sent
-        const bool inc = miss && ((emitted + rank == 0) || (spent + excl < limit));
-        const uint64_t imask = __ballot(inc);
-        const uint32_t nin = __popcll(imask);
-        if (inc) {
-            const uint64_t slot = emitted + rank;
-            if (slot < S->cap) L.out[S->out_base + slot] = row;
-            else overflow = 1;
-        }
-        // bytes of the included prefix = inclusive scan at the last included lane
-        int64_t sum_in = 0;
-        int last = -1;
-        if (nin) {
-            last = 63 - __builtin_clzll(imask);
-            sum_in = __shfl(incl, last, 64);
-        }
-        emitted += nin;
-        spent += sum_in;
-        if (emitted > 0 && spent >= limit) {
-            done = 1;
-            useful = t0 + (uint64_t)last + 1;
+#pragma unroll
+        for (int u = 0; u < kGroup; ++u) {
+            const uint64_t t0 = g0 + 64 * u;
+            if (done || t0 >= n) break;
+            const uint64_t t = t0 + lane;
+            const bool miss = t < n && miss_w[t];
+            const int64_t len = miss ? (int64_t)lens[u] : 0;
+            const int64_t incl = wave_inclusive_scan(len);
+            const int64_t excl = incl - len;
+            const uint64_t mmask = __ballot(miss);
+            const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+            const uint32_t rank = __popcll(mmask & lt);
+            // send while the budget before this packet is positive; the first packet is always sent
+            const bool inc = miss && ((emitted + rank == 0) || (spent + excl < limit));
+            const uint64_t imask = __ballot(inc);
+            const uint32_t nin = __popcll(imask);
+            if (inc) {
+                const uint64_t slot = emitted + rank;
+                if (slot < S->cap) L.out[S->out_base + slot] = row_w[t];
+                else overflow = 1;
+            }
+            // bytes of the included prefix = inclusive scan at the last included lane
+            int64_t sum_in = 0;
+            int last = -1;
+            if (nin) {
+                last = 63 - __builtin_clzll(imask);
+                sum_in = __shfl(incl, last, 64);
+            }
+            emitted += nin;
+            spent += sum_in;
+            if (emitted > 0 && spent >= limit) {
+                done = 1;
+                useful = t0 + (uint64_t)last + 1;
+            }
         }
     }
     overflow = __any(overflow) ? 1u : 0u;
@@ -472,8 +653,8 @@ __global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
         if (overflow) L.flags[1] = 1;
         if (done || S->exhausted) S->done = 1;
         L.act_done[a_slot] = (uint8_t)S->done;
-        atomicAdd((unsigned long long*)&L.counters[kCntPairs], (unsigned long long)n);
-        atomicAdd((unsigned long long*)&L.counters[kCntUseful], (unsigned long long)useful);
+        atomicAdd(counter(L.counters, kCntPairs), (unsigned long long)n);
+        atomicAdd(counter(L.counters, kCntUseful), (unsigned long long)useful);
     }
 }
 

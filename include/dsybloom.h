@@ -120,6 +120,10 @@ int dsy_ctx_reset_timing(dsy_ctx* ctx);
  * windows --, out4[3] lane-block slots of the hashing waves (64 x the longest lane per wave-task): out4[0] / out4[3]
  * is the active-lane fraction. */
 int dsy_ctx_work(dsy_ctx* ctx, int which, uint64_t* out4);
+/* Cap the responder's window at max_pairs (a multiple of 64; 0 restores the default, which grows from 4096 to 2^18
+ * pairs per claim as claims finish).  Results do not depend on it; tests use small windows to exercise the
+ * resumable cursor. */
+int dsy_ctx_set_window(dsy_ctx* ctx, uint64_t max_pairs);
 
 /* ---------------------------------------------------------------------------------- BloomFilter kernels */
 /* Replaces BloomFilter.add / add_keys (bloomfilter.py:163-194): ORs the k bits of every key into filter_inout

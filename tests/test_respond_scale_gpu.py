@@ -23,7 +23,12 @@ METAS = [("a", 1, "ASC", 128, None), ("d", 2, "DESC", 200, None), ("p", 3, "ASC"
 def build(seed, n, gt_max, skew):
     rng = np.random.Generator(np.random.PCG64(seed))
     meta = rng.choice([1, 2, 3, 4], size=n, p=[0.5, 0.25, 0.2, 0.05])
-    if skew:
+    if skew == "dense":  # one row per global time, consecutive within each meta (k_fill's arithmetic path)
+        gt = np.zeros(n, dtype=np.int64)
+        for m in (1, 2, 3, 4):
+            idx = np.flatnonzero(meta == m)
+            gt[idx] = np.arange(1, len(idx) + 1) + 10 * m
+    elif skew:
         gt = np.minimum(rng.zipf(1.1, size=n), gt_max)
     else:
         gt = rng.integers(1, gt_max + 1, size=n)
@@ -48,13 +53,17 @@ def oracle_metas():
     return [dict(name=n, id=i, direction=d, priority=p, pruning=pr) for n, i, d, p, pr in METAS]
 
 
-@pytest.mark.parametrize("skew", [False, True])
-def test_respond_vs_oracle(skew):
-    rows, conn = build(11 + skew, 60_000, 200_000 if not skew else 5_000, skew)
+@pytest.mark.parametrize("window", [0, 256, 4160])
+@pytest.mark.parametrize("skew", [False, True, "dense"])
+def test_respond_vs_oracle(skew, window):
+    """window caps the responder's window (dsy_ctx_set_window): 0 is the default growing window; 256 and 4160 force
+    claims across many windows, so the resumable (meta, candidate, sub-row) cursor is exercised in every direction."""
+    seed = {False: 0, True: 1, "dense": 2}[skew]
+    rows, conn = build(11 + seed, 60_000, 200_000 if skew is False else 5_000, skew)
     store = SyncStore.from_rows(rows)
-    gt_now = 200_100 if not skew else 5_050
+    gt_now = {False: 200_100, True: 5_050, "dense": 30_100}[skew]
     com = SyncCommunity(store, metas(), global_time=gt_now)
-    rng = np.random.Generator(np.random.PCG64(5 + skew))
+    rng = np.random.Generator(np.random.PCG64(5 + seed))
     packets = {r[0]: r[4] for r in rows}
     reqs, oracle_blooms = [], []
     shapes = [(10160, 0.01), (4096, 0.001), (1 << 15, 0.01), (1 << 16, 0.0001)]
@@ -74,9 +83,20 @@ def test_respond_vs_oracle(skew):
         assert bf.bytes == ob.to_bytes()
         reqs.append(ClaimRequest(lo, hi, modulo, offset, bf))
         oracle_blooms.append(ob)
-    for include_inactive, limit in ((False, 5120), (True, 1 << 40), (False, 1)):
-        got = com.respond(reqs, include_inactive=include_inactive, byte_limit=limit)
-        for q, ob, g in zip(reqs, oracle_blooms, got):
-            want = sync_ref.respond_lists(conn, oracle_metas(), (q.time_low, q.time_high, q.offset, q.modulo), ob,
-                                          gt_now, limit, include_inactive)
-            assert store.rowid[g].tolist() == want, (q.time_low, q.time_high, q.modulo, q.offset, limit)
+    store.ctx.set_window(window)
+    try:
+        results = [(inc, limit, com.respond(reqs, include_inactive=inc, byte_limit=limit))
+                   for inc, limit in ((False, 5120), (True, 1 << 40), (False, 1))]
+    finally:
+        store.ctx.set_window(0)
+    for include_inactive, limit, got in results:
+        for i, (q, ob, g) in enumerate(zip(reqs, oracle_blooms, got)):
+            key = (skew, include_inactive, limit, i)
+            if key not in _ORACLE:  # the oracle's answer does not depend on the window: computed once per claim
+                _ORACLE[key] = sync_ref.respond_lists(conn, oracle_metas(), (q.time_low, q.time_high, q.offset,
+                                                                             q.modulo), ob, gt_now, limit,
+                                                      include_inactive)
+            assert store.rowid[g].tolist() == _ORACLE[key], (q.time_low, q.time_high, q.modulo, q.offset, limit)
+
+
+_ORACLE = {}
