@@ -843,8 +843,10 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
 
     // ---- windows: fill -> hash/test (one launch per hash family) -> compact; one host sync per window.  Only
     // the active claims take part; as they finish, the rest share the pool in bigger windows.
-    std::vector<uint32_t> act;
-    bool first = true;
+    void *d_packed_v, *d_packed_off_v;
+    if ((rc = ws_get(c, "packed", std::max<uint64_t>(cap_total, 1) * 8, &d_packed_v))) return rc;
+    if ((rc = ws_get(c, "packed_off", ((size_t)R + 1) * 8, &d_packed_off_v))) return rc;
+    bool first = true, ran = false;
     for (;;) {
         std::vector<std::pair<size_t, size_t>> runs;  // per family: (first slot, slots)
         size_t n_act = 0;
@@ -866,6 +868,7 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
             HIP_TRY(hipMemcpyAsync(d_act, h_act, n_act * 4, hipMemcpyHostToDevice, c->stream));
         }
         first = false;
+        ran = true;
         static const bool fill_profile = getenv("DSY_FILL_PROFILE") != nullptr;
         void* d_fc = nullptr;
         if (fill_profile) {
@@ -908,6 +911,9 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
         HIP_TRY(launch_compact(L));
         timer_end(c, &t);
         HIP_TRY(hipMemcpyAsync(h_io, d_io, head_b + n_act, hipMemcpyDeviceToHost, c->stream));
+        // speculatively pack the output now (it is redone if another window follows): the GPU packs while the
+        // host wakes up and reads the status
+        HIP_TRY(launch_pack(L, (uint64_t*)d_packed_v, (uint64_t*)d_packed_off_v, nullptr));
         HIP_TRY(hipStreamSynchronize(c->stream));
         // capacity overflow can only come from a wrong min_len bound; report it loudly
         if (((uint32_t*)(h_io + cnt_b))[1]) return fail(DSY_ECAPACITY, "internal: a claim overflowed its output capacity");
@@ -923,10 +929,7 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     uint64_t h_tot[kCntN] = {0};
     for (uint32_t i = 0; i < kCntSpread; ++i)
         for (uint32_t k = 0; k < kCntN; ++k) h_tot[k] += ((const uint64_t*)h_io)[i * kCntN + k];
-    void *d_packed_v, *d_packed_off_v;
-    if ((rc = ws_get(c, "packed", std::max<uint64_t>(cap_total, 1) * 8, &d_packed_v))) return rc;
-    if ((rc = ws_get(c, "packed_off", ((size_t)R + 1) * 8, &d_packed_off_v))) return rc;
-    HIP_TRY(launch_pack(L, (uint64_t*)d_packed_v, (uint64_t*)d_packed_off_v, nullptr));
+    if (!ran) HIP_TRY(launch_pack(L, (uint64_t*)d_packed_v, (uint64_t*)d_packed_off_v, nullptr));
     timers_collect_lazy(c);
     c->blocks[kTimePairTest] += h_tot[kCntBlocks];
     c->bytes[kTimePairTest] += h_tot[kCntBytes];
