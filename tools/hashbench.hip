@@ -481,6 +481,66 @@ float run(const uint8_t* blob, const uint64_t* off, const uint32_t* order, uint3
 }
 
 // the product's hash_key_dma (dsy_message.h) in WG-thread workgroups, one 64-key wave-task per wave
+// load-only probe: the DMA pattern of hash_key_dma_reg<S> with every stage's 64*S-byte piece aligned down to a
+// 64*S boundary (pieces = whole cache lines); consumes the LDS bytes with a cheap XOR (not a digest)
+template <int S, int WG, bool ALIGN>
+__global__ void __launch_bounds__(WG) k_load_probe(const uint8_t* blob, const uint64_t* off, const uint32_t* order,
+                                                   uint32_t n, uint32_t* out) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    using G = DmaGeometry<S, 1>;
+    uint8_t* lds_wave = dyn + (threadIdx.x >> 6) * G::kWaveBytes;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t i = blockIdx.x * WG + threadIdx.x;
+    const uint32_t key = order ? order[min(i, n - 1)] : min(i, n - 1);
+    const uint64_t a = off[key], e = off[key + 1];
+    const uint32_t len = i < n ? (uint32_t)(e - a) : 0u;
+    const uint64_t start = (uint64_t)(uintptr_t)(blob + a) - 1;  // 1-byte prefix
+    const uint64_t base = ALIGN ? start & ~(uint64_t)(S * 64 - 1) : start;
+    const uint32_t total = (uint32_t)(start - base) + 1 + len + 9;
+    uint32_t nst = (total + S * 64 - 1) / (S * 64);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) nst = max(nst, (uint32_t)__shfl_xor((int)nst, d, 64));
+    uint32_t acc = 0;
+    for (uint32_t s = 0; s < nst; ++s) {
+#pragma unroll
+        for (int k = 0; k < G::kInsts; ++k) {
+            const int p = G::kKeysPerInst * k + (int)(lane / G::kChunks);
+            const uint32_t blo = __shfl((int)(uint32_t)base, p, 64), bhi = __shfl((int)(uint32_t)(base >> 32), p, 64);
+            const uint32_t pend = __shfl((int)total, p, 64);
+            const uint32_t c = lane % G::kChunks;
+            const uint64_t b64 = ((uint64_t)bhi << 32) | blo;
+            if (s * (S * 64) < pend)
+                __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)(b64 + s * (S * 64) + 16 * c),
+                                                 (__attribute__((address_space(3))) void*)(lds_wave + k * 1024), 16, 0, 0);
+        }
+        __builtin_amdgcn_s_waitcnt(0x0f70);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < 4 * S; ++q) acc ^= *(const uint32_t*)(lds_wave + (lane / G::kKeysPerInst) * 1024 + 16 * (G::kChunks * (lane % G::kKeysPerInst) + q));
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (i < n) out[i] = acc;
+}
+
+template <int S, int WG, bool ALIGN>
+float run_probe(const uint8_t* blob, const uint64_t* off, const uint32_t* order, uint32_t n, uint32_t* out, int reps) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    dim3 grid((n + WG - 1) / WG);
+    const size_t dl = (size_t)(WG / 64) * DmaGeometry<S, 1>::kWaveBytes;
+    hipLaunchKernelGGL((k_load_probe<S, WG, ALIGN>), grid, dim3(WG), dl, 0, blob, off, order, n, out);
+    CK(hipEventRecord(a));
+    for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((k_load_probe<S, WG, ALIGN>), grid, dim3(WG), dl, 0, blob, off, order, n, out);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    g_checksum = 0;
+    return ms / reps;
+}
+
 template <class H, int S, int WG>
 __global__ void __launch_bounds__(WG) k_hash_dma_r(const uint8_t* blob, const uint64_t* off, const uint32_t* order,
                                                    uint32_t n, const uint8_t* pre, uint32_t plen, uint32_t* out) {
@@ -509,6 +569,162 @@ float run_dma_r(const uint8_t* blob, const uint64_t* off, const uint32_t* order,
     CK(hipEventRecord(a));
     for (int r = 0; r < reps; ++r)
         hipLaunchKernelGGL((k_hash_dma_r<H, S, WG>), grid, dim3(WG), dl, 0, blob, off, order, n, pre, plen, out);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    std::vector<uint32_t> h(n), ord(n), byk(n);
+    CK(hipMemcpy(h.data(), out, n * 4, hipMemcpyDeviceToHost));
+    if (order) {
+        CK(hipMemcpy(ord.data(), order, n * 4, hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < n; ++i) byk[ord[i]] = h[i];
+    } else byk = h;
+    uint64_t cs = 0;
+    for (uint32_t i = 0; i < n; ++i) cs = cs * 1000003u + byk[i];
+    g_checksum = cs;
+    return ms / reps;
+}
+
+// EXPERIMENT (not in the product; result in DESIGN.md): line-aligned variant (64-byte-block hashes): every DMA piece is one whole, aligned 128-byte line of the key's
+// window [start & ~127, ...), so a key of L bytes costs ceil((mis + L + pad) / 128) lines instead of the ~2x that
+// unaligned 128-byte pieces touch (tools/hashbench probes: 4.6 vs 3.4 TB/s loads-only, 10.2 vs 17.6 GB fetched
+// for 8 GB of packets).  Two stage buffers form a per-key ring of 16 chunks; block b of the message sits at window
+// byte mis + 64 b and is assembled from 5 aligned 16-byte chunks by a per-lane funnel shift.  In every iteration a
+// lane compresses the (at most two) blocks that end inside the stages landed so far, from registers, while the
+// next stage's DMA is in flight.  Dead lanes issue nothing; every wait is vmcnt(0).
+template <class H, int S = 2>
+__device__ __forceinline__ void hb_hash_key_dma_aligned(const KeyView& kv, H& st, uint8_t* lds_wave) {
+    static_assert(H::block_bytes == 64, "LDS-DMA staging is for 64-byte blocks");
+    using G = DmaGeometry<S, 1>;
+    constexpr uint32_t kSt = 64 * S;  // stage bytes per key (aligned to kSt)
+    constexpr int kD = 4 * (4 * S + 1);  // dwords of the chunks S blocks need
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t r = kv.plen;
+    const uint32_t total = r + kv.len;
+    const uint32_t nb = n_blocks(total, 64, H::len_bytes);
+    const uint64_t start = (uint64_t)(uintptr_t)kv.key - r;
+    const uint64_t base = start & ~(uint64_t)(kSt - 1);
+    const uint32_t mis = (uint32_t)(start - base);
+    const uint32_t wend = mis + 64 * nb;  // window bytes the message's blocks occupy
+    const uint32_t dend = mis + total;    // stages past the key's last byte hold only padding: not loaded
+    uint32_t nst = (wend + kSt - 1) / kSt;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) nst = max(nst, (uint32_t)__shfl_xor((int)nst, d, 64));
+    uint32_t preword = 0;
+    for (uint32_t j = 0; j < r; ++j) preword |= (uint32_t)kv.pre[j] << (8 * j);
+    // the key's 16-byte chunk C of the window (stage C / kChunks) lives in buffer (stage & 1) at the slot
+    // hash_key_dma_reg's layout gives chunk C % kChunks
+    const uint32_t row = (lane / G::kKeysPerInst) * 1024 + 16 * G::kChunks * (lane % G::kKeysPerInst);
+    auto chunk_addr = [&](uint32_t C) {
+        const uint32_t c = C % G::kChunks;
+        return lds_wave + ((C / G::kChunks) & 1) * G::kStageBytes + row +
+               16 * ((c - (lane >> G::kShift)) % G::kChunks);
+    };
+    auto issue = [&](uint32_t s) {
+        uint8_t* buf = lds_wave + (s & 1) * G::kStageBytes;
+#pragma unroll
+        for (int i = 0; i < G::kInsts; ++i) {
+            const int p = G::kKeysPerInst * i + (int)(lane / G::kChunks);
+            const uint32_t blo = __shfl((int)(uint32_t)base, p, 64), bhi = __shfl((int)(uint32_t)(base >> 32), p, 64);
+            const uint32_t pend = __shfl((int)dend, p, 64);
+            const uint32_t c = ((lane % G::kChunks) + ((uint32_t)p >> G::kShift)) % G::kChunks;
+            const uint64_t b64 = ((uint64_t)bhi << 32) | blo;
+            if (s * kSt < pend)
+                __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)(b64 + s * kSt + 16 * c),
+                                                 (__attribute__((address_space(3))) void*)(buf + i * 1024), 16, 0, 0);
+        }
+    };
+    st.init();
+    // the funnel shift (dword part as two select masks, byte part), the same for every block of the key
+    const uint32_t m2 = (mis & 8) ? ~0u : 0u, m1 = (mis & 4) ? ~0u : 0u, bs = mis & 3;
+    uint32_t b = 0;  // this lane's next block
+    if (nst) issue(0);
+    for (uint32_t s = 0; s < nst; ++s) {
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): stage s has landed
+        __builtin_amdgcn_wave_barrier();
+        // the blocks b .. b+S-1 that end inside stages <= s (a block not done yet starts in stage s-1 or s)
+        const uint32_t lim = kSt * (s + 1);
+        const uint32_t C0 = (mis + 64 * b) >> 4;
+        uint32_t d[kD];
+#pragma unroll
+        for (int q = 0; q < kD / 4; ++q) {
+            const uint4 v = *(const uint4*)chunk_addr(C0 + q);
+            d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): buffer (s-1) & 1 may be refilled now
+        __builtin_amdgcn_wave_barrier();
+        if (s + 1 < nst) issue(s + 1);
+#pragma unroll 1
+        for (uint32_t u = 0, b0 = b; u < (uint32_t)S; ++u) {
+            const uint32_t bb = b0 + u;
+            if (bb < nb && mis + 64 * bb + 64 <= lim) {
+                // f[j] = d[ds + j] by value selects (no indexed register array), then w[i] = bytes bs.. of f[i], f[i+1]
+                uint32_t e[18], f[17];
+#pragma unroll
+                for (int i = 0; i < 18; ++i) e[i] = bop3<kCh>(m2, d[i + 2], d[i]);
+#pragma unroll
+                for (int i = 0; i < 17; ++i) f[i] = bop3<kCh>(m1, e[i + 1], e[i]);
+                uint32_t w[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_alignbyte(f[i + 1], f[i], bs);
+                const uint32_t o0 = bb * 64;
+                if (bb == 0 && r) w[0] = (w[0] & ~low_bytes_mask(r)) | preword;
+                if (o0 + 64 > total) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        const int rel = (int)total - (int)o0 - 4 * i;
+                        if (rel <= 0) w[i] = rel == 0 ? 0x80u : 0u;
+                        else if (rel < 4) w[i] = (w[i] & ((1u << (8 * rel)) - 1u)) | (0x80u << (8 * rel));
+                    }
+                }
+                if (H::big_endian) {
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) w[i] = bswap32(w[i]);
+                }
+                if (bb + 1 == nb) {
+                    const uint64_t bits = (uint64_t)total * 8u;
+                    if (H::big_endian) { w[14] = (uint32_t)(bits >> 32); w[15] = (uint32_t)bits; }
+                    else { w[14] = (uint32_t)bits; w[15] = (uint32_t)(bits >> 32); }
+                }
+                st.compress(w);
+                ++b;
+            }
+            if (S > 1) {
+#pragma unroll
+                for (int i = 0; i < kD - 16; ++i) d[i] = d[i + 16];  // the next block's chunks
+            }
+        }
+    }
+}
+
+template <class H, int S, int WG>
+__global__ void __launch_bounds__(WG) k_hash_dma_a(const uint8_t* blob, const uint64_t* off, const uint32_t* order,
+                                                   uint32_t n, const uint8_t* pre, uint32_t plen, uint32_t* out) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    const uint32_t i = blockIdx.x * WG + threadIdx.x;
+    const uint32_t key = order ? order[min(i, n - 1)] : min(i, n - 1);
+    const uint64_t a = off[key], e = off[key + 1];
+    KeyView kv{blob + a, i < n ? (uint32_t)(e - a) : 0u, pre, plen};
+    H st;
+    hb_hash_key_dma_aligned<H, S>(kv, st, dyn + (threadIdx.x >> 6) * DmaGeometry<S, 2>::kWaveBytes);
+    uint32_t x = 0;
+#pragma unroll
+    for (int j = 0; j < H::digest_bytes / 4; ++j) x ^= st.be_word(j);
+    if (i < n) out[i] = x;
+}
+
+template <class H, int S, int WG>
+float run_dma_a(const uint8_t* blob, const uint64_t* off, const uint32_t* order, uint32_t n, const uint8_t* pre,
+                uint32_t plen, uint32_t* out, int reps) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    dim3 grid((n + WG - 1) / WG);
+    const size_t dl = (size_t)(WG / 64) * DmaGeometry<S, 2>::kWaveBytes;
+    hipLaunchKernelGGL((k_hash_dma_a<H, S, WG>), grid, dim3(WG), dl, 0, blob, off, order, n, pre, plen, out);
+    CK(hipEventRecord(a));
+    for (int r = 0; r < reps; ++r)
+        hipLaunchKernelGGL((k_hash_dma_a<H, S, WG>), grid, dim3(WG), dl, 0, blob, off, order, n, pre, plen, out);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     float ms;
@@ -613,21 +829,20 @@ int main(int argc, char** argv) {
         struct R { const char* name; float ms; uint64_t cs = 0; };
         std::vector<R> rs;
 #define V(NAME, CALL) { float ms_ = CALL; rs.push_back({NAME, ms_, g_checksum}); }
-        V("md5 dma(2,2) wg256", (run_dma_p<Md5, 2, 2, 256, 0>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
-        V("md5 dmareg(1) wg256", (run_dma_r<Md5, 1, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
         V("md5 dmareg(2) wg256", (run_dma_r<Md5, 2, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
-        V("md5 dmareg(2) wg128", (run_dma_r<Md5, 2, 128>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
-        V("md5 dmareg(4) wg256", (run_dma_r<Md5, 4, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
-        V("md5 dmareg(2) wg256 scat", (run_dma_r<Md5, 2, 256>(d_blob, d_off, d_scat_sorted, n, d_pre, 1, d_out, reps)));
-        V("null dma(2,2) wg256", (run_dma_p<NullHash, 2, 2, 256, 0>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
-        V("null dmareg(2) wg256", (run_dma_r<NullHash, 2, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
-        V("null dmareg(4) wg256", (run_dma_r<NullHash, 4, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
-        V("sha1 fast sorted", (run<Sha1, kFast>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
-        V("sha1 dmareg(1) wg256", (run_dma_r<Sha1, 1, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+        V("md5 aligned S2 wg256", (run_dma_a<Md5, 2, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+        V("md5 aligned S1 wg256", (run_dma_a<Md5, 1, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+        V("md5 aligned S1 wg128", (run_dma_a<Md5, 1, 128>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+        V("md5 dmareg(2) plen3", (run_dma_r<Md5, 2, 256>(d_blob, d_off, d_order, n, d_pre, 3, d_out, reps)));
+        V("md5 aligned S1 plen3", (run_dma_a<Md5, 1, 256>(d_blob, d_off, d_order, n, d_pre, 3, d_out, reps)));
+        V("md5 aligned S2 plen3", (run_dma_a<Md5, 2, 256>(d_blob, d_off, d_order, n, d_pre, 3, d_out, reps)));
         V("sha1 dmareg(2) wg256", (run_dma_r<Sha1, 2, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
-        V("sha1 pure sorted", (run<Sha1, kPure>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
-        V("sha256 fast sorted", (run<Sha256, kFast>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
-        V("sha256 dmareg(1) wg256", (run_dma_r<Sha256, 1, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+        V("sha1 aligned S1 wg256", (run_dma_a<Sha1, 1, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+        V("sha1 aligned S2 wg256", (run_dma_a<Sha1, 2, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+        V("md5 dmareg(2) scat", (run_dma_r<Md5, 2, 256>(d_blob, d_off, d_scat_sorted, n, d_pre, 1, d_out, reps)));
+        V("md5 aligned S1 scat", (run_dma_a<Md5, 1, 256>(d_blob, d_off, d_scat_sorted, n, d_pre, 1, d_out, reps)));
+        V("probe S=1 aligned", (run_probe<1, 256, true>(d_blob, d_off, d_order, n, d_out, reps)));
+        V("probe S=2 unaligned", (run_probe<2, 256, false>(d_blob, d_off, d_order, n, d_out, reps)));
 #undef V
         for (auto& r : rs) (void)0;
         for (auto& r : rs)

@@ -28,13 +28,18 @@ def short(name):
 
 def main():
     rnd, trace = sys.argv[1], sys.argv[2]
-    pmc_dirs = sys.argv[3:]
+    pmc_dirs = [d for d in sys.argv[3:] if not d.startswith("--full=")]
+    full = [d[len("--full="):] for d in sys.argv[3:] if d.startswith("--full=")]
     out = os.path.join(ROOT, "profiles")
     os.makedirs(out, exist_ok=True)
     stats = glob.glob(os.path.join(trace, "**", "*kernel_stats.csv"), recursive=True)
     if stats:
         shutil.copy(stats[0], os.path.join(out, "%s_kernel_stats.csv" % rnd))
         print(open(stats[0]).read()[:3000])
+    for d in full:
+        fs = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)
+        if fs:
+            shutil.copy(fs[0], os.path.join(out, "%s_full_kernel_stats.csv" % rnd))
     per = defaultdict(lambda: defaultdict(list))
     for d in pmc_dirs:
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
