@@ -177,8 +177,12 @@ class Context(object):
     def synchronize(self):
         check(self.lib.dsy_ctx_synchronize(self.handle))
 
-    def set_timing(self, on):
-        check(self.lib.dsy_ctx_set_timing(self.handle, 1 if on else 0))
+    def set_timing(self, on, only=None):
+        """on: bracket kernel launches with HIP events; only: an iterable of TIME_* classes to bracket (default all)."""
+        mode = 0
+        if on:
+            mode = 1 if only is None else 0x100 | sum(1 << int(w) for w in only)
+        check(self.lib.dsy_ctx_set_timing(self.handle, mode))
 
     def reset_timing(self):
         check(self.lib.dsy_ctx_reset_timing(self.handle))

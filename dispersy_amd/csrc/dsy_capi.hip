@@ -58,7 +58,7 @@ struct dsy_ctx {
     std::mutex mu;
     std::map<std::string, DevBuf> ws;
     uint32_t max_grid = 2048;
-    bool timing = false;
+    uint32_t timing = 0;  // bit i: bracket class i with events
     std::vector<PendingTimer> pending;
     std::vector<hipEvent_t> event_pool;
     double time_ms[kTimeClasses] = {0, 0, 0, 0};
@@ -87,8 +87,9 @@ struct dsy_store {
 namespace {
 
 // grow-only named workspace buffer
-int ws_get(dsy_ctx* c, const char* name, size_t bytes, void** out) {
+int ws_get(dsy_ctx* c, const char* name, size_t bytes, void** out, bool* fresh = nullptr) {
     DevBuf& b = c->ws[name];
+    if (fresh) *fresh = b.bytes < bytes;
     if (b.bytes < bytes) {
         if (b.ptr) hipFree(b.ptr);
         b.ptr = nullptr;
@@ -135,7 +136,7 @@ hipEvent_t take_event(dsy_ctx* c) {
 void timer_begin(dsy_ctx* c, PendingTimer* t, int cls) {
     t->cls = cls;
     t->a = t->b = nullptr;
-    if (!c->timing) return;
+    if (!(c->timing & (1u << cls))) return;
     t->a = take_event(c);
     t->b = take_event(c);
     hipEventRecord(t->a, c->stream);
@@ -363,7 +364,7 @@ void* dsy_ctx_stream(dsy_ctx* c) { return c ? (void*)c->stream : nullptr; }
 int dsy_ctx_set_timing(dsy_ctx* c, int enable) {
     if (!c) return fail(DSY_EINVAL, "ctx is NULL");
     Guard g(c);
-    c->timing = enable != 0;
+    c->timing = (enable & 0x100) ? (uint32_t)(enable & 0xff) : enable ? 0xffu : 0u;
     return DSY_OK;
 }
 
@@ -701,13 +702,17 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     size_t prefix_b = 0;
     for (uint32_t r = 0; r < R; ++r) prefix_b += reqs[r].prefix_len;
     const size_t reqs_b = (size_t)R * sizeof(DevRequest), metas_b = (size_t)J * sizeof(SegMeta);
-    const size_t in_b = reqs_b + metas_b + (size_t)R * 8 + (prefix_b + 15) / 16 * 16 + 64;
+    const size_t in_b = (reqs_b + metas_b + (size_t)R * 8 + (prefix_b + 15) / 16 * 16 + 64 + 15) / 16 * 16;
     const size_t act_done_b = ((size_t)R + 15) / 16 * 16;
     const size_t cnt_b = kCntSpread * kCntN * 8, head_b = cnt_b + 64;
     const size_t io_b = head_b + act_done_b + (size_t)R * 8;
     int rc;
-    void *d_in, *d_io, *d_plans, *d_state, *d_pairs, *d_off, *d_len, *d_miss, *d_task;
+    void *d_in, *d_io, *d_plans, *d_state, *d_pairs, *d_off, *d_len, *d_miss, *d_task, *d_emit, *d_ticket;
     if ((rc = ws_get(c, "resp_in", in_b, &d_in))) return rc;
+    if ((rc = ws_get(c, "emitted_n", std::max<size_t>(R, 1) * 8, &d_emit))) return rc;
+    bool fresh = false;
+    if ((rc = ws_get(c, "ticket", 64, &d_ticket, &fresh))) return rc;
+    if (fresh) HIP_TRY(hipMemsetAsync(d_ticket, 0, 64, c->stream));
     if ((rc = ws_get(c, "resp_io", io_b, &d_io))) return rc;
     if ((rc = ws_get(c, "plans", std::max<size_t>((size_t)R * J, 1) * sizeof(Plan), &d_plans))) return rc;
     if ((rc = ws_get(c, "state", std::max<size_t>(R, 1) * sizeof(ReqState), &d_state))) return rc;
@@ -773,8 +778,6 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
         for (auto& fa : fam_active)
             for (uint32_t r : fa) h_act0[a++] = r;
     }
-    HIP_TRY(hipMemcpyAsync(d_in, h_in, in_b, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemsetAsync(d_io, 0, io_b, c->stream));
     uint8_t* io = (uint8_t*)d_io;
 
     RespondLaunch L{};
@@ -800,6 +803,8 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     L.plans = (Plan*)d_plans;
     L.state = (ReqState*)d_state;
     L.upper = (uint64_t*)(io + head_b + act_done_b);
+    L.emitted_n = (uint64_t*)d_emit;
+    L.ticket = (uint32_t*)d_ticket;
     L.pair_row = (uint64_t*)d_pairs;
     L.pair_off = (uint64_t*)d_off;
     L.pair_len = (uint32_t*)d_len;
@@ -809,21 +814,23 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     L.counters = (uint64_t*)io;
     L.stream = c->stream;
 
-    PendingTimer t;
-    timer_begin(c, &t, kTimeSelect);
-    HIP_TRY(launch_plan(L));
-    timer_end(c, &t);
     // ---- per-claim output capacity: every emitted packet but the last costs >= min_len bytes of budget, so a
     // claim sends at most byte_limit / min_len + 2 packets.  When that bound is small the capacities and output
     // bases are computed on the device (no host round-trip); otherwise from the plan's row counts on the host.
+    // k_setup reads the staged claims straight from pinned host memory (its copy to d_in is what later kernels
+    // read) and zeroes the status counters: no copy-engine or fill dispatch ahead of it.
     void* d_out;
     uint64_t cap_total = 0;
     const uint64_t per_claim = byte_limit <= 0 ? 1 : (s->min_len > 0 ? (uint64_t)byte_limit / s->min_len + 2 : ~0ull);
-    if (per_claim != ~0ull && per_claim <= (1ull << 26) / std::max<uint32_t>(R, 1)) {
+    const bool dev_caps = per_claim != ~0ull && per_claim <= (1ull << 26) / std::max<uint32_t>(R, 1);
+    PendingTimer t;
+    timer_begin(c, &t, kTimeSelect);
+    HIP_TRY(launch_setup(L, h_in, d_in, in_b, d_io, head_b, dev_caps ? per_claim : 0));
+    timer_end(c, &t);
+    if (dev_caps) {
         cap_total = per_claim * R;
         if ((rc = ws_get(c, "out", std::max<uint64_t>(cap_total, 1) * 8, &d_out))) return rc;
         L.out = (uint64_t*)d_out;
-        HIP_TRY(launch_caps(L, per_claim));
     } else {
         std::vector<uint64_t> upper(R);
         if (R) HIP_TRY(hipMemcpyAsync(upper.data(), L.upper, (size_t)R * 8, hipMemcpyDeviceToHost, c->stream));

@@ -137,6 +137,8 @@ struct RespondLaunch {
     Plan* plans;              // device [R*J]
     ReqState* state;          // device [R]
     uint64_t* upper;          // device [R]: upper bound of selected rows per claim
+    uint64_t* emitted_n;      // device [R]: state[r].emitted, compact (written by k_compact, read by k_pack)
+    uint32_t* ticket;         // device: k_setup's last-workgroup counter (zero between calls)
     uint64_t* pair_row;       // device [pool]: store row of window slot t
     uint64_t* pair_off;       // device [pool]: its packet's blob offset
     uint32_t* pair_len;       // device [pool]: its packet's length
@@ -150,12 +152,15 @@ struct RespondLaunch {
     hipStream_t stream;
 };
 
-hipError_t launch_plan(const RespondLaunch& L);
+// copy the staged claims (pinned host h_src -> d_dst), zero d_zero, plans, upper bounds, and (per_claim_cap != 0)
+// the per-claim capacities and states
+hipError_t launch_setup(const RespondLaunch& L, const void* h_src, void* d_dst, size_t in_bytes, void* d_zero,
+                        size_t zero_bytes, uint64_t per_claim_cap);
+static constexpr uint32_t kPackFusedMax = 8192;  // claims packed by one launch (k_pack_fused)
 hipError_t launch_fill(const RespondLaunch& L);
 // hash + test the window's pairs of the listed window slots, all of one (hash kind, chunk) family
 hipError_t launch_pair_test_list(const RespondLaunch& L, int kind, uint32_t chunk, const uint32_t* d_list, uint32_t n);
 hipError_t launch_compact(const RespondLaunch& L);
-hipError_t launch_caps(const RespondLaunch& L, uint64_t per_claim_cap);
 hipError_t launch_pack(const RespondLaunch& L, uint64_t* packed, uint64_t* packed_offsets, uint64_t* d_scan_tmp);
 
 // ---------------------------------------------------------------------------------------- simulator

@@ -8,16 +8,20 @@
 // ranges (a filter that covers everything, a global time shared by 10^5 rows) take big windows instead of
 // hundreds of small ones.
 //
-//   k_plan        one lane per (claim, meta): binary-search the live-row span of [time_low', time_high] in the
-//                 meta's global_time-sorted segment; choose scan (every row) or enumerate (every global time
-//                 g = g0 + i*modulo, each found by binary search) by which touches fewer bytes.
+//   k_setup       copies the call's staged claims from pinned host memory to the device and zeroes the status
+//                 counters (no copy-engine or fill dispatch), then one lane per (claim, meta): binary-search the
+//                 live-row span of [time_low', time_high] in the meta's global_time-sorted segment; choose scan
+//                 (every row) or enumerate (every global time g = g0 + i*modulo, each found by binary search) by
+//                 which touches fewer bytes.  The last workgroup to finish sums the per-claim spans and, when
+//                 the output bound is small, scans the per-claim capacities (no separate launch).
 //   k_fill        one 256-lane workgroup per claim: the next <= W rows in send order (ASC / DESC / Feistel-
 //                 permuted RANDOM), block prefix-sum placement, resumable (meta, candidate, sub-row) cursor.
 //   k_pair_test   one lane per pair, a wave per 64 pairs of one claim (filter/prefix/m/k wave-uniform): digest
 //                 of prefix || packet, k probes -> missing flag.
 //   k_compact     one wave per claim: ballot + prefix-sum compaction of missing pairs in send order with the
 //                 byte-limit rule of community.py:2559-2567 (the crossing packet is sent).
-//   k_pack        exclusive scan of per-claim counts and a copy into the packed output.
+//   k_pack        exclusive scan of per-claim counts and a copy into the packed output (one launch for up to
+//                 kPackFusedMax claims: each workgroup sums the counts before its claim itself).
 #include "dsy_kernels.h"
 
 namespace dsy {
@@ -85,12 +89,8 @@ __device__ __forceinline__ uint64_t permute(uint64_t x, uint64_t n, uint32_t bit
     return x;
 }
 
-__global__ void k_plan(RespondLaunch L) {
-    const uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= L.R * L.J) return;
-    const uint32_t r = idx / L.J, j = idx % L.J;
-    const DevRequest& q = L.reqs[r];
-    const SegMeta& mt = L.metas[j];
+__device__ __forceinline__ void plan_one(const RespondLaunch& L, const DevRequest& q, const SegMeta& mt, uint32_t idx,
+                                         uint32_t r, uint32_t j) {
     uint64_t lo = q.time_low, hi = q.time_high;
     if (!L.include_inactive && mt.has_pruning) {
         // time_low' = min(max(time_low, global_time - inactive + 1), 2^63-1)   (community.py:2806)
@@ -136,7 +136,81 @@ __global__ void k_plan(RespondLaunch L) {
         p.perm_key = (uint64_t)mix32(L.seed ^ ((uint64_t)r << 32) ^ j) << 32 | mix32(L.seed * 31 + r * 131 + j);
     }
     L.plans[idx] = p;
-    atomicAdd((unsigned long long*)&L.upper[r], (unsigned long long)span);
+}
+
+__device__ __forceinline__ uint64_t block_sum_256(uint64_t v, uint64_t* lds4) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    if (lane == 0) lds4[wv] = v;
+    __syncthreads();
+    const uint64_t t = lds4[0] + lds4[1] + lds4[2] + lds4[3];
+    __syncthreads();
+    return t;
+}
+
+// src: the staged upload region in pinned host memory ([DevRequest R | SegMeta J | ...], respond_core's layout),
+// copied to dst (= L.reqs) in 16-byte words; zero: the status counters.  per_claim_cap == 0: upper bounds only
+// (the host derives the capacities).
+__global__ void __launch_bounds__(256) k_setup(RespondLaunch L, const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                               uint32_t in_words, uint4* __restrict__ zero, uint32_t zero_words,
+                                               uint64_t per_claim_cap) {
+    __shared__ uint64_t red[4];
+    __shared__ uint32_t last;
+    const uint32_t tid = blockIdx.x * 256 + threadIdx.x, nthr = gridDim.x * 256;
+    for (uint32_t i = tid; i < in_words; i += nthr) dst[i] = src[i];
+    for (uint32_t i = tid; i < zero_words; i += nthr) zero[i] = make_uint4(0, 0, 0, 0);
+    if (tid < L.R * L.J) {
+        const uint32_t r = tid / L.J, j = tid % L.J;
+        const DevRequest* hq = (const DevRequest*)src;
+        const SegMeta* hm = (const SegMeta*)((const uint8_t*)src + (size_t)L.R * sizeof(DevRequest));
+        plan_one(L, hq[r], hm[j], tid, r, j);
+    }
+    // the last workgroup to finish: upper[r] = sum of the claim's spans, then the capacities
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(L.ticket, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    const uint32_t per = (L.R + 255) / 256;  // thread t owns claims [t*per, t*per + per)
+    uint64_t sum = 0;
+    for (uint32_t i = 0; i < per; ++i) {
+        const uint32_t r = threadIdx.x * per + i;
+        if (r >= L.R) break;
+        uint64_t u = 0;
+        for (uint32_t j = 0; j < L.J; ++j) {
+            const Plan& p = L.plans[(size_t)r * L.J + j];
+            u += p.b - p.a;
+        }
+        L.upper[r] = u;
+        sum += min(u, per_claim_cap);
+    }
+    if (per_claim_cap) {
+        // exclusive scan of the capacities over the owners (wave scan + one LDS round)
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        uint64_t incl = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t o = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += o;
+        }
+        if (lane == 63) red[wv] = incl;
+        __syncthreads();
+        uint64_t run = incl - sum;
+        for (int w = 0; w < wv; ++w) run += red[w];
+        for (uint32_t i = 0; i < per; ++i) {
+            const uint32_t r = threadIdx.x * per + i;
+            if (r >= L.R) break;
+            ReqState st{};
+            st.cap = min(L.upper[r], per_claim_cap);
+            st.out_base = run;
+            st.done = L.upper[r] == 0;
+            L.state[r] = st;
+            run += st.cap;
+        }
+    }
+    if (threadIdx.x == 0) *L.ticket = 0;  // ready for the next call
 }
 
 // ------------------------------------------------------------------------------------------- k_fill
@@ -585,7 +659,10 @@ __global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
     const uint32_t r = L.act[a_slot];
     ReqState* S = &L.state[r];
     if (S->done) {
-        if (threadIdx.x == 0) L.act_done[a_slot] = 1;
+        if (threadIdx.x == 0) {
+            L.act_done[a_slot] = 1;
+            L.emitted_n[r] = S->emitted;
+        }
         return;
     }
     const uint64_t W = L.window;
@@ -648,6 +725,7 @@ __global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
     overflow = __any(overflow) ? 1u : 0u;
     if (lane == 0) {
         S->emitted = emitted;
+        L.emitted_n[r] = emitted;
         S->spent = spent;
         S->overflow = overflow;
         if (overflow) L.flags[1] = 1;
@@ -688,44 +766,6 @@ __global__ void __launch_bounds__(1024) k_scan_counts(RespondLaunch L, uint64_t*
     if (t == 1023) packed_offsets[L.R] = part[1023];
 }
 
-// Per-claim output capacity and state, on the device (no host round-trip): cap = min(upper bound of selected
-// rows, per_claim_cap), out_base = exclusive scan of cap.  Single workgroup.
-__global__ void __launch_bounds__(1024) k_caps(RespondLaunch L, uint64_t per_claim_cap) {
-    __shared__ uint64_t part[1024];
-    const uint32_t t = threadIdx.x;
-    const uint32_t per = (L.R + 1023) / 1024;
-    uint64_t sum = 0;
-    for (uint32_t i = 0; i < per; ++i) {
-        const uint32_t r = t * per + i;
-        if (r < L.R) sum += min(L.upper[r], per_claim_cap);
-    }
-    part[t] = sum;
-    __syncthreads();
-    for (int d = 1; d < 1024; d <<= 1) {
-        const uint64_t add = t >= (uint32_t)d ? part[t - d] : 0;
-        __syncthreads();
-        part[t] += add;
-        __syncthreads();
-    }
-    uint64_t run = part[t] - sum;
-    for (uint32_t i = 0; i < per; ++i) {
-        const uint32_t r = t * per + i;
-        if (r < L.R) {
-            ReqState st{};
-            st.cap = min(L.upper[r], per_claim_cap);
-            st.out_base = run;
-            st.done = L.upper[r] == 0;
-            L.state[r] = st;
-            run += st.cap;
-        }
-    }
-}
-
-hipError_t launch_caps(const RespondLaunch& L, uint64_t per_claim_cap) {
-    hipLaunchKernelGGL(k_caps, dim3(1), dim3(1024), 0, L.stream, L, per_claim_cap);
-    return hipGetLastError();
-}
-
 __global__ void __launch_bounds__(256) k_copy_out(RespondLaunch L, const uint64_t* packed_offsets, uint64_t* packed) {
     const uint32_t r = blockIdx.x;
     const ReqState& S = L.state[r];
@@ -733,10 +773,31 @@ __global__ void __launch_bounds__(256) k_copy_out(RespondLaunch L, const uint64_
     for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) packed[packed_offsets[r] + i] = L.out[S.out_base + i];
 }
 
-hipError_t launch_plan(const RespondLaunch& L) {
-    const uint32_t n = L.R * L.J;
-    if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_plan, dim3((n + 255) / 256), dim3(256), 0, L.stream, L);
+// one workgroup per claim: its output offset is the sum of the counts before it (read from the compact emitted_n
+// array: R * 8 bytes per workgroup at most), then its rows are copied
+__global__ void __launch_bounds__(256) k_pack_fused(RespondLaunch L, uint64_t* packed_offsets, uint64_t* packed) {
+    __shared__ uint64_t red[4];
+    const uint32_t r = blockIdx.x;
+    uint64_t s = 0;
+    for (uint32_t i = threadIdx.x; i < r; i += 256) s += L.emitted_n[i];
+    const uint64_t off = block_sum_256(s, red);
+    const ReqState& S = L.state[r];
+    const uint64_t n = S.emitted < S.cap ? S.emitted : S.cap;
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) packed[off + i] = L.out[S.out_base + i];
+    if (threadIdx.x == 0) {
+        packed_offsets[r] = off;
+        if (r + 1 == L.R) packed_offsets[L.R] = off + S.emitted;
+    }
+}
+
+hipError_t launch_setup(const RespondLaunch& L, const void* h_src, void* d_dst, size_t in_bytes, void* d_zero,
+                        size_t zero_bytes, uint64_t per_claim_cap) {
+    const uint32_t in_words = (uint32_t)(in_bytes / 16), zero_words = (uint32_t)(zero_bytes / 16);
+    // one 16-byte word per lane where possible: the host reads are PCIe round trips
+    const uint64_t lanes = std::max<uint64_t>(std::max<uint64_t>((uint64_t)L.R * L.J, in_words), 1);
+    const uint32_t blocks = (uint32_t)((lanes + 255) / 256);
+    hipLaunchKernelGGL(k_setup, dim3(blocks), dim3(256), 0, L.stream, L, (const uint4*)h_src, (uint4*)d_dst,
+                       in_words, (uint4*)d_zero, zero_words, per_claim_cap);
     return hipGetLastError();
 }
 
@@ -753,6 +814,10 @@ hipError_t launch_compact(const RespondLaunch& L) {
 }
 
 hipError_t launch_pack(const RespondLaunch& L, uint64_t* packed, uint64_t* packed_offsets, uint64_t*) {
+    if (L.R && L.R <= kPackFusedMax) {
+        hipLaunchKernelGGL(k_pack_fused, dim3(L.R), dim3(256), 0, L.stream, L, packed_offsets, packed);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, L.stream, L, packed_offsets);
     if (L.R) hipLaunchKernelGGL(k_copy_out, dim3(L.R), dim3(256), 0, L.stream, L, packed_offsets, packed);
     return hipGetLastError();
