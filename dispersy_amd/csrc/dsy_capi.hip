@@ -697,15 +697,18 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     }
     const uint64_t pool = kWindow * std::max<uint64_t>(R, kMinSlots);
     // ---- device layout: one upload region [claims | metas | window slots 0..R-1 | first active list] and one
-    // status region [counters kCntSpread x 64 B | flags 64 B | act_done R B | upper R x u64] zeroed once, read
-    // back (up to act_done) per window
+    // device status region [counters kCntSpread x 64 B | flags 64 B | upper R x u64] (counters and flags zeroed by
+    // k_setup); host-mapped status [totals kCntN x u64 | overflow | act_done R B]: k_compact writes the done flags
+    // and the overflow flag over the bus and the pack kernel folds the counters, so a window's status needs no
+    // copy dispatch
     size_t prefix_b = 0;
     for (uint32_t r = 0; r < R; ++r) prefix_b += reqs[r].prefix_len;
     const size_t reqs_b = (size_t)R * sizeof(DevRequest), metas_b = (size_t)J * sizeof(SegMeta);
     const size_t in_b = (reqs_b + metas_b + (size_t)R * 8 + (prefix_b + 15) / 16 * 16 + 64 + 15) / 16 * 16;
     const size_t act_done_b = ((size_t)R + 15) / 16 * 16;
     const size_t cnt_b = kCntSpread * kCntN * 8, head_b = cnt_b + 64;
-    const size_t io_b = head_b + act_done_b + (size_t)R * 8;
+    const size_t io_b = head_b + (size_t)R * 8;
+    constexpr size_t kHostHead = 128;
     int rc;
     void *d_in, *d_io, *d_plans, *d_state, *d_pairs, *d_off, *d_len, *d_miss, *d_task, *d_emit, *d_ticket;
     if ((rc = ws_get(c, "resp_in", in_b, &d_in))) return rc;
@@ -722,9 +725,9 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     if ((rc = ws_get(c, "miss", pool, &d_miss))) return rc;
     if ((rc = ws_get(c, "task", pool * sizeof(PairTask), &d_task))) return rc;
     uint8_t* h_in;
-    if ((rc = stage_get(c, in_b + io_b, &h_in))) return rc;
-    uint8_t* h_io = h_in + in_b;  // the status region's host mirror
-    std::memset(h_io, 0, head_b);  // counters stay zero if no window runs (R == 0)
+    if ((rc = stage_get(c, in_b + kHostHead + act_done_b, &h_in))) return rc;
+    uint8_t* h_io = h_in + in_b;  // host-mapped status
+    std::memset(h_io, 0, kHostHead);  // totals stay zero if no window runs (R == 0)
     {
         DevRequest* dq = (DevRequest*)h_in;
         uint8_t* h_pre = h_in + reqs_b + metas_b + (size_t)R * 8;
@@ -799,10 +802,11 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     L.seed = seed;
     L.window = kWindow;
     L.act = d_act;
-    L.act_done = io + head_b;
+    L.act_done = h_io + kHostHead;
+    L.h_status = (uint64_t*)h_io;
     L.plans = (Plan*)d_plans;
     L.state = (ReqState*)d_state;
-    L.upper = (uint64_t*)(io + head_b + act_done_b);
+    L.upper = (uint64_t*)(io + head_b);
     L.emitted_n = (uint64_t*)d_emit;
     L.ticket = (uint32_t*)d_ticket;
     L.pair_row = (uint64_t*)d_pairs;
@@ -917,14 +921,13 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
         timer_begin(c, &t, kTimeCompact);
         HIP_TRY(launch_compact(L));
         timer_end(c, &t);
-        HIP_TRY(hipMemcpyAsync(h_io, d_io, head_b + n_act, hipMemcpyDeviceToHost, c->stream));
         // speculatively pack the output now (it is redone if another window follows): the GPU packs while the
         // host wakes up and reads the status
         HIP_TRY(launch_pack(L, (uint64_t*)d_packed_v, (uint64_t*)d_packed_off_v, nullptr));
         HIP_TRY(hipStreamSynchronize(c->stream));
         // capacity overflow can only come from a wrong min_len bound; report it loudly
-        if (((uint32_t*)(h_io + cnt_b))[1]) return fail(DSY_ECAPACITY, "internal: a claim overflowed its output capacity");
-        const uint8_t* done = h_io + head_b;
+        if (((const volatile uint64_t*)h_io)[kCntN]) return fail(DSY_ECAPACITY, "internal: a claim overflowed its output capacity");
+        const volatile uint8_t* done = h_io + kHostHead;
         size_t a = 0;
         for (auto& fa : fam_active) {
             size_t keep = 0;
@@ -933,9 +936,8 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
             fa.resize(keep);
         }
     }
-    uint64_t h_tot[kCntN] = {0};
-    for (uint32_t i = 0; i < kCntSpread; ++i)
-        for (uint32_t k = 0; k < kCntN; ++k) h_tot[k] += ((const uint64_t*)h_io)[i * kCntN + k];
+    uint64_t h_tot[kCntN];
+    for (uint32_t k = 0; k < kCntN; ++k) h_tot[k] = ((const volatile uint64_t*)h_io)[k];
     if (!ran) HIP_TRY(launch_pack(L, (uint64_t*)d_packed_v, (uint64_t*)d_packed_off_v, nullptr));
     timers_collect_lazy(c);
     c->blocks[kTimePairTest] += h_tot[kCntBlocks];

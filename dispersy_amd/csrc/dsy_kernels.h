@@ -133,7 +133,9 @@ struct RespondLaunch {
     uint64_t window;          // W pairs per claim in this window
     const uint32_t* act;      // device [n_act]: window slot a serves claim act[a]
     uint32_t n_act;
-    uint8_t* act_done;        // device [n_act]: written by k_compact, 1 once claim act[a] is done
+    uint8_t* act_done;        // host-mapped [n_act]: written by k_compact, 1 once claim act[a] is done
+    uint64_t* h_status;       // host-mapped [kCntN + 1]: counter totals (folded by the pack kernels) and the
+                              // overflow flag (k_compact)
     Plan* plans;              // device [R*J]
     ReqState* state;          // device [R]
     uint64_t* upper;          // device [R]: upper bound of selected rows per claim

@@ -155,7 +155,7 @@ __device__ __forceinline__ void hash_key_short_prefix(const KeyView& kv, H& st) 
             if (H::big_endian) {
                 w[NW - 2] = (uint32_t)(bits >> 32);
                 w[NW - 1] = (uint32_t)bits;
-                if (NW == 32) { w[28] = 0; w[29] = 0; }
+                if constexpr (NW == 32) { w[28] = 0; w[29] = 0; }
             } else {
                 w[14] = (uint32_t)bits;
                 w[15] = (uint32_t)(bits >> 32);

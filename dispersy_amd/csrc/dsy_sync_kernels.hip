@@ -162,9 +162,20 @@ __global__ void __launch_bounds__(256) k_setup(RespondLaunch L, const uint4* __r
     for (uint32_t i = tid; i < zero_words; i += nthr) zero[i] = make_uint4(0, 0, 0, 0);
     if (tid < L.R * L.J) {
         const uint32_t r = tid / L.J, j = tid % L.J;
-        const DevRequest* hq = (const DevRequest*)src;
-        const SegMeta* hm = (const SegMeta*)((const uint8_t*)src + (size_t)L.R * sizeof(DevRequest));
-        plan_one(L, hq[r], hm[j], tid, r, j);
+        // whole-struct loads issued together: each host read is a PCIe round trip
+        static_assert(sizeof(DevRequest) % 16 == 0 && sizeof(SegMeta) % 16 == 0, "16-byte staged records");
+        const uint4* hq = src + (size_t)r * (sizeof(DevRequest) / 16);
+        const uint4* hm = src + (size_t)L.R * (sizeof(DevRequest) / 16) + (size_t)j * (sizeof(SegMeta) / 16);
+        uint4 qw[sizeof(DevRequest) / 16], mw[sizeof(SegMeta) / 16];
+#pragma unroll
+        for (int i = 0; i < (int)(sizeof(DevRequest) / 16); ++i) qw[i] = hq[i];
+#pragma unroll
+        for (int i = 0; i < (int)(sizeof(SegMeta) / 16); ++i) mw[i] = hm[i];
+        DevRequest q;
+        SegMeta mt;
+        __builtin_memcpy(&q, qw, sizeof q);
+        __builtin_memcpy(&mt, mw, sizeof mt);
+        plan_one(L, q, mt, tid, r, j);
     }
     // the last workgroup to finish: upper[r] = sum of the claim's spans, then the capacities
     __threadfence();
@@ -654,6 +665,21 @@ __device__ __forceinline__ int64_t wave_inclusive_scan(int64_t v) {
     return v;
 }
 
+// Fold the kCntSpread counter copies into the host-mapped status (wave 0 of the calling workgroup).  Called by
+// the pack kernels, which run after the window's k_compact: the kernel boundary orders the counters' atomics.
+__device__ __forceinline__ void fold_status(const RespondLaunch& L) {
+    if (threadIdx.x >= 64) return;
+    const uint32_t lane = threadIdx.x;
+    static_assert(kCntSpread == 64, "one lane per counter copy");
+#pragma unroll
+    for (int k = 0; k < kCntN; ++k) {
+        uint64_t v = L.counters[lane * kCntN + k];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+        if (lane == 0) L.h_status[k] = v;
+    }
+}
+
 __global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
     const uint32_t a_slot = blockIdx.x;
     const uint32_t r = L.act[a_slot];
@@ -728,7 +754,7 @@ __global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
         L.emitted_n[r] = emitted;
         S->spent = spent;
         S->overflow = overflow;
-        if (overflow) L.flags[1] = 1;
+        if (overflow) L.h_status[kCntN] = 1;  // host-mapped: read after the window's sync
         if (done || S->exhausted) S->done = 1;
         L.act_done[a_slot] = (uint8_t)S->done;
         atomicAdd(counter(L.counters, kCntPairs), (unsigned long long)n);
@@ -764,6 +790,7 @@ __global__ void __launch_bounds__(1024) k_scan_counts(RespondLaunch L, uint64_t*
         }
     }
     if (t == 1023) packed_offsets[L.R] = part[1023];
+    fold_status(L);
 }
 
 __global__ void __launch_bounds__(256) k_copy_out(RespondLaunch L, const uint64_t* packed_offsets, uint64_t* packed) {
@@ -788,6 +815,7 @@ __global__ void __launch_bounds__(256) k_pack_fused(RespondLaunch L, uint64_t* p
         packed_offsets[r] = off;
         if (r + 1 == L.R) packed_offsets[L.R] = off + S.emitted;
     }
+    if (r == 0) fold_status(L);
 }
 
 hipError_t launch_setup(const RespondLaunch& L, const void* h_src, void* d_dst, size_t in_bytes, void* d_zero,
