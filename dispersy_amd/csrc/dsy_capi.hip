@@ -722,7 +722,7 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     if ((rc = ws_get(c, "pairs", pool * 8, &d_pairs))) return rc;
     if ((rc = ws_get(c, "pair_off", pool * 8, &d_off))) return rc;
     if ((rc = ws_get(c, "pair_len", pool * 4, &d_len))) return rc;
-    if ((rc = ws_get(c, "miss", pool, &d_miss))) return rc;
+    if ((rc = ws_get(c, "miss_mask", pool / 8 + 64, &d_miss))) return rc;
     if ((rc = ws_get(c, "task", pool * sizeof(PairTask), &d_task))) return rc;
     uint8_t* h_in;
     if ((rc = stage_get(c, in_b + kHostHead + act_done_b, &h_in))) return rc;
@@ -812,7 +812,7 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     L.pair_row = (uint64_t*)d_pairs;
     L.pair_off = (uint64_t*)d_off;
     L.pair_len = (uint32_t*)d_len;
-    L.miss = (uint8_t*)d_miss;
+    L.miss_mask = (uint64_t*)d_miss;
     L.task = (PairTask*)d_task;
     L.flags = (uint32_t*)(io + cnt_b);
     L.counters = (uint64_t*)io;

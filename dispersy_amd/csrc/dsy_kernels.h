@@ -145,7 +145,7 @@ struct RespondLaunch {
     uint64_t* pair_off;       // device [pool]: its packet's blob offset
     uint32_t* pair_len;       // device [pool]: its packet's length
     PairTask* task;           // device [R*W]: per-claim hashing order (window slots sorted by block count)
-    uint8_t* miss;            // device [R*W]
+    uint64_t* miss_mask;      // device [n_act * W / 64]: bit t of claim slot a = window pair t is missing
     uint64_t* out;            // device [sum cap]
     uint32_t* flags;          // device [4]: [1] an output capacity overflowed
     uint64_t* fill_clock;     // optional [n_act][4] s_memtime stamps of k_fill phases (DSY_FILL_PROFILE)

@@ -89,8 +89,8 @@ __device__ __forceinline__ uint64_t permute(uint64_t x, uint64_t n, uint32_t bit
     return x;
 }
 
-__device__ __forceinline__ void plan_one(const RespondLaunch& L, const DevRequest& q, const SegMeta& mt, uint32_t idx,
-                                         uint32_t r, uint32_t j) {
+__device__ __forceinline__ uint64_t plan_one(const RespondLaunch& L, const DevRequest& q, const SegMeta& mt,
+                                             uint32_t idx, uint32_t r, uint32_t j) {
     uint64_t lo = q.time_low, hi = q.time_high;
     if (!L.include_inactive && mt.has_pruning) {
         // time_low' = min(max(time_low, global_time - inactive + 1), 2^63-1)   (community.py:2806)
@@ -136,6 +136,7 @@ __device__ __forceinline__ void plan_one(const RespondLaunch& L, const DevReques
         p.perm_key = (uint64_t)mix32(L.seed ^ ((uint64_t)r << 32) ^ j) << 32 | mix32(L.seed * 31 + r * 131 + j);
     }
     L.plans[idx] = p;
+    return span;
 }
 
 __device__ __forceinline__ uint64_t block_sum_256(uint64_t v, uint64_t* lds4) {
@@ -158,25 +159,41 @@ __global__ void __launch_bounds__(256) k_setup(RespondLaunch L, const uint4* __r
     __shared__ uint64_t red[4];
     __shared__ uint32_t last;
     const uint32_t tid = blockIdx.x * 256 + threadIdx.x, nthr = gridDim.x * 256;
-    for (uint32_t i = tid; i < in_words; i += nthr) dst[i] = src[i];
-    for (uint32_t i = tid; i < zero_words; i += nthr) zero[i] = make_uint4(0, 0, 0, 0);
-    if (tid < L.R * L.J) {
-        const uint32_t r = tid / L.J, j = tid % L.J;
-        // whole-struct loads issued together: each host read is a PCIe round trip
-        static_assert(sizeof(DevRequest) % 16 == 0 && sizeof(SegMeta) % 16 == 0, "16-byte staged records");
-        const uint4* hq = src + (size_t)r * (sizeof(DevRequest) / 16);
-        const uint4* hm = src + (size_t)L.R * (sizeof(DevRequest) / 16) + (size_t)j * (sizeof(SegMeta) / 16);
-        uint4 qw[sizeof(DevRequest) / 16], mw[sizeof(SegMeta) / 16];
+    const bool planner = tid < L.R * L.J;
+    const uint32_t r = planner ? tid / L.J : 0, j = planner ? tid % L.J : 0;
+    // every host read of the thread is issued before the first wait: each is a PCIe round trip
+    static_assert(sizeof(DevRequest) % 16 == 0 && sizeof(SegMeta) % 16 == 0, "16-byte staged records");
+    const uint4* hq = src + (size_t)r * (sizeof(DevRequest) / 16);
+    const uint4* hm = src + (size_t)L.R * (sizeof(DevRequest) / 16) + (size_t)j * (sizeof(SegMeta) / 16);
+    uint4 qw[sizeof(DevRequest) / 16], mw[sizeof(SegMeta) / 16], cw = make_uint4(0, 0, 0, 0);
+    if (planner) {
 #pragma unroll
         for (int i = 0; i < (int)(sizeof(DevRequest) / 16); ++i) qw[i] = hq[i];
 #pragma unroll
         for (int i = 0; i < (int)(sizeof(SegMeta) / 16); ++i) mw[i] = hm[i];
+    }
+    if (tid < in_words) cw = src[tid];
+    if (tid < in_words) dst[tid] = cw;
+    for (uint32_t i = tid + nthr; i < in_words; i += nthr) dst[i] = src[i];
+    for (uint32_t i = tid; i < zero_words; i += nthr) zero[i] = make_uint4(0, 0, 0, 0);
+    if (planner) {
         DevRequest q;
         SegMeta mt;
         __builtin_memcpy(&q, qw, sizeof q);
         __builtin_memcpy(&mt, mw, sizeof mt);
-        plan_one(L, q, mt, tid, r, j);
+        const uint64_t span = plan_one(L, q, mt, tid, r, j);
+        if (L.J == 1 && per_claim_cap) {
+            // one meta: the claim's bound is its span; output slots at r * per_claim_cap (the buffer holds
+            // R * per_claim_cap rows), so no scan is needed
+            L.upper[r] = span;
+            ReqState st{};
+            st.cap = min(span, per_claim_cap);
+            st.out_base = (uint64_t)r * per_claim_cap;
+            st.done = span == 0;
+            L.state[r] = st;
+        }
     }
+    if (L.J == 1 && per_claim_cap) return;
     // the last workgroup to finish: upper[r] = sum of the claim's spans, then the capacities
     __threadfence();
     __syncthreads();
@@ -294,6 +311,8 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
     }
     const DevRequest& q = L.reqs[r];
     const uint64_t W = L.window;
+    // this window's missing-pair bits of the claim start clear (k_pair_test sets them)
+    for (uint64_t w = threadIdx.x; w < W / 64; w += kFillThreads) L.miss_mask[(uint64_t)a_slot * (W / 64) + w] = 0;
     uint64_t* out = L.pair_row + (uint64_t)a_slot * W;
     uint64_t* out_off = L.pair_off + (uint64_t)a_slot * W;
     uint32_t* out_len = L.pair_len + (uint64_t)a_slot * W;
@@ -586,7 +605,8 @@ __global__ void __launch_bounds__(256) k_pair_test(RespondLaunch L, const uint32
         }
         const uint32_t nb = active ? n_blocks(kv.plen + kv.len, H::block_bytes, H::len_bytes) : 0u;
         if (active) {
-            L.miss[(uint64_t)a_slot * W + t] = (uint8_t)(ok ^ 1u);
+            // misses are rare (the requester holds most of its range): one atomic bit per missing pair
+            if (!ok) atomicOr((unsigned long long*)&L.miss_mask[(uint64_t)a_slot * (W / 64) + t / 64], 1ull << (t % 64));
             acc_blocks += nb;
             acc_bytes += kv.len;
         }
@@ -680,6 +700,25 @@ __device__ __forceinline__ void fold_status(const RespondLaunch& L) {
     }
 }
 
+// position of the k-th set bit of w (k < popcount(w))
+__device__ __forceinline__ uint32_t select_bit(uint64_t w, uint32_t k) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (int h = 32; h >= 1; h >>= 1) {
+        const uint32_t c = __popcll(w & ((1ull << h) - 1));
+        if (k >= c) {
+            k -= c;
+            w >>= h;
+            pos += h;
+        }
+    }
+    return pos;
+}
+
+// One wave per claim.  The window's missing pairs are the set bits of the claim's miss_mask words (bit t: window
+// slot t, i.e. send order); each round loads 256 words (16 K slots), ranks their set bits, and takes the misses in
+// batches of 64: lane i fetches the i-th miss's length and row, a prefix sum applies the byte-limit rule of
+// community.py:2559-2567 (send while the budget before the packet is positive; the crossing packet is sent).
 __global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
     const uint32_t a_slot = blockIdx.x;
     const uint32_t r = L.act[a_slot];
@@ -699,52 +738,95 @@ __global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
     uint32_t done = 0, overflow = S->overflow;
     uint64_t useful = n;  // pairs the reference hashes in this window: up to the packet that spends the budget
     const int64_t limit = L.byte_limit;
-    const uint8_t* miss_w = L.miss + (uint64_t)a_slot * W;
+    const uint64_t cap = S->cap, out_base = S->out_base;
+    const uint64_t* mask_w = L.miss_mask + (uint64_t)a_slot * (W / 64);
     const uint32_t* len_w = L.pair_len + (uint64_t)a_slot * W;
     const uint64_t* row_w = L.pair_row + (uint64_t)a_slot * W;
-    // groups of 4 chunks: their flags and lengths are fetched together (one memory round-trip per 256 pairs
-    // instead of one per 64), then the chunks are compacted in order
-    constexpr int kGroup = 4;
-    for (uint64_t g0 = 0; g0 < n && !done; g0 += 64 * kGroup) {
-        uint32_t lens[kGroup];
+    const uint64_t nw = (n + 63) / 64;
+    constexpr uint32_t kPer = 4;  // words per lane per round
+    for (uint64_t wb = 0; wb < nw && !done; wb += 64 * kPer) {
+        uint64_t w[kPer];
+        uint32_t c[kPer], cnt = 0;
 #pragma unroll
-        for (int u = 0; u < kGroup; ++u) {
-            const uint64_t t = g0 + 64 * u + lane;
-            lens[u] = (t < n && miss_w[t]) ? len_w[t] : 0u;
+        for (uint32_t u = 0; u < kPer; ++u) {
+            const uint64_t x = wb + kPer * lane + u;
+            w[u] = x < nw ? mask_w[x] : 0ull;
         }
 #pragma unroll
-        for (int u = 0; u < kGroup; ++u) {
-            const uint64_t t0 = g0 + 64 * u;
-            if (done || t0 >= n) break;
-            const uint64_t t = t0 + lane;
-            const bool miss = t < n && miss_w[t];
-            const int64_t len = miss ? (int64_t)lens[u] : 0;
-            const int64_t incl = wave_inclusive_scan(len);
-            const int64_t excl = incl - len;
-            const uint64_t mmask = __ballot(miss);
-            const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-            const uint32_t rank = __popcll(mmask & lt);
+        for (uint32_t u = 0; u < kPer; ++u) {
+            c[u] = __popcll(w[u]);
+            cnt += c[u];
+        }
+        uint32_t incl = cnt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(incl, d, 64);
+            if ((int)lane >= d) incl += o;
+        }
+        const uint32_t pos = incl - cnt;                  // misses before this lane's words
+        const uint32_t total = __shfl(incl, 63, 64);      // misses in this round
+        for (uint32_t kb = 0; kb < total && !done; kb += 64) {
+            const uint32_t k = kb + lane;
+            const bool miss = k < total;
+            // owner lane: the last lane whose first miss index is <= k (binary search over the monotone pos)
+            uint32_t lo = 0;
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1) {
+                const uint32_t cand = lo + step;
+                const uint32_t pc = (uint32_t)__shfl((int)pos, (int)min(cand, 63u), 64);
+                if (cand < 64 && pc <= k) lo = cand;
+            }
+            uint32_t kk = k - (uint32_t)__shfl((int)pos, (int)lo, 64);
+            uint64_t t = 0;
+            {
+                uint64_t ww[kPer];
+                uint32_t cc[kPer];
+#pragma unroll
+                for (uint32_t u = 0; u < kPer; ++u) {
+                    ww[u] = __shfl(w[u], (int)lo, 64);
+                    cc[u] = (uint32_t)__shfl((int)c[u], (int)lo, 64);
+                }
+                uint32_t u_sel = 0;
+                uint64_t wsel = ww[0];
+#pragma unroll
+                for (uint32_t u = 0; u < kPer - 1; ++u) {
+                    if (u_sel == u && kk >= cc[u]) {
+                        kk -= cc[u];
+                        u_sel = u + 1;
+                        wsel = ww[u + 1];
+                    }
+                }
+                t = (wb + kPer * lo + u_sel) * 64 + (miss ? select_bit(wsel, kk) : 0u);
+            }
+            const int64_t len = miss ? (int64_t)len_w[t] : 0;
+            const uint64_t row = miss ? row_w[t] : 0;
+            int64_t inc_sum = len;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int64_t o = __shfl_up(inc_sum, d, 64);
+                if ((int)lane >= d) inc_sum += o;
+            }
+            const int64_t excl = inc_sum - len;
             // send while the budget before this packet is positive; the first packet is always sent
-            const bool inc = miss && ((emitted + rank == 0) || (spent + excl < limit));
+            const bool inc = miss && ((emitted + lane == 0) || (spent + excl < limit));
             const uint64_t imask = __ballot(inc);
             const uint32_t nin = __popcll(imask);
             if (inc) {
-                const uint64_t slot = emitted + rank;
-                if (slot < S->cap) L.out[S->out_base + slot] = row_w[t];
+                const uint64_t slot = emitted + lane;
+                if (slot < cap) L.out[out_base + slot] = row;
                 else overflow = 1;
             }
-            // bytes of the included prefix = inclusive scan at the last included lane
             int64_t sum_in = 0;
             int last = -1;
             if (nin) {
                 last = 63 - __builtin_clzll(imask);
-                sum_in = __shfl(incl, last, 64);
+                sum_in = __shfl(inc_sum, last, 64);
             }
             emitted += nin;
             spent += sum_in;
             if (emitted > 0 && spent >= limit) {
                 done = 1;
-                useful = t0 + (uint64_t)last + 1;
+                useful = (uint64_t)__shfl((long long)t, last, 64) + 1;
             }
         }
     }
