@@ -342,15 +342,33 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
             const uint64_t avail = cs < it1 ? it1 - cs : 0;
             const uint64_t take = avail < W - filled ? avail : W - filled;
             const uint64_t* __restrict__ offs = L.st.offsets;
-            for (uint64_t i = threadIdx.x; i < take; i += kFillThreads) {
-                const uint64_t ci = cs + i;
-                const uint64_t cd = p.dir == DSY_DESC ? p.ncand - 1 - ci : ci;
-                const uint64_t lr = p.a + (p.mode == 1 ? p.g0 + cd * mod - p.g_lo : cd);
-                const uint64_t row = L.st.live_row ? L.st.live_row[lr] : lr;
-                const uint64_t a0 = offs[row], a1 = offs[row + 1];
-                out[filled + i] = row;
-                out_off[filled + i] = a0;
-                out_len[filled + i] = (uint32_t)(a1 - a0);
+            // kDenseU rows per thread per round, every load of the round issued before the first is consumed
+            constexpr int kDenseU = 8;
+            for (uint64_t i0 = 0; i0 < take; i0 += (uint64_t)kFillThreads * kDenseU) {
+                uint64_t row[kDenseU], a0[kDenseU], a1[kDenseU];
+#pragma unroll
+                for (int u = 0; u < kDenseU; ++u) {
+                    const uint64_t i = i0 + threadIdx.x + (uint64_t)kFillThreads * u;
+                    const uint64_t ci = cs + (i < take ? i : 0);
+                    const uint64_t cd = p.dir == DSY_DESC ? p.ncand - 1 - ci : ci;
+                    const uint64_t lr = p.a + (p.mode == 1 ? p.g0 + cd * mod - p.g_lo : cd);
+                    row[u] = (L.st.live_row && i < take) ? L.st.live_row[lr] : lr;
+                }
+#pragma unroll
+                for (int u = 0; u < kDenseU; ++u) {
+                    const bool in = i0 + threadIdx.x + (uint64_t)kFillThreads * u < take;
+                    a0[u] = in ? offs[row[u]] : 0;
+                    a1[u] = in ? offs[row[u] + 1] : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < kDenseU; ++u) {
+                    const uint64_t i = i0 + threadIdx.x + (uint64_t)kFillThreads * u;
+                    if (i < take) {
+                        out[filled + i] = row[u];
+                        out_off[filled + i] = a0[u];
+                        out_len[filled + i] = (uint32_t)(a1[u] - a0[u]);
+                    }
+                }
             }
             filled += take;
             c = cs + take;
@@ -516,8 +534,28 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
         return (uint32_t)kSortBins - 1u - min(n_blocks(q.prefix_len + (uint32_t)len, blk, lenb), (uint32_t)kSortBins - 1);
     };
     for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads) hist[i] = 0;
+    // small windows (the common case): every pair's (offset, length) loaded once, in one round, into registers
+    constexpr int kSortReg = 8;
+    const bool in_regs = filled <= (uint64_t)kFillThreads * kSortReg;
+    uint64_t reg_off[kSortReg];
+    uint32_t reg_len[kSortReg];
+    __syncthreads();  // the selection's placements (other threads' writes) are complete
+    if (in_regs) {
+#pragma unroll
+        for (int u = 0; u < kSortReg; ++u) {
+            const uint64_t t = threadIdx.x + (uint64_t)kFillThreads * u;
+            reg_off[u] = t < filled ? out_off[t] : 0;
+            reg_len[u] = t < filled ? out_len[t] : 0;
+        }
+    }
     __syncthreads();
-    for (uint64_t t = threadIdx.x; t < filled; t += kFillThreads) atomicAdd(&hist[bin_of(out_len[t])], 1u);
+    if (in_regs) {
+#pragma unroll
+        for (int u = 0; u < kSortReg; ++u)
+            if (threadIdx.x + (uint64_t)kFillThreads * u < filled) atomicAdd(&hist[bin_of(reg_len[u])], 1u);
+    } else {
+        for (uint64_t t = threadIdx.x; t < filled; t += kFillThreads) atomicAdd(&hist[bin_of(out_len[t])], 1u);
+    }
     __syncthreads();
     if (threadIdx.x < 64) {  // exclusive scan of the kSortBins counters by one wave
         const uint32_t per = kSortBins / 64, lane = threadIdx.x;
@@ -538,12 +576,26 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
     }
     __syncthreads();
     PairTask* task = L.task + (uint64_t)a_slot * W;
-    for (uint64_t t = threadIdx.x; t < filled; t += kFillThreads) {
-        PairTask tk;
-        tk.off = out_off[t];
-        tk.len = out_len[t];
-        tk.slot = (uint32_t)t;
-        task[atomicAdd(&hist[bin_of(tk.len)], 1u)] = tk;
+    if (in_regs) {
+#pragma unroll
+        for (int u = 0; u < kSortReg; ++u) {
+            const uint64_t t = threadIdx.x + (uint64_t)kFillThreads * u;
+            if (t < filled) {
+                PairTask tk;
+                tk.off = reg_off[u];
+                tk.len = reg_len[u];
+                tk.slot = (uint32_t)t;
+                task[atomicAdd(&hist[bin_of(tk.len)], 1u)] = tk;
+            }
+        }
+    } else {
+        for (uint64_t t = threadIdx.x; t < filled; t += kFillThreads) {
+            PairTask tk;
+            tk.off = out_off[t];
+            tk.len = out_len[t];
+            tk.slot = (uint32_t)t;
+            task[atomicAdd(&hist[bin_of(tk.len)], 1u)] = tk;
+        }
     }
     if (L.fill_clock && threadIdx.x == 0) {
         uint64_t* fc = L.fill_clock + (uint64_t)a_slot * 4;
