@@ -80,6 +80,8 @@ struct dsy_store {
     const uint64_t* d_offsets = nullptr;
     const uint64_t* d_live_gt = nullptr;
     const uint64_t* d_live_row = nullptr;
+    const uint8_t* d_lines = nullptr;  // line copy of the packets (the responder hashes from it)
+    const RowRec* d_rec = nullptr;
     std::vector<void*> owned;
     std::unordered_map<uint32_t, std::pair<uint64_t, uint64_t>> segs;
 };
@@ -561,6 +563,32 @@ static int store_finish(dsy_ctx* c, dsy_store* s, const uint64_t* h_gt_or_null, 
     return DSY_OK;
 }
 
+// The responder's line copy: row i's packet at rec[i].off, a multiple of 128, so every LDS-DMA piece of the
+// hashing kernel is one whole line (dsy_message.h hash_key_dma_lines).  Costs < 128 bytes per row.
+static int store_build_lines(dsy_ctx* c, dsy_store* s, const uint64_t* h_off) {
+    const uint64_t n = s->n;
+    std::vector<RowRec> rec(std::max<uint64_t>(n, 1));
+    uint64_t at = DSY_BLOB_GUARD;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t len = h_off[i + 1] - h_off[i];
+        rec[i] = RowRec{at, (uint32_t)len, 0u};
+        at += (len + 127) & ~127ull;
+    }
+    const uint64_t bytes = at + DSY_BLOB_GUARD;
+    void *pl, *pr;
+    if (hipMalloc(&pl, bytes) != hipSuccess) return fail(DSY_ENOMEM, "store line copy alloc (%llu B)", (unsigned long long)bytes);
+    s->owned.push_back(pl);
+    if (hipMalloc(&pr, rec.size() * sizeof(RowRec)) != hipSuccess) return fail(DSY_ENOMEM, "store row records alloc");
+    s->owned.push_back(pr);
+    HIP_TRY(hipMemsetAsync(pl, 0, bytes, c->stream));
+    HIP_TRY(hipMemcpyAsync(pr, rec.data(), rec.size() * sizeof(RowRec), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(launch_store_lines(s->d_blob, s->d_offsets, (const RowRec*)pr, n, (uint8_t*)pl, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    s->d_lines = (const uint8_t*)pl;
+    s->d_rec = (const RowRec*)pr;
+    return DSY_OK;
+}
+
 int dsy_store_upload(dsy_ctx* c, const uint8_t* blob, uint64_t blob_len, const uint64_t* offsets, uint64_t n,
                      const uint64_t* global_time, const uint32_t* meta, const uint8_t* undone, dsy_store** out) {
     if (!c || !out || !offsets || (n && (!global_time || !meta))) return fail(DSY_EINVAL, "NULL argument");
@@ -587,6 +615,7 @@ int dsy_store_upload(dsy_ctx* c, const uint8_t* blob, uint64_t blob_len, const u
     s->d_blob = (uint8_t*)pb;
     s->d_offsets = (uint64_t*)po;
     if ((rc = store_finish(c, s, global_time, nullptr, lg, lr, identity))) { dsy_store_free(s); return rc; }
+    if ((rc = store_build_lines(c, s, offsets))) { dsy_store_free(s); return rc; }
     *out = s;
     return DSY_OK;
 }
@@ -622,6 +651,7 @@ int dsy_store_attach(dsy_ctx* c, const uint8_t* d_blob, uint64_t blob_len, const
         return rc;
     }
     if ((rc = store_finish(c, s, nullptr, d_global_time, lg, lr, identity))) { dsy_store_free(s); return rc; }
+    if ((rc = store_build_lines(c, s, off.data()))) { dsy_store_free(s); return rc; }
     *out = s;
     return DSY_OK;
 }
@@ -678,7 +708,8 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
                         uint64_t** d_packed_off, uint64_t* total_pairs) {
     // ---- validate claims (payload.py:89-101, conversion.py:772-789) and their filters; group them by hash family
     // (kind x chunk width: one pair-test launch per family)
-    constexpr int kFamilies = 5 * 3;
+    // family id = (kind * 3 + chunk class) * 2 + long prefix (> 4 bytes: the byte-wise hashing path)
+    constexpr int kFamilies = 5 * 3 * 2;
     std::vector<uint32_t> fam_members[kFamilies];
     for (uint32_t r = 0; r < R; ++r) {
         const dsy_request& q = reqs[r];
@@ -693,7 +724,7 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
         if (q.filter_offset % 4) return fail(DSY_EINVAL, "claim %u: filter_offset must be a multiple of 4", r);
         if (filters_len && q.filter_offset + filter_words(q.m_bits) * 4 > filters_len)
             return fail(DSY_EINVAL, "claim %u: filter beyond the filters buffer", r);
-        fam_members[kind * 3 + (chunk == 2 ? 0 : chunk == 4 ? 1 : 2)].push_back(r);
+        fam_members[(kind * 3 + (chunk == 2 ? 0 : chunk == 4 ? 1 : 2)) * 2 + (q.prefix_len > 4)].push_back(r);
     }
     const uint64_t pool = kWindow * std::max<uint64_t>(R, kMinSlots);
     // ---- device layout: one upload region [claims | metas | window slots 0..R-1 | first active list] and one
@@ -786,6 +817,8 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     RespondLaunch L{};
     L.st.blob = s->d_blob;
     L.st.offsets = s->d_offsets;
+    L.st.lines = s->d_lines;
+    L.st.rec = s->d_rec;
     L.st.live_gt = s->d_live_gt;
     L.st.live_row = s->d_live_row;
     L.st.n_live = s->n_live;
@@ -914,7 +947,8 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
             if (!runs[f].second) continue;
             const int fid = fam_id[f];
             timer_begin(c, &t, kTimePairTest);
-            HIP_TRY(launch_pair_test_list(L, fid / 3, fid % 3 == 0 ? 2 : fid % 3 == 1 ? 4 : 8, d_slots + runs[f].first,
+            const int kc = fid / 2;
+            HIP_TRY(launch_pair_test_list(L, kc / 3, kc % 3 == 0 ? 2 : kc % 3 == 1 ? 4 : 8, fid % 2 == 1, d_slots + runs[f].first,
                                           (uint32_t)runs[f].second));
             timer_end(c, &t);
         }

@@ -60,9 +60,18 @@ hipError_t launch_len_sort(const LenSort& s, const uint64_t* offsets, const uint
 
 // ------------------------------------------------------------------------------------------ responder
 // Store view the responder kernels read.  `live` rows are the rows with undone == 0, in index order.
+// A store row's packet in the line copy: starts on a 128-byte line of StoreView::lines.
+struct RowRec {
+    uint64_t off;
+    uint32_t len;
+    uint32_t pad;
+};
+
 struct StoreView {
     const uint8_t* blob;
     const uint64_t* offsets;  // [n_rows + 1] over ALL rows
+    const uint8_t* lines;     // line copy of the packets (each starts on a 128-byte line)
+    const RowRec* rec;        // [n_rows] where row i's packet sits in `lines`
     const uint64_t* live_gt;  // [n_live] global_time of live row i
     const uint64_t* live_row; // [n_live] store row of live row i (nullptr: identity)
     uint64_t n_live;
@@ -161,9 +170,14 @@ hipError_t launch_setup(const RespondLaunch& L, const void* h_src, void* d_dst, 
 static constexpr uint32_t kPackFusedMax = 8192;  // claims packed by one launch (k_pack_fused)
 hipError_t launch_fill(const RespondLaunch& L);
 // hash + test the window's pairs of the listed window slots, all of one (hash kind, chunk) family
-hipError_t launch_pair_test_list(const RespondLaunch& L, int kind, uint32_t chunk, const uint32_t* d_list, uint32_t n);
+// long_prefix: the listed claims' prefixes are longer than 4 bytes (hashed without the LDS-DMA staging)
+hipError_t launch_pair_test_list(const RespondLaunch& L, int kind, uint32_t chunk, bool long_prefix,
+                                 const uint32_t* d_list, uint32_t n);
 hipError_t launch_compact(const RespondLaunch& L);
 hipError_t launch_pack(const RespondLaunch& L, uint64_t* packed, uint64_t* packed_offsets, uint64_t* d_scan_tmp);
+// copy each row's packet from (blob, offsets) to its line-aligned place rec[i].off in lines
+hipError_t launch_store_lines(const uint8_t* blob, const uint64_t* offsets, const RowRec* rec, uint64_t n,
+                              uint8_t* lines, hipStream_t stream);
 
 // ---------------------------------------------------------------------------------------- simulator
 static constexpr uint32_t kSimFilterWordsMax = 2048;  // m <= 65536 bits

@@ -341,11 +341,12 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
             const uint64_t cs = c > it0 ? c : it0;
             const uint64_t avail = cs < it1 ? it1 - cs : 0;
             const uint64_t take = avail < W - filled ? avail : W - filled;
-            const uint64_t* __restrict__ offs = L.st.offsets;
+            const RowRec* __restrict__ rec = L.st.rec;
             // kDenseU rows per thread per round, every load of the round issued before the first is consumed
             constexpr int kDenseU = 8;
             for (uint64_t i0 = 0; i0 < take; i0 += (uint64_t)kFillThreads * kDenseU) {
-                uint64_t row[kDenseU], a0[kDenseU], a1[kDenseU];
+                uint64_t row[kDenseU];
+                RowRec rr[kDenseU];
 #pragma unroll
                 for (int u = 0; u < kDenseU; ++u) {
                     const uint64_t i = i0 + threadIdx.x + (uint64_t)kFillThreads * u;
@@ -357,16 +358,15 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
 #pragma unroll
                 for (int u = 0; u < kDenseU; ++u) {
                     const bool in = i0 + threadIdx.x + (uint64_t)kFillThreads * u < take;
-                    a0[u] = in ? offs[row[u]] : 0;
-                    a1[u] = in ? offs[row[u] + 1] : 0;
+                    rr[u] = in ? rec[row[u]] : RowRec{};
                 }
 #pragma unroll
                 for (int u = 0; u < kDenseU; ++u) {
                     const uint64_t i = i0 + threadIdx.x + (uint64_t)kFillThreads * u;
                     if (i < take) {
                         out[filled + i] = row[u];
-                        out_off[filled + i] = a0[u];
-                        out_len[filled + i] = (uint32_t)(a1[u] - a0[u]);
+                        out_off[filled + i] = rr[u].off;
+                        out_len[filled + i] = rr[u].len;
                     }
                 }
             }
@@ -441,26 +441,24 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
         const uint64_t pos = block_exclusive_scan(tcnt, scan, &total);
         // emit the rows of these candidates that still fit in the window, in candidate order: first every
         // candidate's first row with all loads issued together, then the rare extra rows of shared global times
-        const uint64_t* __restrict__ offs = L.st.offsets;
-        uint64_t row0[kCand], o0[kCand], o1[kCand];
+        const RowRec* __restrict__ rec = L.st.rec;
+        uint64_t row0[kCand];
+        RowRec r0[kCand];
 #pragma unroll
         for (int u = 0; u < kCand; ++u) {
             const uint64_t lr = xs[u];
             row0[u] = (cnts[u] && L.st.live_row) ? L.st.live_row[lr] : lr;
         }
 #pragma unroll
-        for (int u = 0; u < kCand; ++u) {
-            o0[u] = cnts[u] ? offs[row0[u]] : 0;
-            o1[u] = cnts[u] ? offs[row0[u] + 1] : 0;
-        }
+        for (int u = 0; u < kCand; ++u) r0[u] = cnts[u] ? rec[row0[u]] : RowRec{};
         uint64_t at = pos;
 #pragma unroll
         for (int u = 0; u < kCand; ++u) {
             const uint64_t dst = filled + at;
             if (cnts[u] && dst < W) {
                 out[dst] = row0[u];
-                out_off[dst] = o0[u];
-                out_len[dst] = (uint32_t)(o1[u] - o0[u]);
+                out_off[dst] = r0[u].off;
+                out_len[dst] = r0[u].len;
             }
             at += cnts[u];
         }
@@ -472,10 +470,10 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
                 if (dst >= W) break;
                 const uint64_t lr = p.dir == DSY_DESC ? xs[u] - e : xs[u] + e;
                 const uint64_t row = L.st.live_row ? L.st.live_row[lr] : lr;
-                const uint64_t a0 = offs[row], a1 = offs[row + 1];
+                const RowRec rw = rec[row];
                 out[dst] = row;
-                out_off[dst] = a0;
-                out_len[dst] = (uint32_t)(a1 - a0);
+                out_off[dst] = rw.off;
+                out_len[dst] = rw.len;
             }
             at += cnts[u];
         }
@@ -608,7 +606,7 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
 
 // -------------------------------------------------------------------------------------- k_pair_test
 template <class H, int CHUNK, bool DMA>
-__global__ void __launch_bounds__(256) k_pair_test(RespondLaunch L, const uint32_t* __restrict__ req_list,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_pair_test(RespondLaunch L, const uint32_t* __restrict__ req_list,
                                                    uint32_t n_list) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dma_lds[];
     const uint64_t W = L.window;
@@ -631,17 +629,16 @@ __global__ void __launch_bounds__(256) k_pair_test(RespondLaunch L, const uint32
         const bool active = i < n;
         const DevRequest& q = L.reqs[r];
         uint32_t t = 0;
-        KeyView kv{L.st.blob, 0u, q.prefix, q.prefix_len};  // idle lanes hash an empty key
+        KeyView kv{L.st.lines, 0u, q.prefix, q.prefix_len};  // idle lanes hash an empty key
         if (active) {
             const PairTask tk = L.task[(uint64_t)a_slot * W + i];
             t = tk.slot;
-            kv.key = L.st.blob + tk.off;
+            kv.key = L.st.lines + tk.off;
             kv.len = tk.len;
         }
         H st;
         if constexpr (DMA) {
-            if (q.prefix_len <= 4) hash_key_dma_reg<H, 2>(kv, st, my_lds);
-            else hash_key<H>(kv, st);
+            hash_key_dma_lines<H>(kv, st, my_lds);  // the host routes prefixes > 4 bytes to DMA = false
         } else {
             hash_key<H>(kv, st);
         }
@@ -693,7 +690,7 @@ __global__ void __launch_bounds__(256) k_pair_test(RespondLaunch L, const uint32
 }
 
 template <class H, int CHUNK>
-static hipError_t pair_test_family(const RespondLaunch& L, const uint32_t* list, uint32_t n_list) {
+static hipError_t pair_test_family(const RespondLaunch& L, bool long_prefix, const uint32_t* list, uint32_t n_list) {
     const uint64_t waves = (uint64_t)n_list * (L.window / 64);
     uint64_t blocks = (waves + 3) / 4;
     if (blocks > 256 * 16) blocks = 256 * 16;
@@ -702,27 +699,37 @@ static hipError_t pair_test_family(const RespondLaunch& L, const uint32_t* list,
     // instruction, single LDS buffer, next stage in flight while the current one is compressed from registers:
     // tools/hashbench, profiles/hashbench_r1_dmareg.txt); SHA-2 is compute-bound enough that direct loads match it
     constexpr bool dma = H::kind == DSY_MD5 || H::kind == DSY_SHA1;
-    const size_t lds = dma ? 4 * DmaGeometry<2, 1>::kWaveBytes : 0;
-    hipLaunchKernelGGL((k_pair_test<H, CHUNK, dma>), dim3((uint32_t)blocks), dim3(256), lds, L.stream, L, list, n_list);
+    if constexpr (dma) {
+        if (!long_prefix) {
+            const size_t lds = 4 * DmaGeometry<2, 1>::kWaveBytes;
+            hipLaunchKernelGGL((k_pair_test<H, CHUNK, true>), dim3((uint32_t)blocks), dim3(256), lds, L.stream, L, list,
+                               n_list);
+            return hipGetLastError();
+        }
+    }
+    hipLaunchKernelGGL((k_pair_test<H, CHUNK, false>), dim3((uint32_t)blocks), dim3(256), 0, L.stream, L, list, n_list);
     return hipGetLastError();
 }
 
 template <class H>
-static hipError_t pair_test_chunk(const RespondLaunch& L, uint32_t chunk, const uint32_t* list, uint32_t n) {
+static hipError_t pair_test_chunk(const RespondLaunch& L, uint32_t chunk, bool lp, const uint32_t* list, uint32_t n) {
     switch (chunk) {
-        case 2: return pair_test_family<H, 2>(L, list, n);
-        case 4: return pair_test_family<H, 4>(L, list, n);
-        default: return pair_test_family<H, 8>(L, list, n);
+        case 2: return pair_test_family<H, 2>(L, lp, list, n);
+        case 4: return pair_test_family<H, 4>(L, lp, list, n);
+        default: return pair_test_family<H, 8>(L, lp, list, n);
     }
 }
 
-hipError_t launch_pair_test_list(const RespondLaunch& L, int kind, uint32_t chunk, const uint32_t* list, uint32_t n) {
+hipError_t launch_pair_test_list(const RespondLaunch& L, int kind, uint32_t chunk, bool long_prefix, const uint32_t* list,
+                                 uint32_t n) {
     switch (kind) {
-        case DSY_MD5: return pair_test_chunk<Md5>(L, chunk, list, n);
-        case DSY_SHA1: return chunk == 2 ? pair_test_family<Sha1, 2>(L, list, n) : pair_test_family<Sha1, 4>(L, list, n);
-        case DSY_SHA256: return pair_test_chunk<Sha256>(L, chunk, list, n);
-        case DSY_SHA384: return pair_test_chunk<Sha384>(L, chunk, list, n);
-        default: return pair_test_chunk<Sha512>(L, chunk, list, n);
+        case DSY_MD5: return pair_test_chunk<Md5>(L, chunk, long_prefix, list, n);
+        case DSY_SHA1:
+            return chunk == 2 ? pair_test_family<Sha1, 2>(L, long_prefix, list, n)
+                              : pair_test_family<Sha1, 4>(L, long_prefix, list, n);
+        case DSY_SHA256: return pair_test_chunk<Sha256>(L, chunk, long_prefix, list, n);
+        case DSY_SHA384: return pair_test_chunk<Sha384>(L, chunk, long_prefix, list, n);
+        default: return pair_test_chunk<Sha512>(L, chunk, long_prefix, list, n);
     }
 }
 
@@ -950,6 +957,26 @@ __global__ void __launch_bounds__(256) k_pack_fused(RespondLaunch L, uint64_t* p
         if (r + 1 == L.R) packed_offsets[L.R] = off + S.emitted;
     }
     if (r == 0) fold_status(L);
+}
+
+// one wave per row: bytes of the packet to its line-aligned place (coalesced 64-byte stretches)
+__global__ void __launch_bounds__(256) k_store_lines(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ offsets,
+                                                     const RowRec* __restrict__ rec, uint64_t n, uint8_t* __restrict__ lines) {
+    const uint64_t row = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    if (row >= n) return;
+    const uint8_t* src = blob + offsets[row];
+    uint8_t* dst = lines + rec[row].off;
+    const uint32_t len = rec[row].len;
+    for (uint32_t k = lane; k < len; k += 64) dst[k] = src[k];
+}
+
+hipError_t launch_store_lines(const uint8_t* blob, const uint64_t* offsets, const RowRec* rec, uint64_t n,
+                              uint8_t* lines, hipStream_t stream) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_store_lines, dim3((uint32_t)((n * 64 + 255) / 256)), dim3(256), 0, stream, blob, offsets, rec,
+                       n, lines);
+    return hipGetLastError();
 }
 
 hipError_t launch_setup(const RespondLaunch& L, const void* h_src, void* d_dst, size_t in_bytes, void* d_zero,

@@ -156,8 +156,10 @@ int dsy_bloom_test_dev(dsy_ctx* ctx, const dsy_bloom_params* p, const uint8_t* d
  * undone may be NULL (all rows live).  Rows with undone != 0 never take part in selection. */
 int dsy_store_upload(dsy_ctx* ctx, const uint8_t* blob, uint64_t blob_len, const uint64_t* offsets, uint64_t n,
                      const uint64_t* global_time, const uint32_t* meta, const uint8_t* undone, dsy_store** out);
-/* Same, over device buffers the caller keeps alive (no copy).  d_blob needs DSY_BLOB_GUARD readable bytes
- * before offsets[0] and past offsets[n]. */
+/* Same, over device buffers the caller keeps alive (the index arrays are not copied).  d_blob needs
+ * DSY_BLOB_GUARD readable bytes before offsets[0] and past offsets[n].
+ * Both forms also build the responder's line copy of the packets on the device: every packet starts on a
+ * 128-byte line (< 128 bytes of padding per row), so the hashing kernel's loads are whole cache lines. */
 int dsy_store_attach(dsy_ctx* ctx, const uint8_t* d_blob, uint64_t blob_len, const uint64_t* d_offsets, uint64_t n,
                      const uint64_t* d_global_time, const uint32_t* d_meta, const uint8_t* d_undone, dsy_store** out);
 int dsy_store_free(dsy_store* store);

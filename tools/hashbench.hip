@@ -697,6 +697,52 @@ __device__ __forceinline__ void hb_hash_key_dma_aligned(const KeyView& kv, H& st
     }
 }
 
+template <class H, int MODE, int WG>
+__global__ void __launch_bounds__(WG) k_hash_pad(const uint8_t* blob, const uint64_t* poff, const uint32_t* lens,
+                                                 const uint32_t* order, uint32_t n, const uint8_t* pre, uint32_t plen,
+                                                 uint32_t* out) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t dyn[];
+    const uint32_t i = blockIdx.x * WG + threadIdx.x;
+    const uint32_t key = order ? order[min(i, n - 1)] : min(i, n - 1);
+    KeyView kv{blob + poff[key], i < n ? lens[key] : 0u, pre, plen};
+    H st;
+    uint8_t* lw = dyn + (threadIdx.x >> 6) * DmaGeometry<2, 1>::kWaveBytes;
+    if (MODE == 0) hash_key_dma_reg<H, 2>(kv, st, lw);
+    else hash_key_dma_lines<H>(kv, st, lw);
+    uint32_t x = 0;
+#pragma unroll
+    for (int j = 0; j < H::digest_bytes / 4; ++j) x ^= st.be_word(j);
+    if (i < n) out[i] = x;
+}
+
+template <class H, int MODE, int WG>
+float run_pad(const uint8_t* blob, const uint64_t* poff, const uint32_t* lens, const uint32_t* order, uint32_t n,
+              const uint8_t* pre, uint32_t plen, uint32_t* out, int reps) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    dim3 grid((n + WG - 1) / WG);
+    const size_t dl = (size_t)(WG / 64) * DmaGeometry<2, 1>::kWaveBytes;
+    hipLaunchKernelGGL((k_hash_pad<H, MODE, WG>), grid, dim3(WG), dl, 0, blob, poff, lens, order, n, pre, plen, out);
+    CK(hipEventRecord(a));
+    for (int r = 0; r < reps; ++r)
+        hipLaunchKernelGGL((k_hash_pad<H, MODE, WG>), grid, dim3(WG), dl, 0, blob, poff, lens, order, n, pre, plen, out);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    std::vector<uint32_t> h(n), ord(n), byk(n);
+    CK(hipMemcpy(h.data(), out, n * 4, hipMemcpyDeviceToHost));
+    if (order) {
+        CK(hipMemcpy(ord.data(), order, n * 4, hipMemcpyDeviceToHost));
+        for (uint32_t i = 0; i < n; ++i) byk[ord[i]] = h[i];
+    } else byk = h;
+    uint64_t cs = 0;
+    for (uint32_t i = 0; i < n; ++i) cs = cs * 1000003u + byk[i];
+    g_checksum = cs;
+    return ms / reps;
+}
+
 template <class H, int S, int WG>
 __global__ void __launch_bounds__(WG) k_hash_dma_a(const uint8_t* blob, const uint64_t* off, const uint32_t* order,
                                                    uint32_t n, const uint8_t* pre, uint32_t plen, uint32_t* out) {
@@ -824,25 +870,46 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(d_off, off.data(), (n + 1) * 8, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_order, order.data(), n * 4, hipMemcpyHostToDevice));
     CK(hipMemset(d_pre, 0x2a, 256));
-    printf("n=%u bytes=%.1f MB blocks(md5)=%llu\n", n, bytes / 1e6, (unsigned long long)blocks);
+    // the same packets, each starting on a 128-byte line
+    std::vector<uint64_t> poff(n);
+    std::vector<uint32_t> lens(n);
+    uint64_t pat = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        poff[i] = pat;
+        lens[i] = (uint32_t)(off[i + 1] - off[i]);
+        pat = (pat + lens[i] + 127) & ~127ull;
+    }
+    std::vector<uint8_t> pblob(pat + 256, 0);
+    for (uint32_t i = 0; i < n; ++i) memcpy(&pblob[poff[i]], &blob[off[i]], lens[i]);
+    uint8_t* d_pblob;
+    uint64_t* d_poff;
+    uint32_t* d_lens;
+    CK(hipMalloc(&d_pblob, pblob.size() + 256));
+    d_pblob += 128;  // the prefix byte before the first packet is read (and patched) by the unaligned path
+    CK(hipMalloc(&d_poff, n * 8));
+    CK(hipMalloc(&d_lens, n * 4));
+    CK(hipMemcpy(d_pblob, pblob.data(), pblob.size(), hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_poff, poff.data(), n * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_lens, lens.data(), n * 4, hipMemcpyHostToDevice));
+    printf("n=%u bytes=%.1f MB blocks(md5)=%llu padded=%.1f MB\n", n, bytes / 1e6, (unsigned long long)blocks, pat / 1e6);
     for (int round = 0; round < 2; ++round) {
         struct R { const char* name; float ms; uint64_t cs = 0; };
         std::vector<R> rs;
 #define V(NAME, CALL) { float ms_ = CALL; rs.push_back({NAME, ms_, g_checksum}); }
         V("md5 dmareg(2) wg256", (run_dma_r<Md5, 2, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
-        V("md5 aligned S2 wg256", (run_dma_a<Md5, 2, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
-        V("md5 aligned S1 wg256", (run_dma_a<Md5, 1, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
-        V("md5 aligned S1 wg128", (run_dma_a<Md5, 1, 128>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+        V("md5 dmareg(2) padded", (run_pad<Md5, 0, 256>(d_pblob, d_poff, d_lens, d_order, n, d_pre, 1, d_out, reps)));
+        V("md5 pa padded", (run_pad<Md5, 1, 256>(d_pblob, d_poff, d_lens, d_order, n, d_pre, 1, d_out, reps)));
+        V("md5 dmareg(2) plen0", (run_dma_r<Md5, 2, 256>(d_blob, d_off, d_order, n, d_pre, 0, d_out, reps)));
+        V("md5 pa plen0", (run_pad<Md5, 1, 256>(d_pblob, d_poff, d_lens, d_order, n, d_pre, 0, d_out, reps)));
         V("md5 dmareg(2) plen3", (run_dma_r<Md5, 2, 256>(d_blob, d_off, d_order, n, d_pre, 3, d_out, reps)));
-        V("md5 aligned S1 plen3", (run_dma_a<Md5, 1, 256>(d_blob, d_off, d_order, n, d_pre, 3, d_out, reps)));
-        V("md5 aligned S2 plen3", (run_dma_a<Md5, 2, 256>(d_blob, d_off, d_order, n, d_pre, 3, d_out, reps)));
+        V("md5 pa plen3", (run_pad<Md5, 1, 256>(d_pblob, d_poff, d_lens, d_order, n, d_pre, 3, d_out, reps)));
+        V("md5 dmareg(2) plen4", (run_dma_r<Md5, 2, 256>(d_blob, d_off, d_order, n, d_pre, 4, d_out, reps)));
+        V("md5 pa plen4", (run_pad<Md5, 1, 256>(d_pblob, d_poff, d_lens, d_order, n, d_pre, 4, d_out, reps)));
         V("sha1 dmareg(2) wg256", (run_dma_r<Sha1, 2, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
-        V("sha1 aligned S1 wg256", (run_dma_a<Sha1, 1, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
-        V("sha1 aligned S2 wg256", (run_dma_a<Sha1, 2, 256>(d_blob, d_off, d_order, n, d_pre, 1, d_out, reps)));
+        V("sha1 pa padded", (run_pad<Sha1, 1, 256>(d_pblob, d_poff, d_lens, d_order, n, d_pre, 1, d_out, reps)));
         V("md5 dmareg(2) scat", (run_dma_r<Md5, 2, 256>(d_blob, d_off, d_scat_sorted, n, d_pre, 1, d_out, reps)));
-        V("md5 aligned S1 scat", (run_dma_a<Md5, 1, 256>(d_blob, d_off, d_scat_sorted, n, d_pre, 1, d_out, reps)));
-        V("probe S=1 aligned", (run_probe<1, 256, true>(d_blob, d_off, d_order, n, d_out, reps)));
-        V("probe S=2 unaligned", (run_probe<2, 256, false>(d_blob, d_off, d_order, n, d_out, reps)));
+        V("md5 pa scat", (run_pad<Md5, 1, 256>(d_pblob, d_poff, d_lens, d_scat_sorted, n, d_pre, 1, d_out, reps)));
+        V("probe S=2 aligned", (run_probe<2, 256, true>(d_blob, d_off, d_order, n, d_out, reps)));
 #undef V
         for (auto& r : rs) (void)0;
         for (auto& r : rs)
