@@ -50,9 +50,10 @@ def parse():
     ap.add_argument("--sim-initial", type=int, default=100)
     ap.add_argument("--sim-rounds", type=int, default=10)
     ap.add_argument("--sim-warmup", type=int, default=2)
-    ap.add_argument("--extra", default="1,3,4,5",
+    ap.add_argument("--extra", default="ingest,1,3,4,5",
                     help="BASELINE configs measured beside the headline (config 2): 1 single filter, 3 gossip "
-                         "simulator, 4 large filters, 5 heavy-tailed packets; '' for none")
+                         "simulator, 4 large filters, 5 heavy-tailed packets, ingest: received packets appended to "
+                         "the headline store; '' for none")
     ap.add_argument("--large-keys", type=int, default=100_000_000, help="config 4: keys added per filter")
     ap.add_argument("--large-tests", type=int, default=10_000_000, help="config 4: keys tested per filter")
     return ap.parse_args()
@@ -226,6 +227,10 @@ def main():
 
     extra = set(x for x in args.extra.split(",") if x and x != "none")
 
+    ingest = None
+    if "ingest" in extra:
+        ingest = ingest_bench(args, ctx, lib, store, step, pairs, N)
+
     gossip = None
     if "3" in extra and args.sim_peers > 0:
         gossip = gossip_sim(args, ctx, dev, rank, world, dist)
@@ -272,12 +277,84 @@ def main():
             "single_filter": single,
             "large_filter": large,
             "heavy_tail": heavy,
+            "ingest": ingest,
         }
         print(json.dumps(line))
     if store is not None:
         lib.dsy_store_free(store)
     if dist:
         dist.destroy_process_group()
+
+
+def ingest_bench(args, ctx, lib, store, step, pairs, N, batch=10_000, batches=10):
+    """SURVEY §8f row 1, requester-side ingest: `Dispersy._store` INSERTs each batch of received sync packets
+    (dispersy.py:1475-1612).  Here batches of `batch` packets (100-1500 B, global times spread over the store's
+    range, so they land everywhere in the index and tie with stored rows) go into the headline's 10 M-packet store
+    through dsy_store_append: host buffers -> HBM, line copy, and the (meta, global_time, rowid) index merge on the
+    device (k_ingest_*: 16 B read + 16 B written per indexed row).  The first append moves the caller-owned
+    (attached) store into grow-able buffers of its own and is reported apart.  A responder step runs on the grown
+    store afterwards.  Wall time per call, PCIe upload of the packets included."""
+    import torch
+    rng = np.random.Generator(np.random.PCG64(99))
+
+    def make():
+        lens = rng.integers(100, 1501, size=batch)
+        off = np.zeros(batch + 1, dtype=np.uint64)
+        np.cumsum(lens, out=off[1:])
+        data = rng.bytes(int(off[-1]))
+        gts = rng.integers(1, N + 1, size=batch).astype(np.uint64)
+        metas = np.ones(batch, dtype=np.uint32)
+        return data, off, gts, metas
+
+    def append(b):
+        data, off, gts, metas = b
+        _native.check(lib.dsy_store_append(ctx.handle, store, data, len(data), off.ctypes.data, batch,
+                                           gts.ctypes.data, metas.ctypes.data))
+
+    work = [make() for _ in range(batches + 1)]
+    t0 = time.perf_counter()
+    append(work[0])
+    first_ms = (time.perf_counter() - t0) * 1e3
+    times = []
+    for b in work[1:]:
+        t0 = time.perf_counter()
+        append(b)
+        times.append(time.perf_counter() - t0)
+    ms = sorted(times)[len(times) // 2] * 1e3
+    rows = int(lib.dsy_store_rows(store))
+    pkt_bytes = sum(len(b[0]) for b in work[1:]) / batches
+    step()
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    cpu = None
+    if args.cpu_claims > 0:  # the CPU baseline leg: the reference's INSERT through sqlite3 (oracle/sync_ref.py)
+        import sqlite3
+        from oracle.sync_ref import SYNC_SCHEMA, insert_packets
+        conn = sqlite3.connect(":memory:")
+        conn.executescript(SYNC_SCHEMA)
+        pre = 200_000
+        crng = np.random.Generator(np.random.PCG64(5))
+        plens = crng.integers(100, 1501, size=pre)
+        conn.executemany("INSERT INTO sync (community, member, global_time, meta_message, packet) VALUES (1, ?, ?, 1, ?)",
+                         ((i, int(g), crng.bytes(int(l))) for i, (g, l) in
+                          enumerate(zip(crng.integers(1, N + 1, size=pre), plens))))
+        conn.commit()
+        data, off, gts, _ = work[1]
+        rows = [(pre + i, int(gts[i]), 1, data[int(off[i]):int(off[i + 1])]) for i in range(batch)]
+        t0 = time.perf_counter()
+        insert_packets(conn, 1, rows)
+        conn.commit()
+        dt = time.perf_counter() - t0
+        conn.close()
+        cpu = {"value": round(batch / dt, 1), "unit": "packets/s", "cores": 1, "kind": "port",
+               "sample": "one batch of %d packets INSERTed one statement each (dispersy.py:1523-1533) into an "
+                         "in-memory sqlite3 sync table with its index, pre-filled with %d rows" % (batch, pre)}
+    return {"metric": "received packets stored/sec", "batch": batch, "batches": batches, "cpu_baseline": cpu,
+            "store_rows_after": rows, "median_ms_per_batch": round(ms, 3),
+            "packets_per_s": round(batch / (ms / 1e3), 1),
+            "first_append_ms": round(first_ms, 2),
+            "index_bytes_per_append": 32 * rows, "packet_bytes_per_append": int(pkt_bytes),
+            "respond_after_ingest_pairs": int(pairs.value)}
 
 
 def gossip_sim(args, ctx, dev, rank, world, dist):

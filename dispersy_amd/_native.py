@@ -82,6 +82,7 @@ SIGNATURES = {
     "dsy_store_attach": (ctypes.c_int, [_P, _P, _U64, _P, _U64, _P, _P, _P, ctypes.POINTER(_P)]),
     "dsy_store_free": (ctypes.c_int, [_P]),
     "dsy_store_rows": (_U64, [_P]),
+    "dsy_store_append": (ctypes.c_int, [_P, _P, _P, _U64, _P, _U64, _P, _P]),
     "dsy_bloom_add_rows": (ctypes.c_int, [_P, ctypes.POINTER(BloomParams), _P, _P, _U64, _P]),
     "dsy_sync_respond": (ctypes.c_int, [_P, _P, ctypes.POINTER(Request), _U32, _P, _U64, ctypes.POINTER(Meta), _U32,
                                         _U64, ctypes.c_int, ctypes.c_int64, _U64, _P, _U64, _P]),

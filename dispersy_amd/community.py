@@ -159,6 +159,22 @@ class SyncCommunity(object):
         if packets:
             cache.bloom_filter.add_keys(packets)
 
+    def store_messages(self, messages):
+        """Dispersy._store (dispersy.py:1475-1612) for the sync table: INSERT the messages' packets (one batched
+        SyncStore.append -> dsy_store_append into HBM), raise the community's global time to the highest stored one,
+        then dispersy_store(messages) updates the cached claim filter.  A message carries .packet,
+        .distribution.global_time and its meta's database id (.database_id, or .meta.database_id).  As in the
+        reference, the caller has already dropped duplicates (dispersy.py:1496-1498); LastSyncDistribution's history
+        pruning (DELETE of older rows, :1560-1604) is not part of this path.  Returns the new store rows."""
+        if not messages:
+            return np.zeros(0, dtype=np.int64)
+        metas = [m.database_id if hasattr(m, "database_id") else m.meta.database_id for m in messages]
+        gts = [m.distribution.global_time for m in messages]
+        rows = self._store.append([m.packet for m in messages], gts, metas)
+        self.update_global_time(max(gts))
+        self.dispersy_store(messages)
+        return rows
+
     def dispersy_claim_sync_bloom_filter(self, request_cache):
         """community.py:709-758.  Returns (time_low, time_high, modulo, offset, bloom_filter) or None."""
         if self._sync_cache:

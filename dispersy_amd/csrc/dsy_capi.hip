@@ -84,6 +84,16 @@ struct dsy_store {
     const RowRec* d_rec = nullptr;
     std::vector<void*> owned;
     std::unordered_map<uint32_t, std::pair<uint64_t, uint64_t>> segs;
+    // capacities for dsy_store_append (0: exactly the built size)
+    uint64_t blob_cap = 0;    // bytes usable at d_blob (a DSY_BLOB_GUARD tail follows)
+    uint64_t off_cap = 0;     // entries of d_offsets
+    uint64_t lines_used = 0;  // bytes of d_lines in use (front guard + line-aligned packets)
+    uint64_t lines_cap = 0;   // bytes of d_lines (the tail guard included)
+    uint64_t rec_cap = 0;     // entries of d_rec
+    uint64_t live_cap = 0;    // entries of d_live_gt / d_live_row when they are the ingest's own buffers
+    uint64_t* spare_gt = nullptr;   // the ingest's second index buffer pair (the next merge's target)
+    uint64_t* spare_row = nullptr;
+    uint64_t spare_cap = 0;
 };
 
 namespace {
@@ -586,6 +596,9 @@ static int store_build_lines(dsy_ctx* c, dsy_store* s, const uint64_t* h_off) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     s->d_lines = (const uint8_t*)pl;
     s->d_rec = (const RowRec*)pr;
+    s->lines_used = at;
+    s->lines_cap = bytes;
+    s->rec_cap = rec.size();
     return DSY_OK;
 }
 
@@ -614,6 +627,8 @@ int dsy_store_upload(dsy_ctx* c, const uint8_t* blob, uint64_t blob_len, const u
     HIP_TRY(hipMemcpyAsync(po, offsets, (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
     s->d_blob = (uint8_t*)pb;
     s->d_offsets = (uint64_t*)po;
+    s->blob_cap = blob_len;
+    s->off_cap = n + 1;
     if ((rc = store_finish(c, s, global_time, nullptr, lg, lr, identity))) { dsy_store_free(s); return rc; }
     if ((rc = store_build_lines(c, s, offsets))) { dsy_store_free(s); return rc; }
     *out = s;
@@ -669,6 +684,210 @@ int dsy_store_free(dsy_store* s) {
 }
 
 uint64_t dsy_store_rows(const dsy_store* s) { return s ? s->n : 0; }
+
+// ------------------------------------------------------------------------------------------------ ingest
+namespace {
+
+bool store_owns(const dsy_store* s, const void* p) {
+    return std::find(s->owned.begin(), s->owned.end(), p) != s->owned.end();
+}
+
+void store_release(dsy_store* s, const void* p) {
+    auto it = std::find(s->owned.begin(), s->owned.end(), p);
+    if (it == s->owned.end()) return;  // a caller's buffer (dsy_store_attach): not ours to free
+    hipFree(*it);
+    s->owned.erase(it);
+}
+
+uint64_t grown(uint64_t need, uint64_t have) { return std::max<uint64_t>(need, have + have / 4 + 4096); }
+
+}  // namespace
+
+int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blob_len, const uint64_t* offsets,
+                     uint64_t a, const uint64_t* gt, const uint32_t* meta) {
+    if (!c || !s || !offsets || (a && (!gt || !meta || (blob_len && !blob)))) return fail(DSY_EINVAL, "NULL argument");
+    if (s->ctx != c) return fail(DSY_EINVAL, "store belongs to another context");
+    int rc = check_offsets(offsets, a, blob_len);
+    if (rc) return rc;
+    if (a == 0) return DSY_OK;
+    Guard g(c);
+    const uint64_t n0 = s->n, base0 = offsets[0], add = offsets[a] - base0;
+
+    // the new rows in index order (meta_message, global_time, rowid): argument order breaks ties
+    std::vector<uint64_t> ord(a);
+    for (uint64_t j = 0; j < a; ++j) ord[j] = j;
+    std::stable_sort(ord.begin(), ord.end(), [&](uint64_t x, uint64_t y) {
+        return meta[x] != meta[y] ? meta[x] < meta[y] : gt[x] < gt[y];
+    });
+    // each new row's meta segment in the old live index; a new meta sits after every smaller meta's segment
+    std::vector<std::pair<uint32_t, std::pair<uint64_t, uint64_t>>> old(s->segs.begin(), s->segs.end());
+    std::sort(old.begin(), old.end());
+    std::vector<IngestRow> rows(a);
+    uint64_t minlen = ~0ull;
+    for (uint64_t t = 0; t < a; ++t) {
+        const uint64_t j = ord[t];
+        auto it = s->segs.find(meta[j]);
+        uint64_t sa, sb;
+        if (it != s->segs.end()) {
+            sa = it->second.first, sb = it->second.second;
+        } else {
+            sa = 0;
+            for (auto& e : old)
+                if (e.first < meta[j]) sa = std::max(sa, e.second.second);
+            sb = sa;
+        }
+        rows[t] = IngestRow{gt[j], sa, sb, n0 + j};
+        minlen = std::min(minlen, offsets[j + 1] - offsets[j]);
+    }
+
+    // raw blob + offsets (dsy_bloom_add_rows reads them): grow into buffers of our own, then write the new tail
+    HIP_TRY(hipStreamSynchronize(c->stream));  // nothing in flight reads a buffer that is about to be replaced
+    uint8_t* d_blob = const_cast<uint8_t*>(s->d_blob);
+    const void* blob_base = s->d_blob ? s->d_blob - DSY_BLOB_GUARD : nullptr;
+    if (!store_owns(s, blob_base) || s->blob_len + add > s->blob_cap) {
+        const uint64_t cap = grown(s->blob_len + add, s->blob_len);
+        void* nb;
+        if (hipMalloc(&nb, cap + 2 * DSY_BLOB_GUARD) != hipSuccess)
+            return fail(DSY_ENOMEM, "store blob growth (%llu B)", (unsigned long long)cap);
+        HIP_TRY(hipMemsetAsync(nb, 0, DSY_BLOB_GUARD, c->stream));
+        uint8_t* nd = (uint8_t*)nb + DSY_BLOB_GUARD;
+        if (s->blob_len) HIP_TRY(hipMemcpyAsync(nd, s->d_blob, s->blob_len, hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        store_release(s, blob_base);
+        s->owned.push_back(nb);
+        d_blob = nd;
+        s->d_blob = nd;
+        s->blob_cap = cap;
+    }
+    if (add) HIP_TRY(hipMemcpyAsync(d_blob + s->blob_len, blob + base0, add, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(d_blob + s->blob_len + add, 0, DSY_BLOB_GUARD, c->stream));
+    if (!store_owns(s, s->d_offsets) || n0 + a + 1 > s->off_cap) {
+        const uint64_t cap = grown(n0 + a + 1, n0 + 1);
+        void* no;
+        if (hipMalloc(&no, cap * 8) != hipSuccess) return fail(DSY_ENOMEM, "store offsets growth");
+        HIP_TRY(hipMemcpyAsync(no, s->d_offsets, (n0 + 1) * 8, hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        store_release(s, s->d_offsets);
+        s->owned.push_back(no);
+        s->d_offsets = (const uint64_t*)no;
+        s->off_cap = cap;
+    }
+    std::vector<uint64_t> noff(a);
+    for (uint64_t j = 0; j < a; ++j) noff[j] = s->blob_len + offsets[j + 1] - base0;
+
+    // the line copy the responder hashes from, and its row records
+    std::vector<RowRec> nrec(a);
+    uint64_t at = s->lines_used;
+    for (uint64_t j = 0; j < a; ++j) {
+        const uint64_t len = offsets[j + 1] - offsets[j];
+        nrec[j] = RowRec{at, (uint32_t)len, 0u};
+        at += (len + 127) & ~127ull;
+    }
+    if (at + DSY_BLOB_GUARD > s->lines_cap) {
+        const uint64_t cap = grown(at + DSY_BLOB_GUARD, s->lines_cap);
+        void* nl;
+        if (hipMalloc(&nl, cap) != hipSuccess) return fail(DSY_ENOMEM, "store line copy growth (%llu B)", (unsigned long long)cap);
+        HIP_TRY(hipMemcpyAsync(nl, s->d_lines, s->lines_used, hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        store_release(s, s->d_lines);
+        s->owned.push_back(nl);
+        s->d_lines = (const uint8_t*)nl;
+        s->lines_cap = cap;
+    }
+    HIP_TRY(hipMemsetAsync(const_cast<uint8_t*>(s->d_lines) + s->lines_used, 0, at + DSY_BLOB_GUARD - s->lines_used,
+                           c->stream));
+    if (n0 + a > s->rec_cap) {
+        const uint64_t cap = grown(n0 + a, s->rec_cap);
+        void* nr;
+        if (hipMalloc(&nr, cap * sizeof(RowRec)) != hipSuccess) return fail(DSY_ENOMEM, "store row records growth");
+        HIP_TRY(hipMemcpyAsync(nr, s->d_rec, n0 * sizeof(RowRec), hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        store_release(s, s->d_rec);
+        s->owned.push_back(nr);
+        s->d_rec = (const RowRec*)nr;
+        s->rec_cap = cap;
+    }
+
+    // staged uploads: new offsets, records and index rows in one workspace
+    const size_t b_off = a * 8, b_rec = a * sizeof(RowRec), b_rows = a * sizeof(IngestRow);
+    void* d_up;
+    if ((rc = ws_get(c, "ingest", b_off + b_rec + b_rows + a * 8, &d_up))) return rc;
+    uint8_t* up = (uint8_t*)d_up;
+    HIP_TRY(hipMemcpyAsync(up, noff.data(), b_off, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(up + b_off, nrec.data(), b_rec, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(up + b_off + b_rec, rows.data(), b_rows, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(const_cast<uint64_t*>(s->d_offsets) + n0 + 1, up, b_off, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(const_cast<RowRec*>(s->d_rec) + n0, up + b_off, b_rec, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(launch_store_lines(s->d_blob, s->d_offsets + n0, s->d_rec + n0, a, const_cast<uint8_t*>(s->d_lines),
+                               c->stream));
+
+    // the live index, merged into fresh buffers (the old ones are read by the merge)
+    // (double-buffered: the previous append's index becomes the next one's target, so a steady stream of appends
+    // allocates nothing)
+    const uint64_t live = s->n_live + a;
+    if (s->spare_cap < live) {
+        store_release(s, s->spare_gt);
+        store_release(s, s->spare_row);
+        s->spare_gt = s->spare_row = nullptr;
+        s->spare_cap = 0;
+        const uint64_t cap = grown(live, s->n_live);
+        void *pg, *pr;
+        if (hipMalloc(&pg, cap * 8) != hipSuccess) return fail(DSY_ENOMEM, "store live index growth");
+        s->owned.push_back(pg);
+        if (hipMalloc(&pr, cap * 8) != hipSuccess) { store_release(s, pg); return fail(DSY_ENOMEM, "store live index growth"); }
+        s->owned.push_back(pr);
+        s->spare_gt = (uint64_t*)pg;
+        s->spare_row = (uint64_t*)pr;
+        s->spare_cap = cap;
+    }
+    HIP_TRY(launch_ingest_merge(s->d_live_gt, s->d_live_row, s->n_live, (const IngestRow*)(up + b_off + b_rec), a,
+                                (uint64_t*)(up + b_off + b_rec + b_rows), s->spare_gt, s->spare_row, c->max_grid,
+                                c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    uint64_t* prev_gt = const_cast<uint64_t*>(s->d_live_gt);
+    uint64_t* prev_row = const_cast<uint64_t*>(s->d_live_row);
+    const uint64_t prev_cap = s->live_cap;
+    s->d_live_gt = s->spare_gt;
+    s->d_live_row = s->spare_row;
+    s->live_cap = s->spare_cap;
+    if (prev_cap) {  // the index an earlier append built: the next target
+        s->spare_gt = prev_gt;
+        s->spare_row = prev_row;
+        s->spare_cap = prev_cap;
+    } else {         // the index of the upload/attach (possibly the caller's global_time column)
+        store_release(s, prev_gt);
+        store_release(s, prev_row);
+        s->spare_gt = s->spare_row = nullptr;
+        s->spare_cap = 0;
+    }
+
+    // segments: a meta's segment moves by the new rows of smaller metas and grows by its own
+    std::map<uint32_t, uint64_t> cnt;
+    for (uint64_t j = 0; j < a; ++j) ++cnt[meta[j]];
+    for (auto& e : s->segs) {
+        uint64_t before = 0;
+        for (auto& m : cnt)
+            if (m.first < e.first) before += m.second;
+        auto own = cnt.find(e.first);
+        e.second.first += before;
+        e.second.second += before + (own == cnt.end() ? 0 : own->second);
+    }
+    for (auto& m : cnt) {
+        if (s->segs.count(m.first)) continue;
+        uint64_t start = 0;
+        for (auto& e : old)
+            if (e.first < m.first) start = std::max(start, e.second.second);
+        for (auto& m2 : cnt)
+            if (m2.first < m.first) start += m2.second;
+        s->segs[m.first] = {start, start + m.second};
+    }
+    s->min_len = n0 ? std::min(s->min_len, minlen) : minlen;
+    s->n += a;
+    s->n_live = live;
+    s->blob_len += add;
+    s->lines_used = at;
+    return DSY_OK;
+}
 
 int dsy_bloom_add_rows(dsy_ctx* c, const dsy_bloom_params* p, const dsy_store* s, const uint64_t* rows, uint64_t n,
                        uint8_t* filter_inout) {

@@ -179,6 +179,18 @@ hipError_t launch_pack(const RespondLaunch& L, uint64_t* packed, uint64_t* packe
 hipError_t launch_store_lines(const uint8_t* blob, const uint64_t* offsets, const RowRec* rec, uint64_t n,
                               uint8_t* lines, hipStream_t stream);
 
+// ------------------------------------------------------------------------------- ingest (dsy_store_append)
+// One appended row, the rows in (meta, global_time, rowid) order: its meta's live segment [seg_a, seg_b) in the old
+// index ([x, x) at the meta's place when the meta is new) and its store row.
+struct IngestRow {
+    uint64_t gt, seg_a, seg_b, row;
+};
+// merge the appended rows into the live index: (live_gt, live_row | identity)[n_live] + rows[a] ->
+// (out_gt, out_row)[n_live + a]; rank[a] is scratch
+hipError_t launch_ingest_merge(const uint64_t* live_gt, const uint64_t* live_row, uint64_t n_live,
+                               const IngestRow* rows, uint64_t a, uint64_t* rank, uint64_t* out_gt, uint64_t* out_row,
+                               uint32_t max_grid, hipStream_t stream);
+
 // ---------------------------------------------------------------------------------------- simulator
 static constexpr uint32_t kSimFilterWordsMax = 2048;  // m <= 65536 bits
 static constexpr uint32_t kSimRespMax = DSY_SIM_RESP_MAX;

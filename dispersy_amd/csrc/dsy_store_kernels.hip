@@ -1,0 +1,96 @@
+// Requester-side ingest into the packed store: `Dispersy._store` INSERTs every received sync
+// packet into the `sync` table (dispersy.py:1475-1612); the responder serves it from then on through the
+// `sync_meta_message_undone_global_time_index` (dispersydatabase.py:63).  Here the new rows take the next row
+// positions and the store's live index -- live_gt/live_row in (meta_message, global_time, rowid) order -- is merged
+// on the device:
+//   k_ingest_rank       one lane per new row (in index order): upper bound of its global time in its meta's live
+//                       segment = how many old live rows precede it (equal global times: the old row first, it has
+//                       the smaller rowid).
+//   k_ingest_merge_old  one lane per old live row: shift by the number of new rows ranked at or before it.  Each
+//                       workgroup bounds its tile's shifts with two searches, so most lanes search an empty range.
+//   k_ingest_merge_new  one lane per new row: its place is rank + index.
+// Every output slot is written exactly once; reads and writes of the old index stream (16 B in, 16 B out per row).
+#include "dsy_kernels.h"
+
+namespace dsy {
+
+static constexpr uint32_t kIngestThreads = 256;
+static constexpr uint32_t kIngestPerThread = 4;
+static constexpr uint64_t kIngestTile = (uint64_t)kIngestThreads * kIngestPerThread;
+
+__global__ void __launch_bounds__(kIngestThreads) k_ingest_rank(const uint64_t* __restrict__ live_gt,
+                                                                 const IngestRow* __restrict__ rows, uint64_t a,
+                                                                 uint64_t* __restrict__ rank) {
+    const uint64_t j = (uint64_t)blockIdx.x * kIngestThreads + threadIdx.x;
+    if (j >= a) return;
+    const IngestRow r = rows[j];
+    uint64_t lo = r.seg_a, hi = r.seg_b;
+    while (lo < hi) {
+        const uint64_t mid = lo + ((hi - lo) >> 1);
+        if (live_gt[mid] <= r.gt) lo = mid + 1; else hi = mid;
+    }
+    rank[j] = lo;
+}
+
+// number of j in [lo, hi) with rank[j] <= i (rank is non-decreasing)
+__device__ __forceinline__ uint64_t ranks_at_or_before(const uint64_t* __restrict__ rank, uint64_t lo, uint64_t hi,
+                                                       uint64_t i) {
+    while (lo < hi) {
+        const uint64_t mid = lo + ((hi - lo) >> 1);
+        if (rank[mid] <= i) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(kIngestThreads) k_ingest_merge_old(const uint64_t* __restrict__ live_gt,
+                                                                      const uint64_t* __restrict__ live_row,
+                                                                      uint64_t n_live, const uint64_t* __restrict__ rank,
+                                                                      uint64_t a, uint64_t* __restrict__ out_gt,
+                                                                      uint64_t* __restrict__ out_row) {
+    __shared__ uint64_t bound[2];
+    for (uint64_t t0 = (uint64_t)blockIdx.x * kIngestTile; t0 < n_live; t0 += (uint64_t)gridDim.x * kIngestTile) {
+        const uint64_t t1 = t0 + kIngestTile < n_live ? t0 + kIngestTile : n_live;
+        __syncthreads();  // the previous tile's bounds are consumed
+        if (threadIdx.x < 2) bound[threadIdx.x] = ranks_at_or_before(rank, 0, a, threadIdx.x ? t1 - 1 : t0);
+        __syncthreads();
+        const uint64_t s0 = bound[0], s1 = bound[1];
+#pragma unroll
+        for (uint32_t u = 0; u < kIngestPerThread; ++u) {
+            const uint64_t i = t0 + (uint64_t)u * kIngestThreads + threadIdx.x;
+            if (i < t1) {
+                const uint64_t shift = s0 == s1 ? s0 : ranks_at_or_before(rank, s0, s1, i);
+                out_gt[i + shift] = live_gt[i];
+                out_row[i + shift] = live_row ? live_row[i] : i;
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kIngestThreads) k_ingest_merge_new(const IngestRow* __restrict__ rows, uint64_t a,
+                                                                      const uint64_t* __restrict__ rank,
+                                                                      uint64_t* __restrict__ out_gt,
+                                                                      uint64_t* __restrict__ out_row) {
+    const uint64_t j = (uint64_t)blockIdx.x * kIngestThreads + threadIdx.x;
+    if (j >= a) return;
+    const IngestRow r = rows[j];
+    out_gt[rank[j] + j] = r.gt;
+    out_row[rank[j] + j] = r.row;
+}
+
+hipError_t launch_ingest_merge(const uint64_t* live_gt, const uint64_t* live_row, uint64_t n_live,
+                               const IngestRow* rows, uint64_t a, uint64_t* rank, uint64_t* out_gt, uint64_t* out_row,
+                               uint32_t max_grid, hipStream_t stream) {
+    if (!a) return hipSuccess;
+    const uint32_t gnew = (uint32_t)((a + kIngestThreads - 1) / kIngestThreads);
+    hipLaunchKernelGGL(k_ingest_rank, dim3(gnew), dim3(kIngestThreads), 0, stream, live_gt, rows, a, rank);
+    if (n_live) {
+        uint64_t g = (n_live + kIngestTile - 1) / kIngestTile;
+        if (g > (uint64_t)max_grid * 4) g = (uint64_t)max_grid * 4;
+        hipLaunchKernelGGL(k_ingest_merge_old, dim3((uint32_t)g), dim3(kIngestThreads), 0, stream, live_gt, live_row,
+                           n_live, rank, a, out_gt, out_row);
+    }
+    hipLaunchKernelGGL(k_ingest_merge_new, dim3(gnew), dim3(kIngestThreads), 0, stream, rows, a, rank, out_gt, out_row);
+    return hipGetLastError();
+}
+
+}  // namespace dsy

@@ -9,6 +9,11 @@ Rows are kept in the order of the reference's `sync_meta_message_undone_global_t
 The device copy (dsy_store_upload) holds blob/offsets plus a live-row index (undone == 0) with per-meta
 segments; the host copy of the small columns serves the claim-side range selection
 (community.py:881-933) and maps responder output rows back to packets.
+
+`append` is the requester-side ingest (`INSERT INTO sync` of Dispersy._store, dispersy.py:1475-1612): received
+packets take the next row positions, in insertion (rowid) order, and join the index by (meta_message,
+global_time, rowid) -- on the device by dsy_store_append's merge, on the host per meta.  Rows past the constructor's
+are therefore no longer in index order; `live_rows` always is.
 """
 import ctypes
 
@@ -36,6 +41,7 @@ class SyncStore(object):
                 raise ValueError("SyncStore rows must be sorted by (meta_message, global_time, rowid)")
         self._ctx = ctx
         self._handle = None
+        self._n_sorted = self.n  # rows in index order, uploaded by dsy_store_upload; later rows are appends
         self._row_of_id = None
         # live (undone == 0) rows per meta, in global_time order: the claim side's index range scans
         live = np.flatnonzero(self.undone == 0)
@@ -93,6 +99,55 @@ class SyncStore(object):
     def count_live(self, meta_ids):
         return int(sum(len(self.live_rows(m)) for m in meta_ids))
 
+    # ------------------------------------------------------------------------------------------ ingest
+    def append(self, packets, global_time, meta, rowid=None):
+        """INSERT INTO sync of a batch of received packets (dispersy.py:1475-1612), undone = 0.
+
+        packets: list of bytes; global_time / meta: one per packet; rowid: increasing ids above every stored one
+        (default: the next ids, as SQLite assigns them).  Returns the new rows' positions.  When the store is on
+        the device already, the batch goes there in one dsy_store_append call."""
+        a = len(packets)
+        gts = np.ascontiguousarray(global_time, dtype=np.uint64)
+        metas = np.ascontiguousarray(meta, dtype=np.uint32)
+        if len(gts) != a or len(metas) != a:
+            raise ValueError("append: one global_time and one meta per packet")
+        top = int(self.rowid.max()) if self.n else 0
+        ids = (np.arange(top + 1, top + 1 + a, dtype=np.int64) if rowid is None
+               else np.ascontiguousarray(rowid, dtype=np.int64))
+        if len(ids) != a or (a and (ids[0] <= top or (a > 1 and (ids[1:] <= ids[:-1]).any()))):
+            raise ValueError("append: rowids must increase and exceed every stored rowid")
+        rows = np.arange(self.n, self.n + a, dtype=np.int64)
+        if a == 0:
+            return rows
+        lens = np.fromiter((len(p) for p in packets), dtype=np.uint64, count=a)
+        new_off = np.zeros(a + 1, dtype=np.uint64)
+        np.cumsum(lens, out=new_off[1:])
+        data = b"".join(bytes(p) for p in packets)
+        if self._handle is not None:
+            lib = self.ctx.lib
+            _native.check(lib.dsy_store_append(self.ctx.handle, self._handle, data, len(data), new_off.ctypes.data, a,
+                                               gts.ctypes.data, metas.ctypes.data))
+        # host columns
+        base = self.offsets[-1]
+        self.offsets = np.concatenate([self.offsets, base + new_off[1:]])
+        if isinstance(self.blob, np.ndarray):
+            self.blob = np.concatenate([self.blob, np.frombuffer(data, dtype=np.uint8)])
+        else:
+            if not isinstance(self.blob, bytearray):
+                self.blob = bytearray(self.blob)
+            self.blob += data
+        self.global_time = np.concatenate([self.global_time, gts])
+        self.meta = np.concatenate([self.meta, metas])
+        self.undone = np.concatenate([self.undone, np.zeros(a, dtype=np.uint8)])
+        self.rowid = np.concatenate([self.rowid, ids])
+        self.n += a
+        self._row_of_id = None
+        # per-meta live rows: old rows first on equal global times (smaller rowid), new ones in insertion order
+        for m in np.unique(metas):
+            seg = np.concatenate([self._live.get(int(m), self._empty).astype(np.int64), rows[metas == m]])
+            self._live[int(m)] = seg[np.argsort(self.global_time[seg], kind="stable")]
+        return rows
+
     # ------------------------------------------------------------------------------------------ device
     @property
     def ctx(self):
@@ -107,10 +162,17 @@ class SyncStore(object):
             ctx = self.ctx
             blob = self.blob if isinstance(self.blob, bytes) else bytes(self.blob)
             h = ctypes.c_void_p()
-            _native.check(ctx.lib.dsy_store_upload(ctx.handle, blob, len(blob), self.offsets.ctypes.data, self.n,
+            n0 = self._n_sorted
+            blob0 = blob[:int(self.offsets[n0])] if n0 < self.n else blob
+            _native.check(ctx.lib.dsy_store_upload(ctx.handle, blob0, len(blob0), self.offsets.ctypes.data, n0,
                                                    self.global_time.ctypes.data, self.meta.ctypes.data,
                                                    self.undone.ctypes.data, ctypes.byref(h)))
             self._handle = h
+            if n0 < self.n:  # rows appended before the first upload: the same merge as a live append
+                off = np.ascontiguousarray(self.offsets[n0:] - self.offsets[n0])
+                tail = blob[int(self.offsets[n0]):]
+                _native.check(ctx.lib.dsy_store_append(ctx.handle, h, tail, len(tail), off.ctypes.data, self.n - n0,
+                                                       self.global_time[n0:].ctypes.data, self.meta[n0:].ctypes.data))
         return self._handle
 
     def close(self):

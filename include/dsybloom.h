@@ -164,6 +164,14 @@ int dsy_store_attach(dsy_ctx* ctx, const uint8_t* d_blob, uint64_t blob_len, con
                      const uint64_t* d_global_time, const uint32_t* d_meta, const uint8_t* d_undone, dsy_store** out);
 int dsy_store_free(dsy_store* store);
 uint64_t dsy_store_rows(const dsy_store* store);
+/* Requester-side ingest: replaces `INSERT INTO sync (...)` of Dispersy._store (dispersy.py:1475-1612) for a batch
+ * of a received packets (host buffers, any order; undone = 0).  The new rows take row positions n .. n+a-1 in
+ * argument order (so they keep the rowid order of the inserts) and enter the responder's index by
+ * (meta_message, global_time, rowid): a new row follows every stored row with the same meta and global time.
+ * The device buffers grow by >= 1.25x when full (copied once); an attached store's caller buffers are left as they
+ * were and are no longer read.  The index merge is O(n + a) HBM traffic on the device. */
+int dsy_store_append(dsy_ctx* ctx, dsy_store* store, const uint8_t* blob, uint64_t blob_len, const uint64_t* offsets,
+                     uint64_t a, const uint64_t* global_time, const uint32_t* meta);
 
 /* Claim side (community.py:821, :924 and dispersy_store :698): OR the packets of the given store rows into a
  * filter.  rows are store row positions (0-based, export order). */

@@ -11,10 +11,30 @@ Restated functions (reference file:line):
   select_range         community.py:839-879
   claim_largest        community.py:763-837
   claim_modulo         community.py:908-933
+  insert_packets       dispersy.py:1523-1533 (Dispersy._store's INSERT INTO sync, one execute per message)
+  SYNC_SCHEMA          dispersydatabase.py:53-64 (the sync table and its (meta_message, undone, global_time) index)
 """
 import math
 
 MAX_GT = 2 ** 63 - 1
+
+SYNC_SCHEMA = """
+CREATE TABLE sync(id INTEGER PRIMARY KEY AUTOINCREMENT, community INTEGER, member INTEGER, global_time INTEGER,
+                  meta_message INTEGER, undone INTEGER DEFAULT 0, packet BLOB, sequence INTEGER,
+                  UNIQUE(community, member, global_time));
+CREATE INDEX sync_mug ON sync(meta_message, undone, global_time);
+"""
+
+
+def insert_packets(conn, community, rows):
+    """Dispersy._store's INSERT (dispersy.py:1523-1533): one statement per message, in message order.
+    rows: iterable of (member, global_time, meta_message, packet).  Returns the new row ids (lastrowid)."""
+    ids = []
+    for member, gt, meta, packet in rows:
+        cur = conn.execute("INSERT INTO sync (community, member, global_time, meta_message, packet, sequence) "
+                           "VALUES (?, ?, ?, ?, ?, ?)", (community, member, gt, meta, packet, None))
+        ids.append(cur.lastrowid)
+    return ids
 
 
 def syncable(metas):

@@ -37,12 +37,7 @@ def keys_for(spec):
     raise ValueError(kind)
 
 
-SYNC_SCHEMA = """
-CREATE TABLE sync(id INTEGER PRIMARY KEY AUTOINCREMENT, community INTEGER, member INTEGER, global_time INTEGER,
-                  meta_message INTEGER, undone INTEGER DEFAULT 0, packet BLOB, sequence INTEGER,
-                  UNIQUE(community, member, global_time));
-CREATE INDEX sync_mug ON sync(meta_message, undone, global_time);
-"""
+from oracle.sync_ref import SYNC_SCHEMA  # noqa: E402  (dispersydatabase.py:53-64)
 
 
 def sqlite_from_rows(rows):
