@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--byte-limit", type=int, default=5120)
     ap.add_argument("--cpu-claims", type=int, default=96, help="claims in the CPU-baseline sample (0: skip)")
     ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--window", type=int, default=0, help="cap on the responder's window (pairs per claim; 0: default)")
     ap.add_argument("--sim-peers", type=int, default=1_000_000, help="config 3 gossip simulator peers (0: skip)")
     ap.add_argument("--sim-universe", type=int, default=10_000)
     ap.add_argument("--sim-initial", type=int, default=100)
@@ -138,6 +139,8 @@ def main():
     metas[0].meta_id, metas[0].direction = 1, _native.DSY_ASC
 
     p_out, p_off, pairs = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+    if args.window:
+        ctx.set_window(args.window)
 
     def step():
         _native.check(lib.dsy_sync_respond_dev(ctx.handle, store, reqs, R, d_filters.data_ptr(), metas, 1, N, 0,
@@ -655,6 +658,8 @@ def heavy_tail(args, ctx, lib, dev, rank, world, dist):
     metas = (_native.Meta * 1)()
     metas[0].meta_id, metas[0].direction = 1, _native.DSY_ASC
     p_out, p_off, pairs = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+    if args.window:
+        ctx.set_window(args.window)
 
     def step():
         _native.check(lib.dsy_sync_respond_dev(ctx.handle, store, reqs, R, d_filters.data_ptr(), metas, 1, G_MAX, 0,

@@ -129,6 +129,7 @@ struct SegMeta {          // one syncable meta in serving order, resolved agains
     uint64_t inactive;
 };
 
+enum { kFlagChunks = 0 };
 struct RespondLaunch {
     StoreView st;
     const DevRequest* reqs;   // device [R]
@@ -156,7 +157,8 @@ struct RespondLaunch {
     PairTask* task;           // device [R*W]: per-claim hashing order (window slots sorted by block count)
     uint64_t* miss_mask;      // device [n_act * W / 64]: bit t of claim slot a = window pair t is missing
     uint64_t* out;            // device [sum cap]
-    uint32_t* flags;          // device [4]: [1] an output capacity overflowed
+    uint32_t* flags;          // device [16], zeroed by k_setup: [kFlagChunks] the window's longest claim in 64-pair
+                              // chunks (k_fill atomicMax, read by k_pair_test, reset by k_compact)
     uint64_t* fill_clock;     // optional [n_act][4] s_memtime stamps of k_fill phases (DSY_FILL_PROFILE)
     uint64_t* counters;       // device [kCntSpread][kCntN]: pairs hashed, compression blocks, packet bytes, pairs the reference
                               // would have hashed (it stops at the byte limit), lane-block slots of the hashing waves

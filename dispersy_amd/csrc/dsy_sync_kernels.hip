@@ -519,6 +519,8 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
         S->sub = s;
         S->n_window = filled;
         if (j >= L.J) S->exhausted = 1;
+        // the window's longest claim, in 64-pair chunks: k_pair_test visits no chunk beyond it
+        if (filled) atomicMax(&L.flags[kFlagChunks], (uint32_t)((filled + 63) / 64));
     }
     const uint64_t clk1 = L.fill_clock ? __builtin_amdgcn_s_memtime() : 0;
     // Load balance: order this window's pairs by compression-block count (counting sort in LDS) so the 64
@@ -610,7 +612,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
                                                    uint32_t n_list) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dma_lds[];
     const uint64_t W = L.window;
-    const uint64_t waves_per_req = W / 64;
+    // chunks per claim: the window's longest claim (k_fill), not W / 64 -- a claim of ~1000 pairs in a 4096-pair
+    // window would otherwise leave 3/4 of the wave-tasks empty, each costing a dependent load chain to skip
+    const uint64_t waves_per_req = min((uint64_t)L.flags[kFlagChunks], W / 64);
     const uint64_t total_waves = (uint64_t)n_list * waves_per_req;
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t wave0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -780,6 +784,7 @@ __device__ __forceinline__ uint32_t select_bit(uint64_t w, uint32_t k) {
 // community.py:2559-2567 (send while the budget before the packet is positive; the crossing packet is sent).
 __global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
     const uint32_t a_slot = blockIdx.x;
+    if (a_slot == 0 && threadIdx.x == 0) L.flags[kFlagChunks] = 0;  // every k_pair_test of this window has run
     const uint32_t r = L.act[a_slot];
     ReqState* S = &L.state[r];
     if (S->done) {
