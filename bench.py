@@ -343,9 +343,9 @@ def ingest_bench(args, ctx, lib, store, step, pairs, N, batch=10_000, batches=10
                           enumerate(zip(crng.integers(1, N + 1, size=pre), plens))))
         conn.commit()
         data, off, gts, _ = work[1]
-        rows = [(pre + i, int(gts[i]), 1, data[int(off[i]):int(off[i + 1])]) for i in range(batch)]
+        msgs = [(pre + i, int(gts[i]), 1, data[int(off[i]):int(off[i + 1])]) for i in range(batch)]
         t0 = time.perf_counter()
-        insert_packets(conn, 1, rows)
+        insert_packets(conn, 1, msgs)
         conn.commit()
         dt = time.perf_counter() - t0
         conn.close()

@@ -22,8 +22,14 @@ __device__ __forceinline__ uint32_t len_bin(uint64_t len, const LenSort& s) {
 }
 
 __device__ __forceinline__ void key_span(const uint64_t* __restrict__ offsets, const uint64_t* __restrict__ rows,
-                                         uint64_t i, uint64_t* off, uint32_t* len) {
+                                         const RowRec* __restrict__ rec, uint64_t i, uint64_t* off, uint32_t* len) {
     const uint64_t row = rows ? rows[i] : i;
+    if (rec) {  // store rows: the packet's place in the store's line copy
+        const RowRec r = rec[row];
+        *off = r.off;
+        *len = r.len;
+        return;
+    }
     const uint64_t a = offsets[row], e = offsets[row + 1];
     *off = a;
     *len = (uint32_t)(e - a);
@@ -32,7 +38,7 @@ __device__ __forceinline__ void key_span(const uint64_t* __restrict__ offsets, c
 // ---------------------------------------------------------------------------- length-bucketed task order
 // pass 1: global histogram of bins (LDS-aggregated)
 __global__ void __launch_bounds__(256) k_len_hist(LenSort s, const uint64_t* __restrict__ offsets,
-                                                  const uint64_t* __restrict__ rows, uint64_t n,
+                                                  const uint64_t* __restrict__ rows, const RowRec* __restrict__ rec, uint64_t n,
                                                   uint32_t* __restrict__ hist) {
     __shared__ uint32_t h[kLenBins];
     for (uint32_t i = threadIdx.x; i < kLenBins; i += blockDim.x) h[i] = 0;
@@ -41,7 +47,7 @@ __global__ void __launch_bounds__(256) k_len_hist(LenSort s, const uint64_t* __r
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         uint64_t off;
         uint32_t len;
-        key_span(offsets, rows, i, &off, &len);
+        key_span(offsets, rows, rec, i, &off, &len);
         atomicAdd(&h[len_bin(len, s)], 1u);
     }
     __syncthreads();
@@ -68,7 +74,7 @@ __global__ void __launch_bounds__(kLenBins) k_len_scan(uint32_t* __restrict__ hi
 // pass 3: scatter task records; each workgroup reserves its bins' ranges with one global atomic per bin
 static constexpr uint32_t kScatterChunk = 4096;
 __global__ void __launch_bounds__(256) k_len_scatter(LenSort s, const uint64_t* __restrict__ offsets,
-                                                     const uint64_t* __restrict__ rows, uint64_t n,
+                                                     const uint64_t* __restrict__ rows, const RowRec* __restrict__ rec, uint64_t n,
                                                      uint32_t* __restrict__ base, PairTask* __restrict__ tasks) {
     __shared__ uint32_t cnt[kLenBins];
     __shared__ uint32_t at[kLenBins];
@@ -79,7 +85,7 @@ __global__ void __launch_bounds__(256) k_len_scatter(LenSort s, const uint64_t* 
         for (uint64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
             uint64_t off;
             uint32_t len;
-            key_span(offsets, rows, i, &off, &len);
+            key_span(offsets, rows, rec, i, &off, &len);
             atomicAdd(&cnt[len_bin(len, s)], 1u);
         }
         __syncthreads();
@@ -90,7 +96,7 @@ __global__ void __launch_bounds__(256) k_len_scatter(LenSort s, const uint64_t* 
         __syncthreads();
         for (uint64_t i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
             PairTask tk;
-            key_span(offsets, rows, i, &tk.off, &tk.len);
+            key_span(offsets, rows, rec, i, &tk.off, &tk.len);
             tk.slot = (uint32_t)i;
             const uint32_t b = len_bin(tk.len, s);
             tasks[at[b] + atomicAdd(&cnt[b], 1u)] = tk;
@@ -104,7 +110,7 @@ __global__ void __launch_bounds__(256) k_len_scatter(LenSort s, const uint64_t* 
 template <class H, int CHUNK, int OP, bool DMA>
 __global__ void __launch_bounds__(256) k_bloom(const DevParams* __restrict__ prm, const uint8_t* __restrict__ blob,
                                                const uint64_t* __restrict__ offsets, const uint64_t* __restrict__ rows,
-                                               const PairTask* __restrict__ tasks, uint64_t n,
+                                               const RowRec* __restrict__ rec, const PairTask* __restrict__ tasks, uint64_t n,
                                                uint32_t* __restrict__ filter, uint32_t nwords, int use_lds,
                                                uint8_t* __restrict__ present) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
@@ -123,7 +129,10 @@ __global__ void __launch_bounds__(256) k_bloom(const DevParams* __restrict__ prm
     for (uint64_t v = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; v < waves; v += wstride) {
         const uint64_t i = v * 64 + lane;
         const bool active = i < n;
-        KeyView kv{blob, 0u, prm->prefix, prm->prefix_len};  // idle lanes hash an empty key
+        // idle lanes hash an empty key; the LDS-DMA path still reads its stage from key - prefix_len, so the key
+        // must sit past readable bytes: a packed blob has DSY_BLOB_GUARD of them before it, a store's line copy
+        // (rec) keeps its guard inside the allocation
+        KeyView kv{rec ? blob + DSY_BLOB_GUARD : blob, 0u, prm->prefix, prm->prefix_len};
         uint64_t slot = i;
         if (active) {
             if (tasks) {
@@ -133,7 +142,7 @@ __global__ void __launch_bounds__(256) k_bloom(const DevParams* __restrict__ prm
                 slot = tk.slot;
             } else {
                 uint64_t off;
-                key_span(offsets, rows, i, &off, &kv.len);
+                key_span(offsets, rows, rec, i, &off, &kv.len);
                 kv.key = blob + off;
             }
         }
@@ -225,17 +234,17 @@ hipError_t launch_or_reduce(const uint32_t* parts, uint32_t n_parts, uint64_t wo
 }
 
 // ------------------------------------------------------------------------------------------ dispatch
-hipError_t launch_len_sort(const LenSort& s, const uint64_t* offsets, const uint64_t* rows, uint64_t n,
+hipError_t launch_len_sort(const LenSort& s, const uint64_t* offsets, const uint64_t* rows, const RowRec* rec, uint64_t n,
                            uint32_t* d_bins, PairTask* d_tasks, uint32_t max_grid, hipStream_t stream) {
     hipError_t e = hipMemsetAsync(d_bins, 0, kLenBins * 4, stream);
     if (e != hipSuccess) return e;
     const uint64_t want = (n + 255) / 256;
     const uint32_t grid = (uint32_t)(want < max_grid ? (want ? want : 1) : max_grid);
-    hipLaunchKernelGGL(k_len_hist, dim3(grid), dim3(256), 0, stream, s, offsets, rows, n, d_bins);
+    hipLaunchKernelGGL(k_len_hist, dim3(grid), dim3(256), 0, stream, s, offsets, rows, rec, n, d_bins);
     hipLaunchKernelGGL(k_len_scan, dim3(1), dim3(kLenBins), 0, stream, d_bins);
     const uint64_t chunks = (n + kScatterChunk - 1) / kScatterChunk;
     const uint32_t sgrid = (uint32_t)(chunks < max_grid ? (chunks ? chunks : 1) : max_grid);
-    hipLaunchKernelGGL(k_len_scatter, dim3(sgrid), dim3(256), 0, stream, s, offsets, rows, n, d_bins, d_tasks);
+    hipLaunchKernelGGL(k_len_scatter, dim3(sgrid), dim3(256), 0, stream, s, offsets, rows, rec, n, d_bins, d_tasks);
     return hipGetLastError();
 }
 
@@ -248,10 +257,10 @@ static hipError_t launch_op(const BloomLaunch& L, uint32_t grid) {
     if (dma) {
         if constexpr (H::block_bytes == 64)
             hipLaunchKernelGGL((k_bloom<H, CHUNK, OP, true>), dim3(grid), dim3(256), lds, L.stream, L.prm, L.blob,
-                               L.offsets, L.rows, L.tasks, L.n, L.filter, L.nwords, L.use_lds, L.present);
+                               L.offsets, L.rows, L.rec, L.tasks, L.n, L.filter, L.nwords, L.use_lds, L.present);
     } else {
         hipLaunchKernelGGL((k_bloom<H, CHUNK, OP, false>), dim3(grid), dim3(256), lds, L.stream, L.prm, L.blob,
-                           L.offsets, L.rows, L.tasks, L.n, L.filter, L.nwords, L.use_lds, L.present);
+                           L.offsets, L.rows, L.rec, L.tasks, L.n, L.filter, L.nwords, L.use_lds, L.present);
     }
     return hipGetLastError();
 }

@@ -85,8 +85,6 @@ struct dsy_store {
     std::vector<void*> owned;
     std::unordered_map<uint32_t, std::pair<uint64_t, uint64_t>> segs;
     // capacities for dsy_store_append (0: exactly the built size)
-    uint64_t blob_cap = 0;    // bytes usable at d_blob (a DSY_BLOB_GUARD tail follows)
-    uint64_t off_cap = 0;     // entries of d_offsets
     uint64_t lines_used = 0;  // bytes of d_lines in use (front guard + line-aligned packets)
     uint64_t lines_cap = 0;   // bytes of d_lines (the tail guard included)
     uint64_t rec_cap = 0;     // entries of d_rec
@@ -260,7 +258,8 @@ int stage_keys(dsy_ctx* c, const uint8_t* blob, uint64_t blob_len, const uint64_
 }
 
 int run_bloom(dsy_ctx* c, BloomOp op, const dsy_bloom_params* p, const uint8_t* d_blob, const uint64_t* d_off,
-              const uint64_t* d_rows, uint64_t n, uint32_t* d_filter, uint8_t* d_present, uint64_t* d_idx) {
+              const uint64_t* d_rows, uint64_t n, uint32_t* d_filter, uint8_t* d_present, uint64_t* d_idx,
+              const RowRec* d_rec = nullptr) {
     DevParams* dp;
     int rc = upload_params(c, p, &dp);
     if (rc) return rc;
@@ -274,6 +273,7 @@ int run_bloom(dsy_ctx* c, BloomOp op, const dsy_bloom_params* p, const uint8_t* 
     L.blob = d_blob;
     L.offsets = d_off;
     L.rows = d_rows;
+    L.rec = d_rec;
     L.n = n;
     L.filter = d_filter;
     L.nwords = (uint32_t)filter_words(p->m_bits);
@@ -291,7 +291,7 @@ int run_bloom(dsy_ctx* c, BloomOp op, const dsy_bloom_params* p, const uint8_t* 
         if ((rc2 = ws_get(c, "len_tasks", n * sizeof(PairTask), &tasks))) return rc2;
         const bool wide = p->hash_kind >= DSY_SHA384;
         LenSort ls{p->prefix_len, wide ? 128u : 64u, wide ? 16u : 8u};
-        HIP_TRY(launch_len_sort(ls, d_off, d_rows, n, (uint32_t*)bins, (PairTask*)tasks, c->max_grid, c->stream));
+        HIP_TRY(launch_len_sort(ls, d_off, d_rows, d_rec, n, (uint32_t*)bins, (PairTask*)tasks, c->max_grid, c->stream));
         L.tasks = (const PairTask*)tasks;
     }
     PendingTimer t;
@@ -602,6 +602,20 @@ static int store_build_lines(dsy_ctx* c, dsy_store* s, const uint64_t* h_off) {
     return DSY_OK;
 }
 
+// The packed blob/offsets only feed the line copy; free them when they are ours.
+static void store_release_raw(dsy_store* s) {
+    if (s->d_blob) {
+        auto it = std::find(s->owned.begin(), s->owned.end(), (const void*)(s->d_blob - DSY_BLOB_GUARD));
+        if (it != s->owned.end()) { hipFree(*it); s->owned.erase(it); }
+    }
+    if (s->d_offsets) {
+        auto it = std::find(s->owned.begin(), s->owned.end(), (const void*)s->d_offsets);
+        if (it != s->owned.end()) { hipFree(*it); s->owned.erase(it); }
+    }
+    s->d_blob = nullptr;
+    s->d_offsets = nullptr;
+}
+
 int dsy_store_upload(dsy_ctx* c, const uint8_t* blob, uint64_t blob_len, const uint64_t* offsets, uint64_t n,
                      const uint64_t* global_time, const uint32_t* meta, const uint8_t* undone, dsy_store** out) {
     if (!c || !out || !offsets || (n && (!global_time || !meta))) return fail(DSY_EINVAL, "NULL argument");
@@ -627,10 +641,10 @@ int dsy_store_upload(dsy_ctx* c, const uint8_t* blob, uint64_t blob_len, const u
     HIP_TRY(hipMemcpyAsync(po, offsets, (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
     s->d_blob = (uint8_t*)pb;
     s->d_offsets = (uint64_t*)po;
-    s->blob_cap = blob_len;
-    s->off_cap = n + 1;
     if ((rc = store_finish(c, s, global_time, nullptr, lg, lr, identity))) { dsy_store_free(s); return rc; }
     if ((rc = store_build_lines(c, s, offsets))) { dsy_store_free(s); return rc; }
+    // every kernel reads the packets from the line copy from here on: the packed upload is not kept
+    store_release_raw(s);
     *out = s;
     return DSY_OK;
 }
@@ -667,6 +681,7 @@ int dsy_store_attach(dsy_ctx* c, const uint8_t* d_blob, uint64_t blob_len, const
     }
     if ((rc = store_finish(c, s, nullptr, d_global_time, lg, lr, identity))) { dsy_store_free(s); return rc; }
     if ((rc = store_build_lines(c, s, off.data()))) { dsy_store_free(s); return rc; }
+    store_release_raw(s);  // the caller's buffers: no longer read
     *out = s;
     return DSY_OK;
 }
@@ -687,10 +702,6 @@ uint64_t dsy_store_rows(const dsy_store* s) { return s ? s->n : 0; }
 
 // ------------------------------------------------------------------------------------------------ ingest
 namespace {
-
-bool store_owns(const dsy_store* s, const void* p) {
-    return std::find(s->owned.begin(), s->owned.end(), p) != s->owned.end();
-}
 
 void store_release(dsy_store* s, const void* p) {
     auto it = std::find(s->owned.begin(), s->owned.end(), p);
@@ -740,41 +751,7 @@ int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blo
         minlen = std::min(minlen, offsets[j + 1] - offsets[j]);
     }
 
-    // raw blob + offsets (dsy_bloom_add_rows reads them): grow into buffers of our own, then write the new tail
     HIP_TRY(hipStreamSynchronize(c->stream));  // nothing in flight reads a buffer that is about to be replaced
-    uint8_t* d_blob = const_cast<uint8_t*>(s->d_blob);
-    const void* blob_base = s->d_blob ? s->d_blob - DSY_BLOB_GUARD : nullptr;
-    if (!store_owns(s, blob_base) || s->blob_len + add > s->blob_cap) {
-        const uint64_t cap = grown(s->blob_len + add, s->blob_len);
-        void* nb;
-        if (hipMalloc(&nb, cap + 2 * DSY_BLOB_GUARD) != hipSuccess)
-            return fail(DSY_ENOMEM, "store blob growth (%llu B)", (unsigned long long)cap);
-        HIP_TRY(hipMemsetAsync(nb, 0, DSY_BLOB_GUARD, c->stream));
-        uint8_t* nd = (uint8_t*)nb + DSY_BLOB_GUARD;
-        if (s->blob_len) HIP_TRY(hipMemcpyAsync(nd, s->d_blob, s->blob_len, hipMemcpyDeviceToDevice, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        store_release(s, blob_base);
-        s->owned.push_back(nb);
-        d_blob = nd;
-        s->d_blob = nd;
-        s->blob_cap = cap;
-    }
-    if (add) HIP_TRY(hipMemcpyAsync(d_blob + s->blob_len, blob + base0, add, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemsetAsync(d_blob + s->blob_len + add, 0, DSY_BLOB_GUARD, c->stream));
-    if (!store_owns(s, s->d_offsets) || n0 + a + 1 > s->off_cap) {
-        const uint64_t cap = grown(n0 + a + 1, n0 + 1);
-        void* no;
-        if (hipMalloc(&no, cap * 8) != hipSuccess) return fail(DSY_ENOMEM, "store offsets growth");
-        HIP_TRY(hipMemcpyAsync(no, s->d_offsets, (n0 + 1) * 8, hipMemcpyDeviceToDevice, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        store_release(s, s->d_offsets);
-        s->owned.push_back(no);
-        s->d_offsets = (const uint64_t*)no;
-        s->off_cap = cap;
-    }
-    std::vector<uint64_t> noff(a);
-    for (uint64_t j = 0; j < a; ++j) noff[j] = s->blob_len + offsets[j + 1] - base0;
-
     // the line copy the responder hashes from, and its row records
     std::vector<RowRec> nrec(a);
     uint64_t at = s->lines_used;
@@ -808,17 +785,24 @@ int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blo
         s->rec_cap = cap;
     }
 
-    // staged uploads: new offsets, records and index rows in one workspace
-    const size_t b_off = a * 8, b_rec = a * sizeof(RowRec), b_rows = a * sizeof(IngestRow);
+    // staged uploads (one workspace): the packets, their offsets, records and index rows; the packets then move to
+    // their line-aligned places
+    std::vector<uint64_t> noff(a + 1);
+    for (uint64_t j = 0; j <= a; ++j) noff[j] = offsets[j] - base0;
+    const size_t b_blob = (add + 15) / 16 * 16, b_off = (a + 1) * 8, b_rec = a * sizeof(RowRec),
+                 b_rows = a * sizeof(IngestRow);
     void* d_up;
-    if ((rc = ws_get(c, "ingest", b_off + b_rec + b_rows + a * 8, &d_up))) return rc;
+    if ((rc = ws_get(c, "ingest", b_blob + b_off + b_rec + b_rows + a * 8, &d_up))) return rc;
     uint8_t* up = (uint8_t*)d_up;
-    HIP_TRY(hipMemcpyAsync(up, noff.data(), b_off, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(up + b_off, nrec.data(), b_rec, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(up + b_off + b_rec, rows.data(), b_rows, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(const_cast<uint64_t*>(s->d_offsets) + n0 + 1, up, b_off, hipMemcpyDeviceToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(const_cast<RowRec*>(s->d_rec) + n0, up + b_off, b_rec, hipMemcpyDeviceToDevice, c->stream));
-    HIP_TRY(launch_store_lines(s->d_blob, s->d_offsets + n0, s->d_rec + n0, a, const_cast<uint8_t*>(s->d_lines),
+    uint8_t* up_off = up + b_blob;
+    uint8_t* up_rec = up_off + b_off;
+    uint8_t* up_rows = up_rec + b_rec;
+    if (add) HIP_TRY(hipMemcpyAsync(up, blob + base0, add, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(up_off, noff.data(), b_off, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(up_rec, nrec.data(), b_rec, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(up_rows, rows.data(), b_rows, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(const_cast<RowRec*>(s->d_rec) + n0, up_rec, b_rec, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(launch_store_lines(up, (const uint64_t*)up_off, s->d_rec + n0, a, const_cast<uint8_t*>(s->d_lines),
                                c->stream));
 
     // the live index, merged into fresh buffers (the old ones are read by the merge)
@@ -840,9 +824,8 @@ int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blo
         s->spare_row = (uint64_t*)pr;
         s->spare_cap = cap;
     }
-    HIP_TRY(launch_ingest_merge(s->d_live_gt, s->d_live_row, s->n_live, (const IngestRow*)(up + b_off + b_rec), a,
-                                (uint64_t*)(up + b_off + b_rec + b_rows), s->spare_gt, s->spare_row, c->max_grid,
-                                c->stream));
+    HIP_TRY(launch_ingest_merge(s->d_live_gt, s->d_live_row, s->n_live, (const IngestRow*)up_rows, a,
+                                (uint64_t*)(up_rows + b_rows), s->spare_gt, s->spare_row, c->max_grid, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     uint64_t* prev_gt = const_cast<uint64_t*>(s->d_live_gt);
     uint64_t* prev_row = const_cast<uint64_t*>(s->d_live_row);
@@ -904,7 +887,9 @@ int dsy_bloom_add_rows(dsy_ctx* c, const dsy_bloom_params* p, const dsy_store* s
     HIP_TRY(hipMemsetAsync(df, 0, words * 4, c->stream));
     HIP_TRY(hipMemcpyAsync(df, filter_inout, nbytes, hipMemcpyHostToDevice, c->stream));
     if (n) HIP_TRY(hipMemcpyAsync(dr, rows, n * 8, hipMemcpyHostToDevice, c->stream));
-    if ((rc = run_bloom(c, BloomOp::Add, p, s->d_blob, s->d_offsets, (uint64_t*)dr, n, (uint32_t*)df, nullptr, nullptr)))
+    // the packets come from the store's line copy (row -> rec[row]): the responder's own copy, grown by appends
+    if ((rc = run_bloom(c, BloomOp::Add, p, s->d_lines, nullptr, (uint64_t*)dr, n, (uint32_t*)df, nullptr, nullptr,
+                        s->d_rec)))
         return rc;
     HIP_TRY(hipMemcpyAsync(filter_inout, df, nbytes, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));

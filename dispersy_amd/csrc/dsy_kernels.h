@@ -27,6 +27,13 @@ struct __attribute__((aligned(16))) PairTask {
     uint32_t slot;
 };
 
+// A store row's packet in the line copy: starts on a 128-byte line of StoreView::lines.
+struct RowRec {
+    uint64_t off;
+    uint32_t len;
+    uint32_t pad;
+};
+
 struct BloomLaunch {
     BloomOp op;
     int kind;
@@ -36,6 +43,7 @@ struct BloomLaunch {
     const uint8_t* blob;
     const uint64_t* offsets;
     const uint64_t* rows;     // optional indirection (add by store row)
+    const RowRec* rec;        // with rows: key i is rec[rows[i]] in blob (a store's line copy); offsets unused
     const PairTask* tasks;    // optional length-bucketed order of the n keys (launch_len_sort)
     uint64_t n;
     uint32_t* filter;
@@ -55,17 +63,11 @@ hipError_t launch_or_reduce(const uint32_t* parts, uint32_t n_parts, uint64_t wo
 struct LenSort {
     uint32_t plen, blk, lenb;
 };
-hipError_t launch_len_sort(const LenSort& s, const uint64_t* offsets, const uint64_t* rows, uint64_t n,
+hipError_t launch_len_sort(const LenSort& s, const uint64_t* offsets, const uint64_t* rows, const RowRec* rec, uint64_t n,
                            uint32_t* d_bins /* 1024 */, PairTask* d_tasks, uint32_t max_grid, hipStream_t stream);
 
 // ------------------------------------------------------------------------------------------ responder
 // Store view the responder kernels read.  `live` rows are the rows with undone == 0, in index order.
-// A store row's packet in the line copy: starts on a 128-byte line of StoreView::lines.
-struct RowRec {
-    uint64_t off;
-    uint32_t len;
-    uint32_t pad;
-};
 
 struct StoreView {
     const uint8_t* blob;

@@ -633,7 +633,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         const bool active = i < n;
         const DevRequest& q = L.reqs[r];
         uint32_t t = 0;
-        KeyView kv{L.st.lines, 0u, q.prefix, q.prefix_len};  // idle lanes hash an empty key
+        KeyView kv{L.st.lines + DSY_BLOB_GUARD, 0u, q.prefix, q.prefix_len};  // idle lanes: an empty key past the guard
         if (active) {
             const PairTask tk = L.task[(uint64_t)a_slot * W + i];
             t = tk.slot;
