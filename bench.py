@@ -312,7 +312,7 @@ def ingest_bench(args, ctx, lib, store, step, pairs, N, batch=10_000, batches=10
     def append(b):
         data, off, gts, metas = b
         _native.check(lib.dsy_store_append(ctx.handle, store, data, len(data), off.ctypes.data, batch,
-                                           gts.ctypes.data, metas.ctypes.data))
+                                           gts.ctypes.data, metas.ctypes.data, None))
 
     work = [make() for _ in range(batches + 1)]
     t0 = time.perf_counter()

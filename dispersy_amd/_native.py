@@ -17,6 +17,8 @@ DSY_OK, DSY_EINVAL, DSY_EHIP, DSY_ENOMEM, DSY_ECAPACITY, DSY_EUNSORTED = 0, -1, 
 DSY_MD5, DSY_SHA1, DSY_SHA256, DSY_SHA384, DSY_SHA512 = range(5)
 HASH_KINDS = {"md5": DSY_MD5, "sha1": DSY_SHA1, "sha256": DSY_SHA256, "sha384": DSY_SHA384, "sha512": DSY_SHA512}
 DSY_ASC, DSY_DESC, DSY_RANDOM = 0, 1, 2
+# dsy_dup_check verdicts (include/dsybloom.h)
+DSY_DUP_NEW, DSY_DUP_EXACT, DSY_DUP_KEEP, DSY_DUP_REPLACE, DSY_DUP_TRIPLET = range(5)
 DIRECTIONS = {"ASC": DSY_ASC, "DESC": DSY_DESC, "RANDOM": DSY_RANDOM}
 BLOB_GUARD = 256
 SYNC_HEADER = 24  # DSY_SYNC_HEADER: '>QQHHBH' + the 1-byte prefix (conversion.py:727-728)
@@ -82,7 +84,10 @@ SIGNATURES = {
     "dsy_store_attach": (ctypes.c_int, [_P, _P, _U64, _P, _U64, _P, _P, _P, ctypes.POINTER(_P)]),
     "dsy_store_free": (ctypes.c_int, [_P]),
     "dsy_store_rows": (_U64, [_P]),
-    "dsy_store_append": (ctypes.c_int, [_P, _P, _P, _U64, _P, _U64, _P, _P]),
+    "dsy_store_append": (ctypes.c_int, [_P, _P, _P, _U64, _P, _U64, _P, _P, _P]),
+    "dsy_store_index_members": (ctypes.c_int, [_P, _P, _P, _P, _U64]),
+    "dsy_dup_check": (ctypes.c_int, [_P, _P, _P, _P, _P, _U64, _P, _U64, _P, _P, _P]),
+    "dsy_store_replace": (ctypes.c_int, [_P, _P, _P, _P, _U64, _P, _U64]),
     "dsy_bloom_add_rows": (ctypes.c_int, [_P, ctypes.POINTER(BloomParams), _P, _P, _U64, _P]),
     "dsy_sync_respond": (ctypes.c_int, [_P, _P, ctypes.POINTER(Request), _U32, _P, _U64, ctypes.POINTER(Meta), _U32,
                                         _U64, ctypes.c_int, ctypes.c_int64, _U64, _P, _U64, _P]),

@@ -33,6 +33,24 @@ MAX_GT = 2 ** 63 - 1  # sqlite's signed 64-bit ceiling (community.py:2545-2548)
 ClaimRequest = namedtuple("ClaimRequest", "time_low time_high modulo offset bloom_filter")
 
 
+class DropMessage(object):
+    """A received message the checks refuse, with the reference's reason text (message.py DropMessage)."""
+
+    def __init__(self, dropped, reason):
+        self.dropped = dropped
+        self.reason = reason
+
+
+def _member_id(message):
+    auth = getattr(message, "authentication", None)
+    return int(auth.member.database_id) if auth is not None else int(message.member)
+
+
+def _signature_length(message, default):
+    auth = getattr(message, "authentication", None)
+    return int(getattr(auth.member, "signature_length", default)) if auth is not None else default
+
+
 class SyncCache(object):
     """community.py:57-67."""
 
@@ -78,6 +96,7 @@ class SyncCommunity(object):
         self._sync_cache_skip_count = 0
         self._nrsyncpackets = 0
         self.dispersy_acceptable_global_time_range = 10000  # community.py:952-953
+        self.sent_packets = []  # (candidate, packet, reason) the checks answer with (Dispersy._send_packets)
 
     # ------------------------------------------------------------------------ plugin hooks (properties)
     @property
@@ -159,6 +178,63 @@ class SyncCommunity(object):
         if packets:
             cache.bloom_filter.add_keys(packets)
 
+    def _check_full_sync_distribution_batch(self, messages):
+        """dispersy.py:921-1065 for a FullSyncDistribution batch without sequence numbers (:1043-1063): every message
+        is returned, in (global_time, packet) order, either as itself (accept) or as DropMessage(message, reason).
+        The per-message `_is_duplicate_sync_message` lookups (:831-918) run as ONE hash join on the GPU
+        (SyncStore.dup_check); their side effects follow in order: the undo proof of an exact duplicate of an undone
+        packet is sent (recorded in self.sent_packets as (candidate, packet, reason)), and a stored packet that
+        differs only after the first signature_length bytes and compares lower is replaced (UPDATE, :903).
+        A message carries .packet, .distribution.global_time, .candidate, its member's database id
+        (.authentication.member.database_id, or .member) and signature length
+        (.authentication.member.signature_length, else the community's), and optionally .meta (its pruning)."""
+        messages = sorted(messages, key=lambda m: (m.distribution.global_time, m.packet))
+        acceptable = self.acceptable_global_time
+        out, todo, unique = [], [], set()
+        for message in messages:
+            gt = message.distribution.global_time
+            if gt > acceptable:
+                out.append(DropMessage(message, "global time is not within acceptable range"))
+                continue
+            meta = getattr(message, "meta", None)
+            pruning = meta.distribution.pruning if meta is not None else None
+            if isinstance(pruning, GlobalTimePruning) and not (self.global_time - gt < pruning.inactive_threshold):
+                out.append(DropMessage(message, "message has been pruned"))  # distribution.py:80-81
+                continue
+            key = (_member_id(message), gt)
+            if key in unique:
+                out.append(DropMessage(message, "duplicate message by member^global_time (2)"))
+                continue
+            unique.add(key)
+            out.append(message)
+            todo.append(len(out) - 1)
+        if todo:
+            checked = [out[i] for i in todo]
+            verdict, rows = self._store.dup_check([_member_id(m) for m in checked],
+                                                  [m.distribution.global_time for m in checked],
+                                                  [m.packet for m in checked],
+                                                  [_signature_length(m, self._signature_length) for m in checked])
+            replace_rows, replace_packets = [], []
+            for i, message, v, row in zip(todo, checked, verdict.tolist(), rows.tolist()):
+                if v == _native.DSY_DUP_NEW:
+                    continue
+                if v == _native.DSY_DUP_EXACT:
+                    undone = int(self._store.undone[row])
+                    if undone:
+                        try:
+                            proof = self._store.packet(self._store.row_of_id(undone))
+                        except KeyError:
+                            proof = None
+                        if proof is not None:
+                            self.sent_packets.append((message.candidate, proof, "-caused by duplicate-undo-"))
+                elif v == _native.DSY_DUP_REPLACE:
+                    replace_rows.append(row)
+                    replace_packets.append(message.packet)
+                out[i] = DropMessage(message, "duplicate message by global_time (2)")
+            if replace_rows:
+                self._store.replace_packet(replace_rows, replace_packets)
+        return out
+
     def store_messages(self, messages):
         """Dispersy._store (dispersy.py:1475-1612) for the sync table: INSERT the messages' packets (one batched
         SyncStore.append -> dsy_store_append into HBM), raise the community's global time to the highest stored one,
@@ -170,7 +246,8 @@ class SyncCommunity(object):
             return np.zeros(0, dtype=np.int64)
         metas = [m.database_id if hasattr(m, "database_id") else m.meta.database_id for m in messages]
         gts = [m.distribution.global_time for m in messages]
-        rows = self._store.append([m.packet for m in messages], gts, metas)
+        members = [_member_id(m) for m in messages] if self._store.member is not None else None
+        rows = self._store.append([m.packet for m in messages], gts, metas, member=members)
         self.update_global_time(max(gts))
         self.dispersy_store(messages)
         return rows

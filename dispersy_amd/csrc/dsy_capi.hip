@@ -89,6 +89,8 @@ struct dsy_store {
     uint64_t lines_cap = 0;   // bytes of d_lines (the tail guard included)
     uint64_t rec_cap = 0;     // entries of d_rec
     uint64_t live_cap = 0;    // entries of d_live_gt / d_live_row when they are the ingest's own buffers
+    DupSlot* dup = nullptr;   // (member, global_time) -> row table (dsy_store_index_members), or none
+    uint64_t dup_cap = 0, dup_count = 0;
     uint64_t* spare_gt = nullptr;   // the ingest's second index buffer pair (the next merge's target)
     uint64_t* spare_row = nullptr;
     uint64_t spare_cap = 0;
@@ -712,12 +714,66 @@ void store_release(dsy_store* s, const void* p) {
 
 uint64_t grown(uint64_t need, uint64_t have) { return std::max<uint64_t>(need, have + have / 4 + 4096); }
 
+// make room for the line copy to reach `at` bytes (its tail guard after); zero the bytes past what is in use
+int lines_reserve(dsy_ctx* c, dsy_store* s, uint64_t at) {
+    if (at + DSY_BLOB_GUARD > s->lines_cap) {
+        const uint64_t cap = grown(at + DSY_BLOB_GUARD, s->lines_cap);
+        void* nl;
+        if (hipMalloc(&nl, cap) != hipSuccess) return fail(DSY_ENOMEM, "store line copy growth (%llu B)", (unsigned long long)cap);
+        HIP_TRY(hipMemcpyAsync(nl, s->d_lines, s->lines_used, hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        store_release(s, s->d_lines);
+        s->owned.push_back(nl);
+        s->d_lines = (const uint8_t*)nl;
+        s->lines_cap = cap;
+    }
+    HIP_TRY(hipMemsetAsync(const_cast<uint8_t*>(s->d_lines) + s->lines_used, 0, at + DSY_BLOB_GUARD - s->lines_used,
+                           c->stream));
+    return DSY_OK;
+}
+
+// keep the (member, global_time) table at most half full: a power-of-two capacity, rehashed on growth
+int dup_reserve(dsy_ctx* c, dsy_store* s, uint64_t count) {
+    if (s->dup && count * 2 <= s->dup_cap) return DSY_OK;
+    uint64_t cap = 1024;
+    while (cap < count * 2) cap <<= 1;
+    void* nt;
+    if (hipMalloc(&nt, cap * sizeof(DupSlot)) != hipSuccess) return fail(DSY_ENOMEM, "duplicate table (%llu slots)", (unsigned long long)cap);
+    s->owned.push_back(nt);
+    HIP_TRY(hipMemsetAsync(nt, 0xff, cap * sizeof(DupSlot), c->stream));
+    if (s->dup) {
+        HIP_TRY(launch_dup_rehash(s->dup, s->dup_cap, (DupSlot*)nt, cap - 1, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        store_release(s, s->dup);
+    }
+    s->dup = (DupSlot*)nt;
+    s->dup_cap = cap;
+    return DSY_OK;
+}
+
+// insert rows first_row .. first_row+n-1 of the given (member, global_time) host arrays into the table
+int dup_insert(dsy_ctx* c, dsy_store* s, const uint64_t* member, const uint64_t* gt, uint64_t first_row, uint64_t n) {
+    int rc;
+    if (!n) return DSY_OK;
+    if ((rc = dup_reserve(c, s, s->dup_count + n))) return rc;
+    void* d;
+    if ((rc = ws_get(c, "dup_keys", n * 16, &d))) return rc;
+    HIP_TRY(hipMemcpyAsync(d, member, n * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync((uint64_t*)d + n, gt, n * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(launch_dup_insert((const uint64_t*)d, (const uint64_t*)d + n, first_row, n, s->dup, s->dup_cap - 1,
+                              c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    s->dup_count += n;
+    return DSY_OK;
+}
+
 }  // namespace
 
 int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blob_len, const uint64_t* offsets,
-                     uint64_t a, const uint64_t* gt, const uint32_t* meta) {
+                     uint64_t a, const uint64_t* gt, const uint32_t* meta, const uint64_t* member) {
     if (!c || !s || !offsets || (a && (!gt || !meta || (blob_len && !blob)))) return fail(DSY_EINVAL, "NULL argument");
     if (s->ctx != c) return fail(DSY_EINVAL, "store belongs to another context");
+    if (s->dup && a && !member) return fail(DSY_EINVAL, "the store has a (member, global_time) table: members required");
     int rc = check_offsets(offsets, a, blob_len);
     if (rc) return rc;
     if (a == 0) return DSY_OK;
@@ -760,19 +816,7 @@ int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blo
         nrec[j] = RowRec{at, (uint32_t)len, 0u};
         at += (len + 127) & ~127ull;
     }
-    if (at + DSY_BLOB_GUARD > s->lines_cap) {
-        const uint64_t cap = grown(at + DSY_BLOB_GUARD, s->lines_cap);
-        void* nl;
-        if (hipMalloc(&nl, cap) != hipSuccess) return fail(DSY_ENOMEM, "store line copy growth (%llu B)", (unsigned long long)cap);
-        HIP_TRY(hipMemcpyAsync(nl, s->d_lines, s->lines_used, hipMemcpyDeviceToDevice, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        store_release(s, s->d_lines);
-        s->owned.push_back(nl);
-        s->d_lines = (const uint8_t*)nl;
-        s->lines_cap = cap;
-    }
-    HIP_TRY(hipMemsetAsync(const_cast<uint8_t*>(s->d_lines) + s->lines_used, 0, at + DSY_BLOB_GUARD - s->lines_used,
-                           c->stream));
+    if ((rc = lines_reserve(c, s, at))) return rc;
     if (n0 + a > s->rec_cap) {
         const uint64_t cap = grown(n0 + a, s->rec_cap);
         void* nr;
@@ -864,11 +908,102 @@ int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blo
             if (m2.first < m.first) start += m2.second;
         s->segs[m.first] = {start, start + m.second};
     }
+    if (s->dup && (rc = dup_insert(c, s, member, gt, n0, a))) return rc;
     s->min_len = n0 ? std::min(s->min_len, minlen) : minlen;
     s->n += a;
     s->n_live = live;
     s->blob_len += add;
     s->lines_used = at;
+    return DSY_OK;
+}
+
+int dsy_store_index_members(dsy_ctx* c, dsy_store* s, const uint64_t* member, const uint64_t* gt, uint64_t n) {
+    if (!c || !s || (n && (!member || !gt))) return fail(DSY_EINVAL, "NULL argument");
+    if (s->ctx != c) return fail(DSY_EINVAL, "store belongs to another context");
+    if (n != s->n) return fail(DSY_EINVAL, "%llu members for a store of %llu rows", (unsigned long long)n, (unsigned long long)s->n);
+    Guard g(c);
+    if (s->dup) {  // rebuild from scratch
+        store_release(s, s->dup);
+        s->dup = nullptr;
+        s->dup_cap = s->dup_count = 0;
+    }
+    int rc = dup_reserve(c, s, n);
+    if (rc) return rc;
+    return dup_insert(c, s, member, gt, 0, n);
+}
+
+int dsy_dup_check(dsy_ctx* c, const dsy_store* s, const uint64_t* member, const uint64_t* gt, const uint8_t* blob,
+                  uint64_t blob_len, const uint64_t* offsets, uint64_t m, const uint32_t* sig_len, uint8_t* out_verdict,
+                  uint64_t* out_row) {
+    if (!c || !s || !offsets || (m && (!member || !gt || !sig_len || !out_verdict || !out_row || (blob_len && !blob))))
+        return fail(DSY_EINVAL, "NULL argument");
+    if (!s->dup) return fail(DSY_EINVAL, "the store has no (member, global_time) table (dsy_store_index_members)");
+    int rc = check_offsets(offsets, m, blob_len);
+    if (rc) return rc;
+    if (!m) return DSY_OK;
+    Guard g(c);
+    const uint64_t base0 = offsets[0], add = offsets[m] - base0;
+    std::vector<uint64_t> noff(m + 1);
+    for (uint64_t j = 0; j <= m; ++j) noff[j] = offsets[j] - base0;
+    const size_t b_blob = (add + 15) / 16 * 16, b_k = m * 8, b_off = (m + 1) * 8, b_sl = (m * 4 + 15) / 16 * 16,
+                 b_v = (m + 15) / 16 * 16;
+    void* d;
+    if ((rc = ws_get(c, "dup_check", b_blob + 2 * b_k + b_off + b_sl + b_v + b_k, &d))) return rc;
+    uint8_t* p = (uint8_t*)d;
+    uint8_t *d_blob = p, *d_mem = p + b_blob, *d_gt = d_mem + b_k, *d_off = d_gt + b_k, *d_sl = d_off + b_off,
+            *d_v = d_sl + b_sl, *d_row = d_v + b_v;
+    if (add) HIP_TRY(hipMemcpyAsync(d_blob, blob + base0, add, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_mem, member, b_k, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_gt, gt, b_k, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_off, noff.data(), b_off, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_sl, sig_len, m * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(launch_dup_check(s->dup, s->dup_cap - 1, s->d_lines, s->d_rec, (const uint64_t*)d_mem,
+                             (const uint64_t*)d_gt, d_blob, (const uint64_t*)d_off, (const uint32_t*)d_sl, m, d_v,
+                             (uint64_t*)d_row, c->stream));
+    HIP_TRY(hipMemcpyAsync(out_verdict, d_v, m, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(out_row, d_row, m * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return DSY_OK;
+}
+
+int dsy_store_replace(dsy_ctx* c, dsy_store* s, const uint64_t* rows, const uint8_t* blob, uint64_t blob_len,
+                      const uint64_t* offsets, uint64_t k) {
+    if (!c || !s || !offsets || (k && (!rows || (blob_len && !blob)))) return fail(DSY_EINVAL, "NULL argument");
+    if (s->ctx != c) return fail(DSY_EINVAL, "store belongs to another context");
+    int rc = check_offsets(offsets, k, blob_len);
+    if (rc) return rc;
+    for (uint64_t i = 0; i < k; ++i)
+        if (rows[i] >= s->n) return fail(DSY_EINVAL, "row %llu out of range (%llu rows)", (unsigned long long)rows[i], (unsigned long long)s->n);
+    if (!k) return DSY_OK;
+    Guard g(c);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const uint64_t base0 = offsets[0], add = offsets[k] - base0;
+    std::vector<RowRec> nrec(k);
+    std::vector<uint64_t> noff(k + 1);
+    uint64_t at = s->lines_used, minlen = s->min_len;
+    for (uint64_t i = 0; i < k; ++i) {
+        const uint64_t len = offsets[i + 1] - offsets[i];
+        nrec[i] = RowRec{at, (uint32_t)len, 0u};
+        at += (len + 127) & ~127ull;
+        minlen = std::min(minlen, len);
+    }
+    for (uint64_t i = 0; i <= k; ++i) noff[i] = offsets[i] - base0;
+    if ((rc = lines_reserve(c, s, at))) return rc;
+    const size_t b_blob = (add + 15) / 16 * 16, b_off = (k + 1) * 8, b_rec = k * sizeof(RowRec), b_rows = k * 8;
+    void* d;
+    if ((rc = ws_get(c, "replace", b_blob + b_off + b_rec + b_rows, &d))) return rc;
+    uint8_t *d_blob = (uint8_t*)d, *d_off = d_blob + b_blob, *d_rec = d_off + b_off, *d_rows = d_rec + b_rec;
+    if (add) HIP_TRY(hipMemcpyAsync(d_blob, blob + base0, add, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_off, noff.data(), b_off, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_rec, nrec.data(), b_rec, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_rows, rows, b_rows, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(launch_store_lines(d_blob, (const uint64_t*)d_off, (const RowRec*)d_rec, k, const_cast<uint8_t*>(s->d_lines),
+                               c->stream));
+    HIP_TRY(launch_rec_scatter(const_cast<RowRec*>(s->d_rec), (const uint64_t*)d_rows, (const RowRec*)d_rec, k,
+                               c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    s->lines_used = at;
+    s->min_len = minlen;
     return DSY_OK;
 }
 

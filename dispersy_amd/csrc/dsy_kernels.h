@@ -183,6 +183,20 @@ hipError_t launch_pack(const RespondLaunch& L, uint64_t* packed, uint64_t* packe
 hipError_t launch_store_lines(const uint8_t* blob, const uint64_t* offsets, const RowRec* rec, uint64_t n,
                               uint8_t* lines, hipStream_t stream);
 
+// ------------------------------------------------------------------------ duplicate check (dsy_dup_check)
+// One slot of the store's (member, global_time) -> row table (open addressing, row == ~0: empty).
+struct DupSlot {
+    uint64_t member, gt, row, pad;
+};
+hipError_t launch_dup_insert(const uint64_t* member, const uint64_t* gt, uint64_t first_row, uint64_t n, DupSlot* tab,
+                             uint64_t mask, hipStream_t stream);
+hipError_t launch_dup_rehash(const DupSlot* old, uint64_t old_cap, DupSlot* tab, uint64_t mask, hipStream_t stream);
+hipError_t launch_dup_check(const DupSlot* tab, uint64_t mask, const uint8_t* lines, const RowRec* rec,
+                            const uint64_t* member, const uint64_t* gt, const uint8_t* blob, const uint64_t* offsets,
+                            const uint32_t* sig_len, uint64_t m, uint8_t* verdict, uint64_t* out_row,
+                            hipStream_t stream);
+hipError_t launch_rec_scatter(RowRec* rec, const uint64_t* rows, const RowRec* src, uint64_t k, hipStream_t stream);
+
 // ------------------------------------------------------------------------------- ingest (dsy_store_append)
 // One appended row, the rows in (meta, global_time, rowid) order: its meta's live segment [seg_a, seg_b) in the old
 // index ([x, x) at the meta's place when the meta is new) and its store row.

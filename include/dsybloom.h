@@ -171,7 +171,29 @@ uint64_t dsy_store_rows(const dsy_store* store);
  * The device buffers grow by >= 1.25x when full (copied once); an attached store's caller buffers are left as they
  * were and are no longer read.  The index merge is O(n + a) HBM traffic on the device. */
 int dsy_store_append(dsy_ctx* ctx, dsy_store* store, const uint8_t* blob, uint64_t blob_len, const uint64_t* offsets,
-                     uint64_t a, const uint64_t* global_time, const uint32_t* meta);
+                     uint64_t a, const uint64_t* global_time, const uint32_t* meta, const uint64_t* member);
+
+/* ------------------------------------------------------------------------------------ duplicate check */
+/* Received sync packets are checked against the store by (member, global_time) before they are stored
+ * (_is_duplicate_sync_message, dispersy.py:831-918; the sync table is UNIQUE(community, member, global_time)).
+ * dsy_store_index_members builds the store's (member, global_time) -> row table from the member and global time
+ * of every row (host arrays, n == dsy_store_rows); afterwards dsy_store_append must be given the appended rows'
+ * members (member may be NULL only while a store has no table). */
+#define DSY_DUP_NEW 0      /* no stored row with this (member, global_time): process the message */
+#define DSY_DUP_EXACT 1    /* binary identical packet stored (dispersy.py:872) */
+#define DSY_DUP_KEEP 2     /* same first signature_length bytes, stored packet >= received: keep ours (:893) */
+#define DSY_DUP_REPLACE 3  /* same first signature_length bytes, stored packet < received: UPDATE it (:901-905) */
+#define DSY_DUP_TRIPLET 4  /* same (member, global_time), different message (:910) */
+int dsy_store_index_members(dsy_ctx* ctx, dsy_store* store, const uint64_t* member, const uint64_t* global_time,
+                            uint64_t n);
+/* m received messages (host buffers): verdict[j] one of DSY_DUP_*, row[j] the stored row (~0 for DSY_DUP_NEW). */
+int dsy_dup_check(dsy_ctx* ctx, const dsy_store* store, const uint64_t* member, const uint64_t* global_time,
+                  const uint8_t* blob, uint64_t blob_len, const uint64_t* offsets, uint64_t m,
+                  const uint32_t* signature_length, uint8_t* out_verdict, uint64_t* out_row);
+/* UPDATE sync SET packet = ? for k rows (dispersy.py:903): the rows keep their place in the index; their new
+ * packets go to the end of the line copy. */
+int dsy_store_replace(dsy_ctx* ctx, dsy_store* store, const uint64_t* rows, const uint8_t* blob, uint64_t blob_len,
+                      const uint64_t* offsets, uint64_t k);
 
 /* Claim side (community.py:821, :924 and dispersy_store :698): OR the packets of the given store rows into a
  * filter.  rows are store row positions (0-based, export order). */

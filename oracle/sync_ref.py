@@ -12,6 +12,7 @@ Restated functions (reference file:line):
   claim_largest        community.py:763-837
   claim_modulo         community.py:908-933
   insert_packets       dispersy.py:1523-1533 (Dispersy._store's INSERT INTO sync, one execute per message)
+  check_full_sync_batch  dispersy.py:921-1065 (no sequence numbers) + is_duplicate_sync_message :831-918
   SYNC_SCHEMA          dispersydatabase.py:53-64 (the sync table and its (meta_message, undone, global_time) index)
 """
 import math
@@ -24,6 +25,55 @@ CREATE TABLE sync(id INTEGER PRIMARY KEY AUTOINCREMENT, community INTEGER, membe
                   UNIQUE(community, member, global_time));
 CREATE INDEX sync_mug ON sync(meta_message, undone, global_time);
 """
+
+
+def is_duplicate_sync_message(conn, community, message, sends):
+    """dispersy.py:831-918 (_is_duplicate_sync_message).  message: dict(member, gt, packet, signature_length, index).
+    Side effects as the reference: the undo proof is 'sent' (appended to sends as (index, packet)) and the stored
+    packet is replaced by UPDATE when only the signature differs and ours is smaller."""
+    row = conn.execute("SELECT packet, undone FROM sync WHERE community = ? AND member = ? AND global_time = ?",
+                       (community, message["member"], message["gt"])).fetchone()
+    if row is None:
+        return False
+    have, undone = bytes(row[0]), row[1]
+    packet = message["packet"]
+    if have == packet:
+        if undone:
+            proof = conn.execute("SELECT packet FROM sync WHERE id = ?", (undone,)).fetchone()
+            if proof is not None:
+                sends.append((message["index"], bytes(proof[0])))
+    else:
+        sl = message["signature_length"]
+        if have[:sl] == packet[:sl]:
+            if have < packet:
+                conn.execute("UPDATE sync SET packet = ? WHERE community = ? AND member = ? AND global_time = ?",
+                             (packet, community, message["member"], message["gt"]))
+    return True
+
+
+def check_full_sync_batch(conn, community, messages, acceptable_global_time, global_time):
+    """dispersy.py:921-1065 (_check_full_sync_distribution_batch), the branch without sequence numbers (:1043-1063).
+    messages: dicts (member, gt, packet, signature_length, inactive or None, index).  Returns ([(index, reason or
+    None)] in the order the reference yields them -- sorted by (global_time, packet) --, sends)."""
+    out, sends, unique = [], [], set()
+    for message in sorted(messages, key=lambda m: (m["gt"], m["packet"])):
+        if message["gt"] > acceptable_global_time:
+            out.append((message["index"], "global time is not within acceptable range"))
+            continue
+        inactive = message.get("inactive")
+        if inactive is not None and not (global_time - message["gt"] < inactive):  # distribution.py:80-81
+            out.append((message["index"], "message has been pruned"))
+            continue
+        key = (message["member"], message["gt"])
+        if key in unique:
+            out.append((message["index"], "duplicate message by member^global_time (2)"))
+            continue
+        unique.add(key)
+        if is_duplicate_sync_message(conn, community, message, sends):
+            out.append((message["index"], "duplicate message by global_time (2)"))
+            continue
+        out.append((message["index"], None))
+    return out, sends
 
 
 def insert_packets(conn, community, rows):

@@ -1,0 +1,138 @@
+"""Duplicate check of received sync packets: `_check_full_sync_distribution_batch` without sequence
+numbers (dispersy.py:1043-1063) and `_is_duplicate_sync_message` (:831-918), with the (member, global_time)
+lookups as one GPU hash join (dsy_dup_check) against the oracle's restatement over sqlite with the reference's SQL
+(oracle/sync_ref.check_full_sync_batch).  Every verdict kind is in the batch: new packets, exact duplicates (of
+live and of undone rows, whose undo proof is sent), same first signature_length bytes with a smaller or larger
+stored packet (the UPDATE), triplet collisions, duplicates inside the batch, global times above the acceptable
+range and pruned messages."""
+import sqlite3
+
+import numpy as np
+import pytest
+
+from dispersy_amd import BloomFilter
+from dispersy_amd.community import DropMessage, SyncCommunity
+from dispersy_amd.distribution import GlobalTimePruning, MetaMessage, SyncDistribution
+from dispersy_amd.store import SyncStore
+from oracle import sync_ref
+from oracle.bloom_ref import OracleBloom
+
+SIG = 60
+GT_NOW = 5_000
+META = MetaMessage("f", 1, SyncDistribution("ASC", 128, GlobalTimePruning(3_000, 4_000)))
+
+
+def make_store_rows(seed, n):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    rows, seen = [], set()
+    while len(rows) < n:
+        member, gt = int(rng.integers(1, 300)), int(rng.integers(1, GT_NOW))
+        if (member, gt) in seen:
+            continue
+        seen.add((member, gt))
+        i = len(rows)
+        packet = i.to_bytes(4, "big") + rng.bytes(int(rng.integers(SIG + 8, 400)) - 4)
+        rows.append([i + 1, gt, 1, 0, packet, member])
+    for i in rng.choice(n, size=n // 20, replace=False):  # undone rows: undone = the id of the proof row
+        rows[int(i)][3] = int(rng.integers(1, n + 1))
+    return [tuple(r) for r in rows]
+
+
+class Dist(object):
+    def __init__(self, gt):
+        self.global_time, self.priority = gt, 128
+
+
+class Msg(object):
+    def __init__(self, index, member, gt, packet):
+        self.index, self.member, self.packet, self.candidate = index, member, packet, "peer-%d" % index
+        self.distribution, self.meta = Dist(gt), META
+
+
+def make_batch(seed, rows, m):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    out = []
+    for j in range(m):
+        kind = int(rng.integers(0, 8))
+        r = rows[int(rng.integers(0, len(rows)))]
+        if kind == 0:  # new (member, global_time)
+            member, gt, packet = int(rng.integers(300, 400)), int(rng.integers(1, GT_NOW)), rng.bytes(int(rng.integers(80, 300)))
+        elif kind == 1:  # exact duplicate (some of them undone rows)
+            member, gt, packet = r[5], r[1], r[4]
+        elif kind in (2, 3):  # same first SIG bytes, different tail: smaller or larger than ours
+            tail = bytearray(r[4][SIG:])
+            if tail:
+                p = int(rng.integers(0, len(tail)))
+                tail[p] = (tail[p] + (1 if kind == 2 else 255)) % 256 or (1 if kind == 2 else 254)
+            if kind == 3 and rng.random() < 0.3:
+                tail = tail[:max(0, len(tail) - 3)]  # a proper prefix is smaller
+            member, gt, packet = r[5], r[1], r[4][:SIG] + bytes(tail)
+        elif kind == 4:  # same triplet, different message
+            member, gt, packet = r[5], r[1], rng.bytes(len(r[4]))
+        elif kind == 5:  # a duplicate inside the batch
+            if out:
+                prev = out[int(rng.integers(0, len(out)))]
+                member, gt, packet = prev.member, prev.distribution.global_time, prev.packet + b"x"
+            else:
+                member, gt, packet = r[5], r[1], r[4]
+        elif kind == 6:  # global time above acceptable (community gt + 10000)
+            member, gt, packet = r[5], GT_NOW + 10_001 + int(rng.integers(0, 5)), r[4]
+        else:  # pruned: community gt - gt >= inactive (3000)
+            member, gt, packet = int(rng.integers(1, 400)), int(rng.integers(1, GT_NOW - 3_000)), rng.bytes(120)
+        out.append(Msg(j, member, gt, packet))
+    return out
+
+
+def sqlite_of(rows):
+    conn = sqlite3.connect(":memory:")
+    conn.executescript(sync_ref.SYNC_SCHEMA)
+    conn.executemany("INSERT INTO sync(id, community, member, global_time, meta_message, undone, packet, sequence) "
+                     "VALUES (?, 1, ?, ?, ?, ?, ?, 0)", [(r[0], r[5], r[1], r[2], r[3], r[4]) for r in rows])
+    return conn
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 2])
+def test_duplicate_check_matches_the_reference(seed):
+    rows = make_store_rows(100 + seed, 20_000)
+    conn = sqlite_of(rows)
+    store = SyncStore.from_rows(rows)
+    com = SyncCommunity(store, [META], global_time=GT_NOW, signature_length=SIG)
+    batch = make_batch(200 + seed, rows, 3000)
+    got = com._check_full_sync_distribution_batch(batch)
+    want, sends = sync_ref.check_full_sync_batch(
+        conn, 1, [dict(member=m.member, gt=m.distribution.global_time, packet=m.packet, signature_length=SIG,
+                       inactive=3_000, index=m.index) for m in batch], com.acceptable_global_time, com.global_time)
+    mine = [(g.dropped.index, g.reason) if isinstance(g, DropMessage) else (g.index, None) for g in got]
+    assert mine == want
+    assert len({r for _, r in want}) == 5  # every outcome occurred (accept + four drop reasons)
+    assert [(int(c.split("-")[1]), p) for c, p, _ in com.sent_packets] == sends and sends
+    # the UPDATEs: every stored packet equals sqlite's, on the host and in HBM (claim filter over all rows)
+    final = dict(conn.execute("SELECT id, packet FROM sync"))
+    assert all(store.packet(i) == bytes(final[int(store.rowid[i])]) for i in range(store.n))
+    assert len(store._replaced) > 0
+    bf, ob = BloomFilter(1 << 20, 0.01, b"\x05"), OracleBloom.from_m_f(1 << 20, 0.01, b"\x05")
+    replaced = sorted(store._replaced)
+    bf.add_store_rows(store, replaced)
+    ob.add_keys([bytes(final[int(store.rowid[i])]) for i in replaced])
+    assert bf.bytes == ob.to_bytes()
+
+
+@pytest.mark.gpu
+def test_duplicate_table_follows_appends():
+    """Rows stored after the table exists (store_messages -> dsy_store_append with members) are found as
+    duplicates; the table grows past its first capacity (rehash)."""
+    rows = make_store_rows(7, 600)
+    store = SyncStore.from_rows(rows)
+    com = SyncCommunity(store, [META], global_time=GT_NOW, signature_length=SIG)
+    assert com._check_full_sync_distribution_batch([Msg(0, rows[0][5], rows[0][1], rows[0][4])])[0].reason
+    rng = np.random.Generator(np.random.PCG64(8))
+    fresh = [Msg(i, 1000 + i, int(rng.integers(2_000, GT_NOW)), rng.bytes(100)) for i in range(3000)]
+    for m in fresh:
+        m.database_id = 1
+    com.store_messages(fresh)
+    again = com._check_full_sync_distribution_batch([Msg(i, m.member, m.distribution.global_time, m.packet)
+                                                     for i, m in enumerate(fresh[::7])])
+    assert all(isinstance(g, DropMessage) and g.reason == "duplicate message by global_time (2)" for g in again)
+    new = com._check_full_sync_distribution_batch([Msg(0, 5000, 4_500, b"n" * 90)])
+    assert not isinstance(new[0], DropMessage)
