@@ -51,10 +51,10 @@ def parse():
     ap.add_argument("--sim-initial", type=int, default=100)
     ap.add_argument("--sim-rounds", type=int, default=10)
     ap.add_argument("--sim-warmup", type=int, default=2)
-    ap.add_argument("--extra", default="ingest,1,3,4,5",
+    ap.add_argument("--extra", default="dedup,ingest,1,3,4,5",
                     help="BASELINE configs measured beside the headline (config 2): 1 single filter, 3 gossip "
                          "simulator, 4 large filters, 5 heavy-tailed packets, ingest: received packets appended to "
-                         "the headline store; '' for none")
+                         "the headline store, dedup: duplicate check of received packets against it; '' for none")
     ap.add_argument("--large-keys", type=int, default=100_000_000, help="config 4: keys added per filter")
     ap.add_argument("--large-tests", type=int, default=10_000_000, help="config 4: keys tested per filter")
     return ap.parse_args()
@@ -231,6 +231,9 @@ def main():
     extra = set(x for x in args.extra.split(",") if x and x != "none")
 
     ingest = None
+    dedup = None
+    if "dedup" in extra:
+        dedup = dedup_bench(args, ctx, lib, store, blob, offsets, N)
     if "ingest" in extra:
         ingest = ingest_bench(args, ctx, lib, store, step, pairs, N)
 
@@ -281,12 +284,91 @@ def main():
             "large_filter": large,
             "heavy_tail": heavy,
             "ingest": ingest,
+            "dedup": dedup,
         }
         print(json.dumps(line))
     if store is not None:
         lib.dsy_store_free(store)
     if dist:
         dist.destroy_process_group()
+
+
+def dedup_bench(args, ctx, lib, store, blob, offsets, N, batch=10_000, reps=10):
+    """SURVEY §8f row 3, the duplicate check of received sync packets (_is_duplicate_sync_message,
+    dispersy.py:831-918) against the headline's 10 M-packet store: the (member, global_time) table is built once
+    (dsy_store_index_members, every row), then batches of `batch` received messages -- half exact copies of stored
+    packets, half new (member, global_time) keys -- go through dsy_dup_check (one wave per message: 64-slot probes,
+    64-byte packet compares).  Wall time per call, PCIe upload of the messages included."""
+    import torch
+    rng = np.random.Generator(np.random.PCG64(123))
+    member = (np.arange(N, dtype=np.uint64) % np.uint64(65536))  # with global_time = row + 1: unique keys
+    gt = np.arange(1, N + 1, dtype=np.uint64)
+    t0 = time.perf_counter()
+    _native.check(lib.dsy_store_index_members(ctx.handle, store, member.ctypes.data, gt.ctypes.data, N))
+    build_ms = (time.perf_counter() - t0) * 1e3
+
+    def make():
+        dup_rows = rng.integers(0, N, size=batch // 2)
+        off_d = offsets[torch.from_numpy(dup_rows).to(offsets.device)].cpu().numpy()
+        end_d = offsets[torch.from_numpy(dup_rows + 1).to(offsets.device)].cpu().numpy()
+        pk = [bytes(blob[int(a):int(e)].cpu().numpy().tobytes()) for a, e in zip(off_d, end_d)]
+        mem = list(member[dup_rows]) + list(rng.integers(70_000, 1 << 30, size=batch - batch // 2))
+        gts = list(gt[dup_rows]) + list(rng.integers(1, N + 1, size=batch - batch // 2))
+        pk += [rng.bytes(int(x)) for x in rng.integers(100, 1501, size=batch - batch // 2)]
+        off = np.zeros(batch + 1, dtype=np.uint64)
+        np.cumsum([len(p) for p in pk], out=off[1:])
+        return (b"".join(pk), off, np.asarray(mem, dtype=np.uint64), np.asarray(gts, dtype=np.uint64))
+
+    data, off, mem, gts = make()
+    sl = np.full(batch, 60, dtype=np.uint32)
+    verdict = np.zeros(batch, dtype=np.uint8)
+    row = np.zeros(batch, dtype=np.uint64)
+
+    def check():
+        _native.check(lib.dsy_dup_check(ctx.handle, store, mem.ctypes.data, gts.ctypes.data, data, len(data),
+                                        off.ctypes.data, batch, sl.ctypes.data, verdict.ctypes.data, row.ctypes.data))
+
+    check()
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        check()
+        times.append(time.perf_counter() - t0)
+    ms = sorted(times)[len(times) // 2] * 1e3
+    exact = int((verdict == _native.DSY_DUP_EXACT).sum())
+    new = int((verdict == _native.DSY_DUP_NEW).sum())
+    cpu = None
+    if args.cpu_claims > 0:  # the reference's SELECT + compare per message over sqlite3 (oracle/sync_ref.py)
+        import sqlite3
+        from oracle.sync_ref import SYNC_SCHEMA, is_duplicate_sync_message
+        conn = sqlite3.connect(":memory:")
+        conn.executescript(SYNC_SCHEMA)
+        pre = 200_000
+        crng = np.random.Generator(np.random.PCG64(6))
+        conn.executemany("INSERT INTO sync (community, member, global_time, meta_message, packet) VALUES (1, ?, ?, 1, ?)",
+                         ((int(member[i]), int(gt[i]), crng.bytes(int(l)))
+                          for i, l in zip(range(pre), crng.integers(100, 1501, size=pre))))
+        conn.commit()
+        # the first half hits a stored (member, global_time) of the smaller table, the second half misses
+        hit_gt = [int(gts[i]) % pre + 1 for i in range(batch // 2)]
+        sample = [dict(member=(g - 1) % 65536, gt=g, packet=data[int(off[i]):int(off[i + 1])], signature_length=60,
+                       index=i) for i, g in enumerate(hit_gt)]
+        sample += [dict(member=int(mem[i]), gt=int(gts[i]), packet=data[int(off[i]):int(off[i + 1])],
+                        signature_length=60, index=i) for i in range(batch // 2, batch)]
+        sends = []
+        t0 = time.perf_counter()
+        for m_ in sample:
+            is_duplicate_sync_message(conn, 1, m_, sends)
+        dt = time.perf_counter() - t0
+        conn.close()
+        cpu = {"value": round(batch / dt, 1), "unit": "messages/s", "cores": 1, "kind": "port",
+               "sample": "%d messages through the reference's SELECT packet, undone ... WHERE community, member, "
+                         "global_time + packet compare (dispersy.py:868-910) on an in-memory sqlite3 sync table of "
+                         "%d rows" % (batch, pre)}
+    return {"metric": "received messages duplicate-checked/sec", "batch": batch, "store_rows": N,
+            "index_build_ms": round(build_ms, 2), "median_ms_per_batch": round(ms, 3),
+            "messages_per_s": round(batch / (ms / 1e3), 1), "found_exact": exact, "found_new": new,
+            "cpu_baseline": cpu}
 
 
 def ingest_bench(args, ctx, lib, store, step, pairs, N, batch=10_000, batches=10):
@@ -309,10 +391,14 @@ def ingest_bench(args, ctx, lib, store, step, pairs, N, batch=10_000, batches=10
         metas = np.ones(batch, dtype=np.uint32)
         return data, off, gts, metas
 
+    member_next = [1 << 40]  # members of the appended rows (the store may hold a duplicate table by now)
+
     def append(b):
         data, off, gts, metas = b
+        mem = np.arange(member_next[0], member_next[0] + batch, dtype=np.uint64)
+        member_next[0] += batch
         _native.check(lib.dsy_store_append(ctx.handle, store, data, len(data), off.ctypes.data, batch,
-                                           gts.ctypes.data, metas.ctypes.data, None))
+                                           gts.ctypes.data, metas.ctypes.data, mem.ctypes.data))
 
     work = [make() for _ in range(batches + 1)]
     t0 = time.perf_counter()
