@@ -233,9 +233,9 @@ def main():
     ingest = None
     dedup = None
     if "dedup" in extra:
-        dedup = dedup_bench(args, ctx, lib, store, blob, offsets, N)
+        dedup = dedup_bench(args, ctx, lib, store, blob, offsets, N, cpu_leg=rank == 0 and world == 1)
     if "ingest" in extra:
-        ingest = ingest_bench(args, ctx, lib, store, step, pairs, N)
+        ingest = ingest_bench(args, ctx, lib, store, step, pairs, N, cpu_leg=rank == 0 and world == 1)
 
     gossip = None
     if "3" in extra and args.sim_peers > 0:
@@ -293,7 +293,7 @@ def main():
         dist.destroy_process_group()
 
 
-def dedup_bench(args, ctx, lib, store, blob, offsets, N, batch=10_000, reps=10):
+def dedup_bench(args, ctx, lib, store, blob, offsets, N, batch=10_000, reps=10, cpu_leg=True):
     """SURVEY §8f row 3, the duplicate check of received sync packets (_is_duplicate_sync_message,
     dispersy.py:831-918) against the headline's 10 M-packet store: the (member, global_time) table is built once
     (dsy_store_index_members, every row), then batches of `batch` received messages -- half exact copies of stored
@@ -338,7 +338,7 @@ def dedup_bench(args, ctx, lib, store, blob, offsets, N, batch=10_000, reps=10):
     exact = int((verdict == _native.DSY_DUP_EXACT).sum())
     new = int((verdict == _native.DSY_DUP_NEW).sum())
     cpu = None
-    if args.cpu_claims > 0:  # the reference's SELECT + compare per message over sqlite3 (oracle/sync_ref.py)
+    if cpu_leg and args.cpu_claims > 0:  # the reference's SELECT + compare per message over sqlite3 (oracle/sync_ref.py)
         import sqlite3
         from oracle.sync_ref import SYNC_SCHEMA, is_duplicate_sync_message
         conn = sqlite3.connect(":memory:")
@@ -371,7 +371,7 @@ def dedup_bench(args, ctx, lib, store, blob, offsets, N, batch=10_000, reps=10):
             "cpu_baseline": cpu}
 
 
-def ingest_bench(args, ctx, lib, store, step, pairs, N, batch=10_000, batches=10):
+def ingest_bench(args, ctx, lib, store, step, pairs, N, batch=10_000, batches=10, cpu_leg=True):
     """SURVEY §8f row 1, requester-side ingest: `Dispersy._store` INSERTs each batch of received sync packets
     (dispersy.py:1475-1612).  Here batches of `batch` packets (100-1500 B, global times spread over the store's
     range, so they land everywhere in the index and tie with stored rows) go into the headline's 10 M-packet store
@@ -416,7 +416,7 @@ def ingest_bench(args, ctx, lib, store, step, pairs, N, batch=10_000, batches=10
     ctx.synchronize()
     torch.cuda.synchronize()
     cpu = None
-    if args.cpu_claims > 0:  # the CPU baseline leg: the reference's INSERT through sqlite3 (oracle/sync_ref.py)
+    if cpu_leg and args.cpu_claims > 0:  # the CPU baseline leg: the reference's INSERT through sqlite3 (oracle/sync_ref.py)
         import sqlite3
         from oracle.sync_ref import SYNC_SCHEMA, insert_packets
         conn = sqlite3.connect(":memory:")

@@ -228,6 +228,8 @@ class SyncCommunity(object):
                         if proof is not None:
                             self.sent_packets.append((message.candidate, proof, "-caused by duplicate-undo-"))
                 elif v == _native.DSY_DUP_REPLACE:
+                    # the host copy changes now (a later proof send in this batch reads it), HBM once below
+                    self._store.replace_packet([row], [message.packet], device=False)
                     replace_rows.append(row)
                     replace_packets.append(message.packet)
                 out[i] = DropMessage(message, "duplicate message by global_time (2)")

@@ -196,11 +196,12 @@ class SyncStore(object):
                                             off.ctypes.data, m, sl.ctypes.data, verdict.ctypes.data, row.ctypes.data))
         return verdict, row.astype(np.int64)
 
-    def replace_packet(self, rows, packets):
-        """UPDATE sync SET packet = ? (dispersy.py:903) for the given rows: same row, index place and rowid."""
+    def replace_packet(self, rows, packets, device=True):
+        """UPDATE sync SET packet = ? (dispersy.py:903) for the given rows: same row, index place and rowid.
+        device=False changes only the host copy (the caller updates HBM with a later call)."""
         for r, p in zip(rows, packets):
             self._replaced[int(r)] = bytes(p)
-        if self._handle is not None and len(rows):
+        if device and self._handle is not None and len(rows):
             self._replace_device(rows, packets)
 
     def _replace_device(self, rows, packets):

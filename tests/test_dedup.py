@@ -136,3 +136,54 @@ def test_duplicate_table_follows_appends():
     assert all(isinstance(g, DropMessage) and g.reason == "duplicate message by global_time (2)" for g in again)
     new = com._check_full_sync_distribution_batch([Msg(0, 5000, 4_500, b"n" * 90)])
     assert not isinstance(new[0], DropMessage)
+
+
+# ---------------------------------------------------------------- golden vectors made by the reference's own methods
+def _golden():
+    from golden_util import load
+    return load("dedup_vectors.json")
+
+
+def _golden_setup(g):
+    rows = [(r["id"], r["gt"], 1, r["undone"], bytes.fromhex(r["packet"]), r["member"]) for r in g["rows"]]
+    batch = [Msg(b["index"], b["member"], b["gt"], bytes.fromhex(b["packet"])) for b in g["batch"]]
+    return rows, batch
+
+
+def test_oracle_matches_reference_vectors():
+    """oracle/sync_ref.check_full_sync_batch == the reference's lifted _check_full_sync_distribution_batch +
+    _is_duplicate_sync_message (tests/golden/gen_dedup_golden.py): verdicts, order, sends and UPDATEs."""
+    g = _golden()
+    rows, batch = _golden_setup(g)
+    conn = sqlite_of(rows)
+    got, sends = sync_ref.check_full_sync_batch(
+        conn, 1, [dict(member=m.member, gt=m.distribution.global_time, packet=m.packet,
+                       signature_length=g["signature_length"], inactive=g["inactive"], index=m.index) for m in batch],
+        g["acceptable_global_time"], g["global_time"])
+    assert [list(x) for x in got] == g["results"]
+    assert [["c%d" % i, p.hex()] for i, p in sends] == [s[:2] for s in g["sent"]]
+    final = {str(i): bytes(p).hex() for i, p in conn.execute("SELECT id, packet FROM sync")}
+    assert {k: v for k, v in final.items() if v != dict((str(r[0]), r[4].hex()) for r in rows)[k]} == g["updated"]
+
+
+@pytest.mark.gpu
+def test_gpu_check_matches_reference_vectors():
+    g = _golden()
+    rows, batch = _golden_setup(g)
+    store = SyncStore.from_rows(rows)
+    meta = MetaMessage("f", 1, SyncDistribution("ASC", 128, GlobalTimePruning(g["inactive"], g["inactive"] + 1000)))
+    for m in batch:
+        m.meta = meta
+    com = SyncCommunity(store, [meta], global_time=g["global_time"], signature_length=g["signature_length"])
+    assert com.acceptable_global_time == g["acceptable_global_time"]
+    got = com._check_full_sync_distribution_batch(batch)
+    assert [[x.dropped.index, x.reason] if isinstance(x, DropMessage) else [x.index, None] for x in got] == g["results"]
+    assert [["c%d" % int(c.split("-")[1]), p.hex(), r] for c, p, r in com.sent_packets] == g["sent"]
+    updated = {str(int(store.rowid[r])): p.hex() for r, p in store._replaced.items()}
+    assert updated == g["updated"]
+    # the device copy was updated too: a filter over the updated rows equals one over the reference's packets
+    rows_u = sorted(store._replaced)
+    bf, ob = BloomFilter(10160, 0.01, b"\x09"), OracleBloom.from_m_f(10160, 0.01, b"\x09")
+    bf.add_store_rows(store, rows_u)
+    ob.add_keys([bytes.fromhex(g["updated"][str(int(store.rowid[r]))]) for r in rows_u])
+    assert bf.bytes == ob.to_bytes()
