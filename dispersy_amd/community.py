@@ -97,6 +97,9 @@ class SyncCommunity(object):
         self._nrsyncpackets = 0
         self.dispersy_acceptable_global_time_range = 10000  # community.py:952-953
         self.sent_packets = []  # (candidate, packet, reason) the checks answer with (Dispersy._send_packets)
+        # community.py:430-431
+        self._do_pruning = any(isinstance(m.distribution, SyncDistribution) and
+                               isinstance(m.distribution.pruning, GlobalTimePruning) for m in meta_messages)
 
     # ------------------------------------------------------------------------ plugin hooks (properties)
     @property
@@ -145,8 +148,16 @@ class SyncCommunity(object):
         return min(self._global_time + self.dispersy_acceptable_global_time_range, MAX_GT)
 
     def update_global_time(self, global_time):
+        """community.py:1082-1096: raise the global time; with GlobalTimePruning metas, DELETE their packets that
+        reached the prune threshold (SyncStore.prune -> dsy_store_prune)."""
         if global_time > self._global_time:
             self._global_time = global_time
+            if self._do_pruning:
+                for meta in self._meta_messages.values():
+                    if (isinstance(meta.distribution, SyncDistribution) and
+                            isinstance(meta.distribution.pruning, GlobalTimePruning)):
+                        self._store.prune(meta.database_id,
+                                          self._global_time - meta.distribution.pruning.prune_threshold)
 
     def get_meta_messages(self):
         return list(self._meta_messages.values())

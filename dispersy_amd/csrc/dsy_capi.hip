@@ -917,6 +917,65 @@ int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blo
     return DSY_OK;
 }
 
+int dsy_store_prune(dsy_ctx* c, dsy_store* s, uint32_t meta, uint64_t max_gt, uint64_t* out_deleted) {
+    if (!c || !s || !out_deleted) return fail(DSY_EINVAL, "NULL argument");
+    if (s->ctx != c) return fail(DSY_EINVAL, "store belongs to another context");
+    *out_deleted = 0;
+    auto it = s->segs.find(meta);
+    if (it == s->segs.end() || it->second.first == it->second.second) return DSY_OK;
+    Guard g(c);
+    const uint64_t a = it->second.first, b = it->second.second;
+    void* d_k;
+    int rc;
+    if ((rc = ws_get(c, "prune_k", 64, &d_k))) return rc;
+    HIP_TRY(launch_prune_count(s->d_live_gt, a, b, max_gt, (uint64_t*)d_k, c->stream));
+    uint64_t k = 0;
+    HIP_TRY(hipMemcpyAsync(&k, d_k, 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (!k) return DSY_OK;
+    const uint64_t live = s->n_live - k;
+    if (s->spare_cap < live) {  // the ingest's second buffer pair is the target, as for a merge
+        store_release(s, s->spare_gt);
+        store_release(s, s->spare_row);
+        s->spare_gt = s->spare_row = nullptr;
+        s->spare_cap = 0;
+        const uint64_t cap = grown(s->n_live, s->n_live);
+        void *pg, *pr;
+        if (hipMalloc(&pg, cap * 8) != hipSuccess) return fail(DSY_ENOMEM, "store live index");
+        s->owned.push_back(pg);
+        if (hipMalloc(&pr, cap * 8) != hipSuccess) { store_release(s, pg); return fail(DSY_ENOMEM, "store live index"); }
+        s->owned.push_back(pr);
+        s->spare_gt = (uint64_t*)pg;
+        s->spare_row = (uint64_t*)pr;
+        s->spare_cap = cap;
+    }
+    HIP_TRY(launch_live_cut(s->d_live_gt, s->d_live_row, live, a, k, s->spare_gt, s->spare_row, c->max_grid, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    uint64_t* prev_gt = const_cast<uint64_t*>(s->d_live_gt);
+    uint64_t* prev_row = const_cast<uint64_t*>(s->d_live_row);
+    const uint64_t prev_cap = s->live_cap;
+    s->d_live_gt = s->spare_gt;
+    s->d_live_row = s->spare_row;
+    s->live_cap = s->spare_cap;
+    if (prev_cap) {
+        s->spare_gt = prev_gt;
+        s->spare_row = prev_row;
+        s->spare_cap = prev_cap;
+    } else {
+        store_release(s, prev_gt);
+        store_release(s, prev_row);
+        s->spare_gt = s->spare_row = nullptr;
+        s->spare_cap = 0;
+    }
+    for (auto& e : s->segs) {  // this meta's segment loses its first k rows; later segments move down by k
+        if (e.first == meta) e.second.second -= k;
+        else if (e.second.first >= b) { e.second.first -= k; e.second.second -= k; }
+    }
+    s->n_live = live;
+    *out_deleted = k;
+    return DSY_OK;
+}
+
 int dsy_store_index_members(dsy_ctx* c, dsy_store* s, const uint64_t* member, const uint64_t* gt, uint64_t n) {
     if (!c || !s || (n && (!member || !gt))) return fail(DSY_EINVAL, "NULL argument");
     if (s->ctx != c) return fail(DSY_EINVAL, "store belongs to another context");

@@ -205,6 +205,12 @@ struct IngestRow {
 };
 // merge the appended rows into the live index: (live_gt, live_row | identity)[n_live] + rows[a] ->
 // (out_gt, out_row)[n_live + a]; rank[a] is scratch
+// GlobalTimePruning DELETE: k = rows of live_gt[a, b) with global_time <= max_gt (device u64), then the index
+// without live rows [a, a + k) -> (out_gt, out_row)[n_out]
+hipError_t launch_prune_count(const uint64_t* live_gt, uint64_t a, uint64_t b, uint64_t max_gt, uint64_t* out_k,
+                              hipStream_t stream);
+hipError_t launch_live_cut(const uint64_t* live_gt, const uint64_t* live_row, uint64_t n_out, uint64_t a, uint64_t k,
+                           uint64_t* out_gt, uint64_t* out_row, uint32_t max_grid, hipStream_t stream);
 hipError_t launch_ingest_merge(const uint64_t* live_gt, const uint64_t* live_row, uint64_t n_live,
                                const IngestRow* rows, uint64_t a, uint64_t* rank, uint64_t* out_gt, uint64_t* out_row,
                                uint32_t max_grid, hipStream_t stream);

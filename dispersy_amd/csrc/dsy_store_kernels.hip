@@ -77,6 +77,48 @@ __global__ void __launch_bounds__(kIngestThreads) k_ingest_merge_new(const Inges
     out_row[rank[j] + j] = r.row;
 }
 
+// DELETE FROM sync WHERE meta_message = ? AND global_time <= ? (community.py:1092-1096, GlobalTimePruning): the rows
+// form a prefix [a, a + k) of the meta's live segment.  k_prune_count finds k (one upper bound by one lane);
+// k_live_cut copies the index without that range (16 B in, 16 B out per indexed row).
+__global__ void k_prune_count(const uint64_t* __restrict__ live_gt, uint64_t a, uint64_t b, uint64_t max_gt,
+                              uint64_t* __restrict__ out_k) {
+    if (threadIdx.x) return;
+    uint64_t lo = a, hi = b;
+    while (lo < hi) {
+        const uint64_t mid = lo + ((hi - lo) >> 1);
+        if (live_gt[mid] <= max_gt) lo = mid + 1; else hi = mid;
+    }
+    *out_k = lo - a;
+}
+
+__global__ void __launch_bounds__(kIngestThreads) k_live_cut(const uint64_t* __restrict__ live_gt,
+                                                              const uint64_t* __restrict__ live_row, uint64_t n_out,
+                                                              uint64_t a, uint64_t k, uint64_t* __restrict__ out_gt,
+                                                              uint64_t* __restrict__ out_row) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kIngestThreads + threadIdx.x; i < n_out;
+         i += (uint64_t)gridDim.x * kIngestThreads) {
+        const uint64_t src = i < a ? i : i + k;
+        out_gt[i] = live_gt[src];
+        out_row[i] = live_row ? live_row[src] : src;
+    }
+}
+
+hipError_t launch_prune_count(const uint64_t* live_gt, uint64_t a, uint64_t b, uint64_t max_gt, uint64_t* out_k,
+                              hipStream_t stream) {
+    hipLaunchKernelGGL(k_prune_count, dim3(1), dim3(64), 0, stream, live_gt, a, b, max_gt, out_k);
+    return hipGetLastError();
+}
+
+hipError_t launch_live_cut(const uint64_t* live_gt, const uint64_t* live_row, uint64_t n_out, uint64_t a, uint64_t k,
+                           uint64_t* out_gt, uint64_t* out_row, uint32_t max_grid, hipStream_t stream) {
+    if (!n_out) return hipSuccess;
+    uint64_t g = (n_out + kIngestThreads - 1) / kIngestThreads;
+    if (g > (uint64_t)max_grid * 4) g = (uint64_t)max_grid * 4;
+    hipLaunchKernelGGL(k_live_cut, dim3((uint32_t)g), dim3(kIngestThreads), 0, stream, live_gt, live_row, n_out, a, k,
+                       out_gt, out_row);
+    return hipGetLastError();
+}
+
 hipError_t launch_ingest_merge(const uint64_t* live_gt, const uint64_t* live_row, uint64_t n_live,
                                const IngestRow* rows, uint64_t a, uint64_t* rank, uint64_t* out_gt, uint64_t* out_row,
                                uint32_t max_grid, hipStream_t stream) {

@@ -51,6 +51,7 @@ class SyncStore(object):
         self._row_of_id = None
         self._replaced = {}  # row -> packet after an UPDATE (dsy_store_replace); the packed blob keeps the original
         self._dup_indexed = False
+        self._prunes = []  # (meta, max_global_time) DELETEs, replayed on the device after a lazy upload
         # live (undone == 0) rows per meta, in global_time order: the claim side's index range scans
         live = np.flatnonzero(self.undone == 0)
         self._live = {}
@@ -169,6 +170,24 @@ class SyncStore(object):
             self._live[int(m)] = seg[np.argsort(self.global_time[seg], kind="stable")]
         return rows
 
+    def prune(self, meta_id, max_global_time):
+        """DELETE FROM sync WHERE meta_message = ? AND global_time <= ? (community.py:1092-1096, GlobalTimePruning):
+        the rows leave the live index (host and device).  Returns the number of rows deleted."""
+        seg = self._live.get(int(meta_id))
+        if seg is None or not len(seg) or max_global_time < 0:
+            return 0
+        k = int(np.searchsorted(self.global_time[seg], np.uint64(max_global_time), side="right"))
+        if not k:
+            return 0
+        self._live[int(meta_id)] = seg[k:]
+        self._prunes.append((int(meta_id), int(max_global_time), self.n))
+        if self._handle is not None:
+            out = ctypes.c_uint64()
+            _native.check(self.ctx.lib.dsy_store_prune(self.ctx.handle, self._handle, int(meta_id),
+                                                       int(max_global_time), ctypes.byref(out)))
+            assert out.value == k, (out.value, k)
+        return k
+
     # ------------------------------------------------------------------------------- duplicate check
     def dup_check(self, members, global_times, packets, signature_lengths):
         """(verdict, row) per received message against the stored (member, global_time) rows (dsy_dup_check,
@@ -233,12 +252,20 @@ class SyncStore(object):
                                                    self.global_time.ctypes.data, self.meta.ctypes.data,
                                                    undone.ctypes.data, ctypes.byref(h)))
             self._handle = h
-            if n0 < self.n:  # rows appended before the first upload: the same merge as a live append
-                off = np.ascontiguousarray(self.offsets[n0:] - self.offsets[n0])
-                tail = blob[int(self.offsets[n0]):]
-                _native.check(ctx.lib.dsy_store_append(ctx.handle, h, tail, len(tail), off.ctypes.data, self.n - n0,
-                                                       self.global_time[n0:].ctypes.data, self.meta[n0:].ctypes.data,
-                                                       None))
+            # rows appended and DELETEs made before the first upload, replayed in their order (a DELETE never
+            # reaches rows appended after it)
+            done = n0
+            for meta_id, max_gt, n_at in self._prunes + [(None, None, self.n)]:
+                if n_at > done:
+                    off = np.ascontiguousarray(self.offsets[done:n_at + 1] - self.offsets[done])
+                    tail = blob[int(self.offsets[done]):int(self.offsets[n_at])]
+                    _native.check(ctx.lib.dsy_store_append(ctx.handle, h, tail, len(tail), off.ctypes.data,
+                                                           n_at - done, self.global_time[done:n_at].ctypes.data,
+                                                           self.meta[done:n_at].ctypes.data, None))
+                    done = n_at
+                if meta_id is not None:
+                    out = ctypes.c_uint64()
+                    _native.check(ctx.lib.dsy_store_prune(ctx.handle, h, meta_id, max_gt, ctypes.byref(out)))
             if self._replaced:  # UPDATEs made before the first upload
                 rows = sorted(self._replaced)
                 self._replace_device(rows, [self._replaced[r] for r in rows])

@@ -173,6 +173,12 @@ uint64_t dsy_store_rows(const dsy_store* store);
 int dsy_store_append(dsy_ctx* ctx, dsy_store* store, const uint8_t* blob, uint64_t blob_len, const uint64_t* offsets,
                      uint64_t a, const uint64_t* global_time, const uint32_t* meta, const uint64_t* member);
 
+/* GlobalTimePruning's DELETE FROM sync WHERE meta_message = ? AND global_time <= ? (community.py:1092-1096, run by
+ * update_global_time): the meta's rows up to max_global_time leave the responder's index.  *out_deleted = their
+ * number.  (Their (member, global_time) keys stay in the duplicate table: any later message with such a global time
+ * is inactive, and _check_full_sync_distribution_batch drops it as pruned before the lookup.) */
+int dsy_store_prune(dsy_ctx* ctx, dsy_store* store, uint32_t meta, uint64_t max_global_time, uint64_t* out_deleted);
+
 /* ------------------------------------------------------------------------------------ duplicate check */
 /* Received sync packets are checked against the store by (member, global_time) before they are stored
  * (_is_duplicate_sync_message, dispersy.py:831-918; the sync table is UNIQUE(community, member, global_time)).

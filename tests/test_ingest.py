@@ -197,3 +197,44 @@ def test_sync_round_trip_through_store_messages():
                                    (lo, hi, offset, modulo), ob, GT_NOW, 5120, False)
     assert store_a.rowid[got2].tolist() == want2
     assert not set(want2) & set(want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lazy", [False, True])
+def test_global_time_pruning_deletes_from_the_responder(lazy):
+    """update_global_time with GlobalTimePruning metas DELETEs their rows up to global_time - prune_threshold
+    (community.py:1082-1096, run on sqlite verbatim as the oracle); the responder no longer serves them even with
+    include_inactive=True, and appends after the DELETE still merge (dsy_store_prune + dsy_store_append)."""
+    rows = make_rows(41, 12_000, 8_000)
+    store = SyncStore.from_rows(rows[:8_000])
+    if not lazy:
+        store.handle  # noqa: B018
+    com = SyncCommunity(store, metas(), global_time=GT_NOW)
+    conn = sqlite_of(rows[:8_000])
+    com.update_global_time(GT_NOW + 1_500)  # meta 3 (prune at 800): rows up to 3800 go
+    for m in METAS:
+        if m[4]:
+            conn.execute("DELETE FROM sync WHERE meta_message = ? AND global_time <= ?", (m[1], GT_NOW + 1_500 - m[4][1]))
+    grow(store, rows[8_000:], 2)
+    conn.executemany("INSERT INTO sync(id, community, member, global_time, meta_message, undone, packet, sequence) "
+                     "VALUES (?, 1, ?, ?, ?, ?, ?, 0)", [(r[0], r[0], r[1], r[2], r[3], r[4]) for r in rows[8_000:]])
+    gt_now = GT_NOW + 1_500
+    for m in (0, 1, 2, 3, 5, 7):
+        want = [i for (i,) in conn.execute("SELECT id FROM sync WHERE meta_message = ? AND undone = 0 "
+                                           "ORDER BY global_time, id", (m,))]
+        assert store.rowid[store.live_rows(m)].tolist() == want, m
+    rng = np.random.Generator(np.random.PCG64(43))
+    reqs, blooms = [], []
+    for q in range(24):
+        lo, prefix = int(rng.integers(1, 3_000)), bytes([q])
+        bf, ob = BloomFilter(10160, 0.01, prefix), OracleBloom.from_m_f(10160, 0.01, prefix)
+        known = [r[4] for r in rows if rng.random() < 0.95]
+        bf.add_keys(known)
+        ob.add_keys(known)
+        reqs.append(ClaimRequest(lo, gt_now, 1, 0, bf))
+        blooms.append(ob)
+    got = com.respond(reqs, include_inactive=True, byte_limit=1 << 40)
+    for q, ob, g in zip(reqs, blooms, got):
+        want = sync_ref.respond_lists(conn, oracle_metas(), (q.time_low, q.time_high, q.offset, q.modulo), ob,
+                                      gt_now, 1 << 40, True)
+        assert store.rowid[g].tolist() == want
