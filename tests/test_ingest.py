@@ -238,3 +238,17 @@ def test_global_time_pruning_deletes_from_the_responder(lazy):
         want = sync_ref.respond_lists(conn, oracle_metas(), (q.time_low, q.time_high, q.offset, q.modulo), ob,
                                       gt_now, 1 << 40, True)
         assert store.rowid[g].tolist() == want
+
+
+def test_prune_host_index():
+    """SyncStore.prune on the host columns: the meta's live rows up to the threshold leave, others stay (CPU)."""
+    rows = make_rows(5, 2000, 2000)
+    store = SyncStore.from_rows(rows, ctx=object())
+    before = {m: store.rowid[store.live_rows(m)].tolist() for m in (1, 2, 3, 7)}
+    k = store.prune(3, 1500)
+    after = store.rowid[store.live_rows(3)].tolist()
+    gt_of = {r[0]: r[1] for r in rows}
+    assert k == len(before[3]) - len(after) > 0
+    assert after == [r for r in before[3] if gt_of[r] > 1500]
+    assert all(store.rowid[store.live_rows(m)].tolist() == before[m] for m in (1, 2, 7))
+    assert store.prune(3, 1500) == 0 and store.prune(99, 10 ** 6) == 0
