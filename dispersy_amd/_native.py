@@ -90,6 +90,7 @@ SIGNATURES = {
     "dsy_dup_check": (ctypes.c_int, [_P, _P, _P, _P, _P, _U64, _P, _U64, _P, _P, _P]),
     "dsy_store_replace": (ctypes.c_int, [_P, _P, _P, _P, _U64, _P, _U64]),
     "dsy_bloom_add_rows": (ctypes.c_int, [_P, ctypes.POINTER(BloomParams), _P, _P, _U64, _P]),
+    "dsy_claim_modulo": (ctypes.c_int, [_P, ctypes.POINTER(BloomParams), _P, _P, _U32, _U64, _U64, _P, _PU64]),
     "dsy_sync_respond": (ctypes.c_int, [_P, _P, ctypes.POINTER(Request), _U32, _P, _U64, ctypes.POINTER(Meta), _U32,
                                         _U64, ctypes.c_int, ctypes.c_int64, _U64, _P, _U64, _P]),
     "dsy_sync_respond_dev": (ctypes.c_int, [_P, _P, ctypes.POINTER(Request), _U32, _P, ctypes.POINTER(Meta), _U32,

@@ -149,6 +149,19 @@ class BloomFilter(object):
                                                  rows.ctypes.data, len(rows), buf))
         self._raw[:] = buf.raw
 
+    def add_store_modulo(self, store, meta_ids, offset, modulo):
+        """The claim side's modulo strategy on the device: select the live rows of `meta_ids` with
+        (global_time + offset) % modulo == 0 (community.py:918, :922) and add their packets (:924) in one call
+        (dsy_claim_modulo).  Returns the number of rows added."""
+        ids = np.ascontiguousarray(meta_ids, dtype=np.uint32)
+        ctx = store.ctx
+        buf = ctypes.create_string_buffer(bytes(self._raw), len(self._raw))
+        count = ctypes.c_uint64(0)
+        _native.check(ctx.lib.dsy_claim_modulo(ctx.handle, ctypes.byref(self.params), store.handle, ids.ctypes.data,
+                                               len(ids), int(offset), int(modulo), buf, ctypes.byref(count)))
+        self._raw[:] = buf.raw
+        return count.value
+
     def clear(self):
         """Set all bits in the filter to zero (bloomfilter.py:196-200)."""
         self._raw[:] = bytes(len(self._raw))

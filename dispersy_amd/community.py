@@ -11,9 +11,10 @@ Kept (same names, argument meaning, return values and statistics):
 and the overridable properties of community.py:599-678, :935-941 (the reference's plugin hooks).
 
 The responder runs as ONE batched call into the HIP library (`respond`): selection, prefix-salted digest, probe
-and byte-limited compaction for every claim of a receive batch.  The claim side selects its packet range on the
-host from the store's index columns (the reference does this in SQLite) and builds the filter on the GPU from the
-store rows already in HBM.
+and byte-limited compaction for every claim of a receive batch.  The claim side's largest strategy selects its
+packet range on the host from the store's index columns (the reference does this in SQLite) and builds the filter on
+the GPU from the store rows already in HBM; the modulo strategy selects and hashes on the device in one call
+(dsy_claim_modulo).
 """
 import ctypes
 import random as _random_module
@@ -410,17 +411,14 @@ class SyncCommunity(object):
         bloom = self._new_claim_filter()
         capacity = bloom.get_capacity(self.dispersy_sync_bloom_filter_error_rate)
         st = self._store
-        live = [st.live_rows(m) for m in syncable]
-        live = np.concatenate(live) if live else np.zeros(0, dtype=np.int64)
-        self._nrsyncpackets = len(live)
+        self._nrsyncpackets = st.count_live(syncable)
         modulo = int(ceil(self._nrsyncpackets / float(capacity)))
         if modulo > 1:
             offset = self._rand.randint(0, modulo - 1)
-            g = st.global_time[live]
-            live = live[(g + np.uint64(offset)) % np.uint64(modulo) == 0]
         else:
             offset, modulo = 0, 1
-        bloom.add_store_rows(st, live)
+        # the SELECTs (:918, :922) and add_keys (:924) run on the device over the store's live index
+        bloom.add_store_modulo(st, syncable, offset, modulo)
         return (1, self.acceptable_global_time, modulo, offset, bloom)
 
     # ----------------------------------------------------------------------------------- responder side

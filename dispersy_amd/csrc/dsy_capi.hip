@@ -1091,6 +1091,51 @@ int dsy_bloom_add_rows(dsy_ctx* c, const dsy_bloom_params* p, const dsy_store* s
     return DSY_OK;
 }
 
+int dsy_claim_modulo(dsy_ctx* c, const dsy_bloom_params* p, const dsy_store* s, const uint32_t* meta_ids,
+                     uint32_t nmeta, uint64_t offset, uint64_t modulo, uint8_t* filter_inout, uint64_t* out_count) {
+    if (!c || !s || !filter_inout || !out_count || (nmeta && !meta_ids)) return fail(DSY_EINVAL, "NULL argument");
+    if (s->ctx != c) return fail(DSY_EINVAL, "store belongs to another context");
+    if (modulo == 0 || offset >= modulo)
+        return fail(DSY_EINVAL, "need 0 <= offset < modulo (offset=%llu modulo=%llu)", (unsigned long long)offset,
+                    (unsigned long long)modulo);
+    int rc = check_params(p);
+    if (rc) return rc;
+    *out_count = 0;
+    std::vector<std::pair<uint64_t, uint64_t>> spans;
+    uint64_t total = 0;
+    for (uint32_t j = 0; j < nmeta; ++j) {
+        auto it = s->segs.find(meta_ids[j]);
+        if (it == s->segs.end() || it->second.first >= it->second.second) continue;
+        spans.push_back(it->second);
+        total += it->second.second - it->second.first;
+    }
+    Guard g(c);
+    const uint64_t nbytes = p->m_bits / 8, words = filter_words(p->m_bits);
+    void *df, *dr, *dn;
+    if ((rc = ws_get(c, "filter", words * 4, &df))) return rc;
+    if ((rc = ws_get(c, "rows", (total + 1) * 8, &dr))) return rc;
+    if ((rc = ws_get(c, "claim_n", 64, &dn))) return rc;
+    HIP_TRY(hipMemsetAsync(df, 0, words * 4, c->stream));
+    HIP_TRY(hipMemcpyAsync(df, filter_inout, nbytes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(dn, 0, 8, c->stream));
+    for (auto& sp : spans)
+        HIP_TRY(launch_claim_modulo(s->d_live_gt, s->d_live_row, sp.first, sp.second, offset, modulo, (uint64_t*)dr,
+                                    (unsigned long long*)dn, c->max_grid, c->stream));
+    uint64_t n = 0;
+    HIP_TRY(hipMemcpyAsync(&n, dn, 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (n > total) return fail(DSY_EHIP, "claim selection counted %llu of %llu rows", (unsigned long long)n,
+                               (unsigned long long)total);
+    if ((rc = run_bloom(c, BloomOp::Add, p, s->d_lines, nullptr, (uint64_t*)dr, n, (uint32_t*)df, nullptr, nullptr,
+                        s->d_rec)))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(filter_inout, df, nbytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    timers_collect_lazy(c);
+    *out_count = n;
+    return DSY_OK;
+}
+
 // -------------------------------------------------------------------------------------------- responder
 // The window pool holds kWindow pairs per claim of the call, and at least kMinSlots claims' worth (16 M pairs,
 // 400 MB of workspace); each window the active claims share it evenly, from kWindow up to kMaxWindow pairs each.

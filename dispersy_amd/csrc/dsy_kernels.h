@@ -211,6 +211,10 @@ hipError_t launch_prune_count(const uint64_t* live_gt, uint64_t a, uint64_t b, u
                               hipStream_t stream);
 hipError_t launch_live_cut(const uint64_t* live_gt, const uint64_t* live_row, uint64_t n_out, uint64_t a, uint64_t k,
                            uint64_t* out_gt, uint64_t* out_row, uint32_t max_grid, hipStream_t stream);
+// claim side, modulo strategy: rows of live segment [a, b) with (gt + offset) % modulo == 0 -> out_rows[*count++]
+hipError_t launch_claim_modulo(const uint64_t* live_gt, const uint64_t* live_row, uint64_t a, uint64_t b,
+                               uint64_t offset, uint64_t modulo, uint64_t* out_rows, unsigned long long* count,
+                               uint32_t max_grid, hipStream_t stream);
 hipError_t launch_ingest_merge(const uint64_t* live_gt, const uint64_t* live_row, uint64_t n_live,
                                const IngestRow* rows, uint64_t a, uint64_t* rank, uint64_t* out_gt, uint64_t* out_row,
                                uint32_t max_grid, hipStream_t stream);

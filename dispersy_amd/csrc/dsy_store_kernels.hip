@@ -135,4 +135,39 @@ hipError_t launch_ingest_merge(const uint64_t* live_gt, const uint64_t* live_row
     return hipGetLastError();
 }
 
+// Claim side, modulo strategy (community.py:908-933): the rows of one meta's live segment [a, b) whose
+// (global_time + offset) % modulo == 0 -- the SELECTs of :918/:922 over the store's index.  One lane per indexed row
+// (8 B of live_gt read, 8 B of live_row for the hits); each wave ranks its hits by ballot and takes one slot range
+// with a single atomic.  The output order is not the index order; the filter the rows go into is an OR, so the
+// claim's bytes do not depend on it.
+__global__ void __launch_bounds__(kIngestThreads) k_claim_modulo(const uint64_t* __restrict__ live_gt,
+                                                                  const uint64_t* __restrict__ live_row, uint64_t a,
+                                                                  uint64_t b, uint64_t offset, uint64_t modulo,
+                                                                  uint64_t* __restrict__ out_rows,
+                                                                  unsigned long long* __restrict__ count) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t stride = (uint64_t)gridDim.x * kIngestThreads;
+    for (uint64_t base = a + (uint64_t)blockIdx.x * kIngestThreads + (threadIdx.x & ~63u); base < b; base += stride) {
+        const uint64_t i = base + lane;
+        const bool hit = i < b && (live_gt[i] + offset) % modulo == 0;
+        const uint64_t mask = __ballot(hit);
+        if (!mask) continue;
+        unsigned long long at = 0;
+        if (lane == 0) at = atomicAdd(count, (unsigned long long)__popcll(mask));
+        at = __shfl(at, 0);
+        if (hit) out_rows[at + __popcll(mask & ((1ull << lane) - 1))] = live_row ? live_row[i] : i;
+    }
+}
+
+hipError_t launch_claim_modulo(const uint64_t* live_gt, const uint64_t* live_row, uint64_t a, uint64_t b,
+                               uint64_t offset, uint64_t modulo, uint64_t* out_rows, unsigned long long* count,
+                               uint32_t max_grid, hipStream_t stream) {
+    if (b <= a) return hipSuccess;
+    uint64_t g = (b - a + kIngestThreads - 1) / kIngestThreads;
+    if (g > (uint64_t)max_grid * 4) g = (uint64_t)max_grid * 4;
+    hipLaunchKernelGGL(k_claim_modulo, dim3((uint32_t)g), dim3(kIngestThreads), 0, stream, live_gt, live_row, a, b,
+                       offset, modulo, out_rows, count);
+    return hipGetLastError();
+}
+
 }  // namespace dsy

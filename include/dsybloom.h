@@ -205,6 +205,12 @@ int dsy_store_replace(dsy_ctx* ctx, dsy_store* store, const uint64_t* rows, cons
  * filter.  rows are store row positions (0-based, export order). */
 int dsy_bloom_add_rows(dsy_ctx* ctx, const dsy_bloom_params* p, const dsy_store* store, const uint64_t* rows,
                        uint64_t n, uint8_t* filter_inout);
+/* Claim side, modulo strategy: replaces the SELECT of _dispersy_claim_sync_bloom_filter_modulo
+ * (community.py:918, :922) and its add_keys (:924).  Selects, on the device, the live rows (undone == 0) of the given
+ * metas with (global_time + offset) % modulo == 0 and ORs their packets into the filter; *out_count = rows added.
+ * 0 <= offset < modulo, else DSY_EINVAL. */
+int dsy_claim_modulo(dsy_ctx* ctx, const dsy_bloom_params* p, const dsy_store* store, const uint32_t* meta_ids,
+                     uint32_t nmeta, uint64_t offset, uint64_t modulo, uint8_t* filter_inout, uint64_t* out_count);
 
 /* ------------------------------------------------------------------------------------------- responder */
 /* Batched responder: replaces _get_packets_for_bloomfilters (community.py:2746-2811) plus the byte-limited
