@@ -51,10 +51,11 @@ def parse():
     ap.add_argument("--sim-initial", type=int, default=100)
     ap.add_argument("--sim-rounds", type=int, default=10)
     ap.add_argument("--sim-warmup", type=int, default=2)
-    ap.add_argument("--extra", default="dedup,ingest,1,3,4,5",
+    ap.add_argument("--extra", default="claim,dedup,ingest,1,3,4,5",
                     help="BASELINE configs measured beside the headline (config 2): 1 single filter, 3 gossip "
                          "simulator, 4 large filters, 5 heavy-tailed packets, ingest: received packets appended to "
-                         "the headline store, dedup: duplicate check of received packets against it; '' for none")
+                         "the headline store, dedup: duplicate check of received packets against it, claim: modulo claims built "
+                         "over it on the device; '' for none")
     ap.add_argument("--large-keys", type=int, default=100_000_000, help="config 4: keys added per filter")
     ap.add_argument("--large-tests", type=int, default=10_000_000, help="config 4: keys tested per filter")
     return ap.parse_args()
@@ -232,6 +233,9 @@ def main():
 
     ingest = None
     dedup = None
+    claim = None
+    if "claim" in extra:
+        claim = claim_bench(args, ctx, lib, store, N, capacity, total_bytes / N, cpu_leg=rank == 0 and world == 1)
     if "dedup" in extra:
         dedup = dedup_bench(args, ctx, lib, store, blob, offsets, N, cpu_leg=rank == 0 and world == 1)
     if "ingest" in extra:
@@ -285,6 +289,7 @@ def main():
             "heavy_tail": heavy,
             "ingest": ingest,
             "dedup": dedup,
+            "claim_modulo": claim,
         }
         print(json.dumps(line))
     if store is not None:
@@ -369,6 +374,62 @@ def dedup_bench(args, ctx, lib, store, blob, offsets, N, batch=10_000, reps=10, 
             "index_build_ms": round(build_ms, 2), "median_ms_per_batch": round(ms, 3),
             "messages_per_s": round(batch / (ms / 1e3), 1), "found_exact": exact, "found_new": new,
             "cpu_baseline": cpu}
+
+
+def claim_bench(args, ctx, lib, store, N, capacity, mean_len, reps=20, cpu_leg=True):
+    """SURVEY §8f row 4, the requester's modulo claim (_dispersy_claim_sync_bloom_filter_modulo,
+    community.py:908-933) over the headline's 10 M-packet store: modulo = ceil(N / capacity), a random offset per
+    claim; dsy_claim_modulo scans the meta's live index for the residue class and hashes the hits into the MTU filter.
+    Wall time per call (filter up and down the bus included).  Algorithmic bytes per claim: 8 B of global_time per
+    indexed row + 8 B row id and the packet bytes of every hit."""
+    from dispersy_amd.bloomfilter import BloomFilter
+    rng = np.random.Generator(np.random.PCG64(77))
+    modulo = int(np.ceil(N / float(capacity)))
+    ids = np.asarray([1], dtype=np.uint32)
+    count = ctypes.c_uint64(0)
+    times, hits = [], []
+    for r in range(reps + 2):
+        bf = BloomFilter(args.filter_bits, args.error_rate, bytes([int(rng.integers(0, 256))]))
+        buf = ctypes.create_string_buffer(bytes(bf._raw), len(bf._raw))
+        offset = int(rng.integers(0, modulo))
+        t0 = time.perf_counter()
+        _native.check(lib.dsy_claim_modulo(ctx.handle, ctypes.byref(bf.params), store, ids.ctypes.data, 1, offset,
+                                           modulo, buf, ctypes.byref(count)))
+        if r >= 2:
+            times.append(time.perf_counter() - t0)
+            hits.append(count.value)
+    ms = sorted(times)[len(times) // 2] * 1e3
+    hit = float(np.mean(hits))
+    alg_bytes = 8.0 * N + hit * (8 + mean_len)
+    cpu = None
+    if cpu_leg and args.cpu_claims > 0:  # the reference's SELECT (community.py:918) in sqlite + hashlib add_keys
+        import sqlite3
+        from oracle.bloom_ref import OracleBloom
+        from oracle.sync_ref import SYNC_SCHEMA
+        pre = 1_000_000
+        crng = np.random.Generator(np.random.PCG64(8))
+        conn = sqlite3.connect(":memory:")
+        conn.executescript(SYNC_SCHEMA)
+        conn.executemany("INSERT INTO sync (community, member, global_time, meta_message, packet) VALUES (1, ?, ?, 1, ?)",
+                         ((i, i + 1, crng.bytes(int(l))) for i, l in enumerate(crng.integers(100, 1501, size=pre))))
+        conn.commit()
+        cmod = int(np.ceil(pre / float(capacity)))
+        t0 = time.perf_counter()
+        nclaims = 3
+        for c in range(nclaims):
+            ob = OracleBloom.from_m_f(args.filter_bits, args.error_rate, bytes([c]))
+            ob.add_keys([bytes(p) for p, in conn.execute(
+                "SELECT sync.packet FROM sync WHERE meta_message IN (1) AND sync.undone = 0 "
+                "AND (sync.global_time + ?) % ? = 0", (c, cmod))])
+        dt = time.perf_counter() - t0
+        conn.close()
+        cpu = {"value": round(nclaims * pre / dt, 1), "unit": "indexed rows/s", "cores": 1, "kind": "port",
+               "sample": "%d modulo claims (modulo %d) through the reference's SELECT (community.py:918) on an in-memory "
+                         "sqlite3 sync table of %d rows + hashlib add_keys of the hits" % (nclaims, cmod, pre)}
+    return {"metric": "modulo claims built/sec", "store_rows": N, "modulo": modulo, "mean_hits": round(hit, 1),
+            "median_ms_per_claim": round(ms, 3), "claims_per_s": round(1e3 / ms, 1),
+            "indexed_rows_per_s": round(N / (ms / 1e3), 1),
+            "achieved_gbs": round(alg_bytes / (ms / 1e3) / 1e9, 1), "cpu_baseline": cpu}
 
 
 def ingest_bench(args, ctx, lib, store, step, pairs, N, batch=10_000, batches=10, cpu_leg=True):
