@@ -138,24 +138,39 @@ hipError_t launch_ingest_merge(const uint64_t* live_gt, const uint64_t* live_row
 // Claim side, modulo strategy (community.py:908-933): the rows of one meta's live segment [a, b) whose
 // (global_time + offset) % modulo == 0 -- the SELECTs of :918/:922 over the store's index.  One lane per indexed row
 // (8 B of live_gt read, 8 B of live_row for the hits); each wave ranks its hits by ballot and takes one slot range
-// with a single atomic.  The output order is not the index order; the filter the rows go into is an OR, so the
-// claim's bytes do not depend on it.
+// with a single atomic; the residue comes from a 64-bit Barrett step (a multiply-high and one correction) instead
+// of a software 64-bit division.  The output order is not the index order; the filter the rows go into is an OR,
+// so the claim's bytes do not depend on it.
 __global__ void __launch_bounds__(kIngestThreads) k_claim_modulo(const uint64_t* __restrict__ live_gt,
                                                                   const uint64_t* __restrict__ live_row, uint64_t a,
                                                                   uint64_t b, uint64_t offset, uint64_t modulo,
-                                                                  uint64_t* __restrict__ out_rows,
+                                                                  uint64_t recip, uint64_t* __restrict__ out_rows,
                                                                   unsigned long long* __restrict__ count) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t stride = (uint64_t)gridDim.x * kIngestThreads;
-    for (uint64_t base = a + (uint64_t)blockIdx.x * kIngestThreads + (threadIdx.x & ~63u); base < b; base += stride) {
-        const uint64_t i = base + lane;
-        const bool hit = i < b && (live_gt[i] + offset) % modulo == 0;
-        const uint64_t mask = __ballot(hit);
-        if (!mask) continue;
-        unsigned long long at = 0;
-        if (lane == 0) at = atomicAdd(count, (unsigned long long)__popcll(mask));
-        at = __shfl(at, 0);
-        if (hit) out_rows[at + __popcll(mask & ((1ull << lane) - 1))] = live_row ? live_row[i] : i;
+    const uint64_t stride = (uint64_t)gridDim.x * kIngestTile;
+    // each wave covers kIngestPerThread x 64 consecutive rows per step, all loads issued before the first ballot
+    for (uint64_t base = a + (uint64_t)blockIdx.x * kIngestTile + (uint64_t)(threadIdx.x >> 6) * 64 * kIngestPerThread;
+         base < b; base += stride) {
+        uint64_t x[kIngestPerThread];
+#pragma unroll
+        for (uint32_t u = 0; u < kIngestPerThread; ++u) {
+            const uint64_t i = base + u * 64 + lane;
+            x[u] = i < b ? live_gt[i] + offset : 0;  // lanes past the segment are masked below
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kIngestPerThread; ++u) {
+            const uint64_t i = base + u * 64 + lane;
+            // x % modulo by Barrett: q = floor(x * recip / 2^64) is floor(x / modulo) or one less
+            uint64_t r = x[u] - __umul64hi(x[u], recip) * modulo;
+            if (r >= modulo) r -= modulo;
+            const bool hit = i < b && r == 0;
+            const uint64_t mask = __ballot(hit);
+            if (!mask) continue;
+            unsigned long long at = 0;
+            if (lane == 0) at = atomicAdd(count, (unsigned long long)__popcll(mask));
+            at = __shfl(at, 0);
+            if (hit) out_rows[at + __popcll(mask & ((1ull << lane) - 1))] = live_row ? live_row[i] : i;
+        }
     }
 }
 
@@ -163,10 +178,11 @@ hipError_t launch_claim_modulo(const uint64_t* live_gt, const uint64_t* live_row
                                uint64_t offset, uint64_t modulo, uint64_t* out_rows, unsigned long long* count,
                                uint32_t max_grid, hipStream_t stream) {
     if (b <= a) return hipSuccess;
-    uint64_t g = (b - a + kIngestThreads - 1) / kIngestThreads;
+    uint64_t g = (b - a + kIngestTile - 1) / kIngestTile;
     if (g > (uint64_t)max_grid * 4) g = (uint64_t)max_grid * 4;
+    const uint64_t recip = ~0ull / modulo;  // floor((2^64 - 1) / modulo): one correction step suffices
     hipLaunchKernelGGL(k_claim_modulo, dim3((uint32_t)g), dim3(kIngestThreads), 0, stream, live_gt, live_row, a, b,
-                       offset, modulo, out_rows, count);
+                       offset, modulo, recip, out_rows, count);
     return hipGetLastError();
 }
 
