@@ -484,9 +484,16 @@ class SyncCommunity(object):
     def respond_wire(self, blocks, include_inactive=False, byte_limit=None, random_seed=None):
         """on_introduction_request's sync half for a receive batch of raw sync blocks: decode (conversion.py:732-799,
         time_high 0 resolved to this community's global time, community.py:2545-2553) and answer every good claim
-        in one responder call.  Returns, per block, a DropPacket (the decoder's verdict) or the store rows to send."""
-        from .conversion import DROP_REASONS, DropPacket, decode_sync_blocks
+        in one responder call.  Returns, per block, a DropPacket (the decoder's verdict) or the store rows to send.
+        A block whose filter the BloomFilter constructor rejects raises AssertionError for the whole batch, as the
+        reference's decode loop does."""
+        from .conversion import DECODE_ASSERT, DROP_REASONS, DropPacket, decode_sync_blocks, raise_for_status
         batch = decode_sync_blocks(blocks, responder_global_time=self.global_time)
+        asserting = np.flatnonzero(batch.status == DECODE_ASSERT)
+        if len(asserting):
+            # the reference's decode loop dies on this block's AssertionError (community.py:2078-2090 catches only
+            # DropPacket/DelayPacket): no claim of the batch is answered
+            raise_for_status(DECODE_ASSERT, int(asserting[0]))
         good = np.flatnonzero(batch.status == 0)
         sub = (_native.Request * max(len(good), 1))(*[batch.requests[int(i)] for i in good])
         rows = self._respond_requests(sub, len(good), batch.filters, include_inactive, byte_limit, random_seed)

@@ -10,6 +10,7 @@ straight into the dsy_request records and aligned filter words the batched respo
 is built per claim.  The single-block helpers raise `DropPacket` with the reference's messages.
 """
 import ctypes
+import struct
 from collections import namedtuple
 
 import numpy as np
@@ -17,7 +18,7 @@ import numpy as np
 from . import _native
 from .bloomfilter import BloomFilter
 
-__all__ = ["DropPacket", "DROP_REASONS", "SyncBatch", "decode_sync_blocks", "encode_sync_blocks",
+__all__ = ["DropPacket", "DROP_REASONS", "DECODE_ASSERT", "SyncBatch", "raise_for_status", "decode_sync_blocks", "encode_sync_blocks",
            "decode_sync_block", "encode_sync_block"]
 
 SYNC_HEADER = _native.SYNC_HEADER
@@ -38,8 +39,14 @@ DROP_REASONS = {
     7: "Invalid size value",
     8: "Invalid size value, must be a multiple of eight",
     9: "Invalid number of bytes available",
-    10: "Invalid bloom filter parameters",  # BloomFilter(bytes, k) asserts (bloomfilter.py:128-156)
 }
+# status DSY_DECODE_ASSERT: the BloomFilter(bytes, k, prefix) constructor the decoder ends with (conversion.py:791)
+# asserts 0 < k <= m and a <= 512-bit digest (bloomfilter.py:129, :144).  The reference raises that AssertionError out
+# of the decoder -- no DropPacket -- and nothing on the receive path catches it (community.py:2086 catches DropPacket
+# only), so the whole receive batch is abandoned.  Pinned by tests/golden/codec_vectors.json.
+DECODE_ASSERT = 10
+
+_U64 = (1 << 64) - 1
 
 # a decoded receive batch: ctypes array of dsy_request (one per block; zeroed where status != 0), the packed
 # filter words they point into, and the per-block status
@@ -77,6 +84,10 @@ def encode_sync_blocks(claims):
         assert bloom.size % 8 == 0
         assert 0 < bloom.functions < 256
         assert len(bloom.prefix) == 1, "must have a one character prefix"
+        # struct '>QQHHBH' (:727): a field that does not fit raises struct.error, as Struct.pack does
+        if not (0 <= time_low <= _U64 and 0 <= time_high <= _U64 and 0 <= modulo <= 0xFFFF and
+                0 <= offset <= 0xFFFF and bloom.size <= 0xFFFF):
+            raise struct.error("sync block field out of range for '>QQHHBH'")
         q = reqs[i]
         q.time_low, q.time_high, q.modulo, q.offset = time_low, time_high, modulo, offset
         q.m_bits, q.k, q.prefix_len = bloom.size, bloom.functions, 1
@@ -98,12 +109,22 @@ def encode_sync_block(time_low, time_high, modulo, offset, bloom_filter):
     return encode_sync_blocks([(time_low, time_high, modulo, offset, bloom_filter)])[0]
 
 
+def raise_for_status(status, index=0):
+    """The reference's verdict for a non-zero dsy_sync_decode status: DropPacket, or the AssertionError of the
+    BloomFilter constructor (DECODE_ASSERT)."""
+    if status == DECODE_ASSERT:
+        raise AssertionError("BloomFilter(bytes, functions, prefix) of sync block %d asserts (bloomfilter.py:129, :144)"
+                             % index)
+    raise DropPacket(DROP_REASONS.get(status, "Invalid sync block (%d)" % status))
+
+
 def decode_sync_block(data):
-    """(time_low, time_high, modulo, offset, BloomFilter) of one sync block, or DropPacket (conversion.py:762-794)."""
+    """(time_low, time_high, modulo, offset, BloomFilter) of one sync block; DropPacket with the reference's message
+    (conversion.py:762-789), or AssertionError where its BloomFilter constructor asserts (:791)."""
     batch = decode_sync_blocks([data])
     st = int(batch.status[0])
     if st:
-        raise DropPacket(DROP_REASONS.get(st, "Invalid sync block (%d)" % st))
+        raise_for_status(st)
     q = batch.requests[0]
     raw = batch.filters[q.filter_offset:q.filter_offset + q.m_bits // 8]
     return q.time_low, q.time_high, q.modulo, q.offset, BloomFilter(raw, q.k, bytes([q.prefix[0]]))

@@ -71,7 +71,9 @@ int dsy_sync_decode(const uint8_t* blob, const uint64_t* offsets, uint32_t n, ui
             else if (!(0 < size)) st = DSY_DROP_SIZE_VALUE;
             else if (size % 8) st = DSY_DROP_SIZE_MULT8;
             else if (length != len - DSY_SYNC_HEADER) st = DSY_DROP_LENGTH;
-            else if (functions > size || !family_of(size, functions, &kind, &chunk)) st = DSY_DROP_FAMILY;
+            // BloomFilter(bytes, functions, prefix) (:791) asserts 0 < k <= m and a <= 512-bit digest
+            // (bloomfilter.py:129, :144): an AssertionError, not a DropPacket, and nothing on the decode path catches it
+            else if (functions > size || !family_of(size, functions, &kind, &chunk)) st = DSY_DECODE_ASSERT;
             if (st == DSY_DROP_OK) {
                 const uint64_t words = (size + 31) / 32;
                 if (at + words * 4 > filters_cap) {
@@ -112,9 +114,10 @@ int dsy_sync_encode(const dsy_request* reqs, uint32_t n, const uint8_t* filters,
     out_offsets[0] = 0;
     for (uint32_t i = 0; i < n; ++i) {
         const dsy_request& q = reqs[i];
-        // conversion.py:723-726 asserts, and the '>QQHHBH' field widths
+        // conversion.py:723-726 asserts and the '>QQHHBH' field widths (struct.error in the reference); like the
+        // reference, the encoder does not check what only the decoder validates (time_low > 0, offset < modulo, ...)
         if (q.m_bits == 0 || q.m_bits % 8 || q.m_bits > 0xffff || q.k == 0 || q.k > 255 || q.prefix_len != 1 ||
-            q.modulo == 0 || q.modulo > 0xffff || q.offset >= q.modulo)
+            q.modulo > 0xffff || q.offset > 0xffff)
             return DSY_EINVAL;
         const uint64_t length = q.m_bits / 8, need = DSY_SYNC_HEADER + length;
         if (at + need > out_cap) {

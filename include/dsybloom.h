@@ -263,8 +263,11 @@ int dsy_filter_or_reduce(dsy_ctx* ctx, const uint32_t* d_parts, uint32_t n_parts
 #define DSY_DROP_SIZE_VALUE 7  /* "Invalid size value"                       :782-783 */
 #define DSY_DROP_SIZE_MULT8 8  /* "Invalid size value, must be a multiple of eight"  :784-785 */
 #define DSY_DROP_LENGTH 9      /* "Invalid number of bytes available"        :787-789 */
-#define DSY_DROP_FAMILY 10     /* BloomFilter(bytes, k) would assert: (m, k) needs > 512 digest bits or k > m
-                                  (bloomfilter.py:128-156) */
+/* Not a DropPacket: BloomFilter(bytes, k, prefix) (conversion.py:791) asserts when k > m or (m, k) needs more than 512
+ * digest bits (bloomfilter.py:129, :144).  That AssertionError leaves _decode_introduction_request uncaught (only
+ * DropPacket is caught, community.py:2086), so the reference abandons the whole receive batch; the Python binding
+ * raises AssertionError for it (pinned by tests/golden/codec_vectors.json). */
+#define DSY_DECODE_ASSERT 10
 /* blob + offsets[n+1]: each item is one sync block (from its first byte to the end of the payload).  When
  * responder_global_time != 0, time_high == 0 is resolved to it and both bounds are clamped to 2^63-1 as
  * on_introduction_request does (community.py:2545-2553).  If out_filters is too small, DSY_ECAPACITY is returned
@@ -272,8 +275,9 @@ int dsy_filter_or_reduce(dsy_ctx* ctx, const uint32_t* d_parts, uint32_t n_parts
 int dsy_sync_decode(const uint8_t* blob, const uint64_t* offsets, uint32_t n, uint64_t responder_global_time,
                     dsy_request* out_reqs, uint8_t* out_filters, uint64_t filters_cap, uint64_t* out_filters_len,
                     int32_t* out_status);
-/* Encode n claims (prefix_len 1, 0 < k < 256, m % 8 == 0, m < 2^16 -- the wire's field widths and the asserts of
- * conversion.py:723-726) into out; out_offsets[n+1] delimit the blocks. */
+/* Encode n claims (prefix_len 1, 0 < k < 256, m % 8 == 0 -- the asserts of conversion.py:723-726 --, and m, modulo,
+ * offset < 2^16 -- the '>QQHHBH' field widths) into out; out_offsets[n+1] delimit the blocks.  Values only the
+ * decoder rejects (time_low 0, offset >= modulo, ...) are encoded as given, as the reference does. */
 int dsy_sync_encode(const dsy_request* reqs, uint32_t n, const uint8_t* filters, uint8_t* out, uint64_t out_cap,
                     uint64_t* out_offsets);
 

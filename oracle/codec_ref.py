@@ -3,8 +3,10 @@
 Restatement of the introduction-request sync block codec of the reference: encode conversion.py:721-728, decode
 conversion.py:762-794 (struct '>QQHHBH' of conversion.py:193, checks in the reference's order, the DropPacket
 messages verbatim), plus the BloomFilter(bytes, functions, prefix) constructor asserts the decode ends with
-(bloomfilter.py:79-87, :125-156).  Parity pinning: the reference's conversion.py needs Twisted/M2Crypto and cannot
-be imported here, so this restatement is pinned by the format string and the checks it quotes.
+(bloomfilter.py:79-87, :125-156).  Parity pinning: tests/golden/codec_vectors.json holds the verdicts of the
+reference's own _decode_introduction_request / _encode_introduction_request (lifted from conversion.py's AST by
+tests/golden/gen_codec_golden.py) for 2400 fuzzed payloads and 171 claims; tests/test_oracle_golden.py checks this
+restatement against them.
 """
 import struct
 from math import ceil
@@ -19,6 +21,7 @@ class DropPacket(Exception):
 
 
 def encode(time_low, time_high, modulo, offset, functions, size, prefix, filter_bytes):
+    """conversion.py:723-728: the asserts, then struct.pack (struct.error for a field that does not fit)."""
     assert size % 8 == 0
     assert 0 < functions < 256
     assert len(prefix) == 1
@@ -51,11 +54,8 @@ def decode(data, offset=0):
     length = size // 8
     if not length == len(data) - offset:
         raise DropPacket("Invalid number of bytes available")
-    # BloomFilter(data[offset:], functions, prefix=prefix): 0 < k <= m and a digest of <= 512 bits
-    if functions > size:
-        raise DropPacket("Invalid bloom filter parameters")
-    try:
-        hash_family(size, functions)
-    except AssertionError:
-        raise DropPacket("Invalid bloom filter parameters")
+    # BloomFilter(data[offset:], functions, prefix=prefix) (conversion.py:791) asserts 0 < k <= m
+    # (bloomfilter.py:129) and a digest of <= 512 bits (:144): AssertionError, not a DropPacket
+    assert 0 < functions <= size, [functions, size]
+    hash_family(size, functions)
     return time_low, time_high, modulo, modulo_offset, functions, size, prefix, bytes(data[offset:offset + length])

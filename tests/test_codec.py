@@ -8,7 +8,7 @@ import pytest
 
 from dispersy_amd import _native
 from dispersy_amd.bloomfilter import BloomFilter
-from dispersy_amd.conversion import (DROP_REASONS, DropPacket, decode_sync_block, decode_sync_blocks,
+from dispersy_amd.conversion import (DECODE_ASSERT, DROP_REASONS, DropPacket, decode_sync_block, decode_sync_blocks,
                                      encode_sync_block, encode_sync_blocks)
 from oracle import codec_ref
 
@@ -28,6 +28,12 @@ def oracle_status(data):
         return None
     except codec_ref.DropPacket as e:
         return str(e)
+    except AssertionError:
+        return "AssertionError"
+
+
+def status_text(code):
+    return None if code == 0 else "AssertionError" if code == DECODE_ASSERT else DROP_REASONS[code]
 
 
 def test_round_trip_mtu_claim():
@@ -48,13 +54,23 @@ def test_round_trip_mtu_claim():
     (dict(functions=0), "Invalid functions value"),
     (dict(size=0), "Invalid size value"),
     (dict(size=10161), "Invalid size value, must be a multiple of eight"),
-    (dict(functions=200, size=40000), "Invalid bloom filter parameters"),
-    (dict(functions=255, size=8), "Invalid bloom filter parameters"),
 ])
 def test_drop_reasons(kwargs, reason):
     data = block(**kwargs)
     assert oracle_status(data) == reason
     with pytest.raises(DropPacket, match="^" + reason.replace("(", r"\(") + "$"):
+        decode_sync_block(data)
+
+
+@pytest.mark.parametrize("kwargs", [dict(functions=200, size=40000), dict(functions=255, size=8),
+                                    dict(functions=33, size=10160), dict(functions=17, size=32768)])
+def test_bloom_constructor_asserts_are_not_drops(kwargs):
+    """k > m or more than 512 digest bits: the reference's BloomFilter(bytes, k, prefix) asserts inside the decoder
+    (bloomfilter.py:129, :144) -- an AssertionError, not a DropPacket (tests/golden/codec_vectors.json)."""
+    data = block(**kwargs)
+    assert oracle_status(data) == "AssertionError"
+    assert int(decode_sync_blocks([data]).status[0]) == DECODE_ASSERT
+    with pytest.raises(AssertionError):
         decode_sync_block(data)
 
 
@@ -85,7 +101,7 @@ def test_batch_fuzz_against_oracle():
     for i, data in enumerate(blocks):
         want = oracle_status(data)
         got = int(batch.status[i])
-        assert (DROP_REASONS[got] if got else None) == want, i
+        assert status_text(got) == want, i
         if not got:
             lo, hi, mod, off, k, m, prefix, body = codec_ref.decode(data)
             q = batch.requests[i]
@@ -98,6 +114,87 @@ def test_batch_fuzz_against_oracle():
 def test_encode_rejects_what_the_wire_cannot_carry():
     with pytest.raises(AssertionError):
         encode_sync_block(1, 0, 1, 0, BloomFilter(10160, 0.01, prefix=b"ab"))
+    with pytest.raises(struct.error):
+        encode_sync_block(1, 0, 65536, 0, BloomFilter(4096, 0.001, prefix=b"a"))
+    # only the decoder validates time_low / modulo / offset: the encoder writes them as given (conversion.py:727)
+    raw = encode_sync_block(0, 0, 0, 3, BloomFilter(4096, 0.001, prefix=b"a"))
+    assert HDR.unpack_from(raw)[:4] == (0, 0, 0, 3)
     many = encode_sync_blocks([(i + 1, 0, 7, i % 7, BloomFilter(4096, 0.001, prefix=bytes([i]))) for i in range(50)])
     assert all(len(b) == 24 + 512 for b in many)
     assert [decode_sync_block(b)[:4] for b in many] == [(i + 1, 0, 7, i % 7) for i in range(50)]
+
+
+# ------------------------------------------------------------------ pinned by the reference (codec_vectors.json)
+def _golden_decode_cases():
+    import hashlib
+    import codec_cases
+    from golden_util import load
+    vec = load("codec_vectors.json")["decode"]
+    payloads = codec_cases.decode_payloads()
+    assert len(payloads) == len(vec)
+    out = []
+    for p, rec in zip(payloads, vec):
+        assert hashlib.sha256(p).hexdigest()[:16] == rec["sha256"], "codec_cases drifted from the golden file"
+        flags = p[18]
+        if rec.get("drop") == "Invalid connection type flag" or not flags & 0x02:
+            continue  # decided by the introduction-request header before the sync block (conversion.py:751-761)
+        out.append((p[21:], rec))
+    return out
+
+
+def _expected(rec):
+    if "drop" in rec:
+        return rec["drop"]
+    if "error" in rec:
+        return rec["error"]
+    return None
+
+
+def test_decode_matches_reference_vectors():
+    """dsy_sync_decode reproduces the reference decoder's verdict on every fuzzed sync block: the decoded claim
+    (filter bytes by digest), the DropPacket message, or the BloomFilter constructor's AssertionError."""
+    import hashlib
+    cases = _golden_decode_cases()
+    assert len(cases) > 2000
+    blocks = [b for b, _ in cases]
+    batch = decode_sync_blocks(blocks, responder_global_time=0)
+    kinds = set()
+    for i, (blk, rec) in enumerate(cases):
+        want = _expected(rec)
+        kinds.add(want)
+        assert status_text(int(batch.status[i])) == want, (i, rec)
+        assert oracle_status(blk) == want, (i, rec)
+        if want is None:
+            s, q = rec["sync"], batch.requests[i]
+            assert (q.time_low, q.time_high, q.modulo, q.offset, q.k, q.m_bits) == (
+                s["time_low"], s["time_high"], s["modulo"], s["offset"], s["functions"], s["size"])
+            assert bytes([q.prefix[0]]).hex() == s["prefix"]
+            body = batch.filters[q.filter_offset:q.filter_offset + q.m_bits // 8]
+            assert hashlib.sha256(body).hexdigest()[:16] == s["filter_sha256"]
+    assert "AssertionError" in kinds and None in kinds and "Invalid offset value" in kinds
+
+
+def test_encode_matches_reference_vectors():
+    import hashlib
+    import codec_cases
+    from golden_util import load
+    for rec in load("codec_vectors.json")["encode"]:
+        time_low, time_high, modulo, offset, m, k, prefix, seed = rec["claim"]
+        body = codec_cases.filter_body(m, seed)
+        try:
+            bf = BloomFilter(body, k, bytes.fromhex(prefix))
+        except AssertionError:
+            assert rec.get("error") == "AssertionError" and rec.get("stage") == "BloomFilter", rec
+            continue
+        try:
+            raw = encode_sync_block(time_low, time_high, modulo, offset, bf)
+        except AssertionError:
+            assert rec.get("error") == "AssertionError", rec
+            continue
+        except struct.error:
+            assert rec.get("error") == "error", rec  # struct.error
+            continue
+        assert "error" not in rec, rec
+        assert len(raw) == rec["length"] and hashlib.sha256(raw).hexdigest() == rec["sha256"]
+        if "hex" in rec:
+            assert raw.hex() == rec["hex"]

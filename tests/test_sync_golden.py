@@ -200,3 +200,18 @@ def test_respond_wire_matches_reference(sc):
         assert store.rowid[out[1]].tolist() == res["response"], req
         n += 1
     assert n > 0
+
+
+def test_respond_wire_batch_dies_on_a_bloom_constructor_assert():
+    """A sync block whose (k, m) the reference's BloomFilter constructor rejects makes _decode_introduction_request
+    raise AssertionError, which the batch loop does not catch (community.py:2078-2090): no claim of the batch is
+    answered.  respond_wire raises before any responder work (host-side decode only, no GPU call)."""
+    import struct as _struct
+    from dispersy_amd.conversion import encode_sync_blocks
+    sc = SYNC["respond"][0]
+    store = store_of(sc["rows"])
+    com = SyncCommunity(store, metas_of(sc["metas"]), global_time=500)
+    [good] = encode_sync_blocks([(1, 0, 1, 0, BloomFilter(4096, 0.001, b"x"))])
+    asserting = _struct.pack(">QQHHBH", 1, 0, 1, 0, 40, 4096) + b"x" + bytes(512)  # k=40 needs 640 digest bits
+    with pytest.raises(AssertionError):
+        com.respond_wire([good, asserting, good])
