@@ -18,6 +18,7 @@ the GPU from the store rows already in HBM; the modulo strategy selects and hash
 """
 import ctypes
 import random as _random_module
+import time as _time
 from collections import OrderedDict, namedtuple
 from math import ceil
 
@@ -83,9 +84,11 @@ class SyncCommunity(object):
     _SKIP_CURVE_STEPS = [0, 0, 0.1, 0.2, 0.3, 0.4, 0.5, 0.6, 0.7, 0.8, 0.9]
     _SKIP_STEPS = len(_SKIP_CURVE_STEPS)
 
-    def __init__(self, store, meta_messages, global_time=0, signature_length=60, rng=None, random_source=None):
+    def __init__(self, store, meta_messages, global_time=0, signature_length=60, rng=None, random_source=None,
+                 clock=None):
         """rng: the community's private Random (expovariate pivot, community.py:778-780); random_source: provider of
-        the module-level random()/randint() draws (prefix, skip, modulo offset).  Both default to `random`."""
+        the module-level random()/randint() draws (prefix, skip, modulo offset).  Both default to `random`.
+        clock: the time() acceptable_global_time's 5-second cache reads (default time.time)."""
         self._store = store
         self._meta_messages = OrderedDict((m.name, m) for m in meta_messages)
         self._global_time = global_time
@@ -97,6 +100,10 @@ class SyncCommunity(object):
         self._sync_cache_skip_count = 0
         self._nrsyncpackets = 0
         self.dispersy_acceptable_global_time_range = 10000  # community.py:952-953
+        self._clock = clock if clock is not None else _time.time
+        self._verified_candidates = []
+        self._acceptable_global_time_deadline = 0.0  # community.py:294, :392
+        self._acceptable_global_time_cache = global_time
         self.sent_packets = []  # (candidate, packet, reason) the checks answer with (Dispersy._send_packets)
         # community.py:430-431
         self._do_pruning = any(isinstance(m.distribution, SyncDistribution) and
@@ -141,12 +148,29 @@ class SyncCommunity(object):
     def global_time(self):
         return max(1, self._global_time)
 
+    def dispersy_yield_verified_candidates(self):
+        """The candidates whose global-time opinion counts (community.py:1036).  The walker that keeps them is out of
+        scope, so the caller supplies them with set_verified_candidates (objects with a .global_time)."""
+        return iter(self._verified_candidates)
+
+    def set_verified_candidates(self, candidates):
+        self._verified_candidates = list(candidates)
+
     @property
     def acceptable_global_time(self):
-        """community.py:1015-1058, the branch without >5 candidate opinions (the walker is out of scope)."""
+        """community.py:1015-1058: the highest global time accepted for incoming messages -- the median of the
+        candidates' opinions when there are more than 5 (the lower middle one, a py2 floor index), else our own
+        global time, plus dispersy_acceptable_global_time_range, at most 2^63-1; recomputed at most every 5 s."""
         if not self.dispersy_enable_bloom_filter_sync:
             return MAX_GT
-        return min(self._global_time + self.dispersy_acceptable_global_time_range, MAX_GT)
+        now = self._clock()
+        if self._acceptable_global_time_deadline < now:
+            options = sorted(g for g in (c.global_time for c in self.dispersy_yield_verified_candidates()) if g > 0)
+            median_global_time = options[len(options) // 2] if len(options) > 5 else 0
+            self._acceptable_global_time_cache = min(max(self._global_time, median_global_time) +
+                                                     self.dispersy_acceptable_global_time_range, MAX_GT)
+            self._acceptable_global_time_deadline = now + 5.0
+        return self._acceptable_global_time_cache
 
     def update_global_time(self, global_time):
         """community.py:1082-1096: raise the global time; with GlobalTimePruning metas, DELETE their packets that

@@ -386,7 +386,73 @@ def claim_state_machine(B, funcs, schema):
     return dict(metas=meta_json(spec), rows=rows, global_time=800, acceptable_global_time=10800, script=script)
 
 
+class _Candidate(object):
+    def __init__(self, global_time):
+        self.global_time = global_time
+
+
+class _Clock(object):
+    def __init__(self):
+        self.now = 1000.0
+
+    def __call__(self):
+        return self.now
+
+
+def acceptable_global_time_vectors():
+    """Community.acceptable_global_time (community.py:1015-1058) lifted from the AST (the @property decorator dropped;
+    `time` bound to a test clock; py2 `/` -> `//` at :1041): the median of > 5 candidate opinions (py2 floor index), the own global time
+    otherwise, the + range, the 2^63-1 ceiling, the 5-second cache and the bloom-sync-disabled branch."""
+    tree = ast.parse(open(os.path.join(REF, "community.py")).read())
+    cls = [n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == "Community"][0]
+    node = [n for n in cls.body if isinstance(n, ast.FunctionDef) and n.name == "acceptable_global_time"][0]
+    node.decorator_list = []
+    # the one py2-ism: `options[len(options) / 2]` (:1041) is integer division in py2
+    divs = [n for n in ast.walk(node) if isinstance(n, ast.BinOp) and isinstance(n.op, ast.Div)]
+    assert len(divs) == 1
+    divs[0].op = ast.FloorDiv()
+    clock = _Clock()
+    g = dict(time=clock)
+    exec(compile(ast.fix_missing_locations(ast.Module([node], [])), "community.py", "exec"), g)
+    fn = g["acceptable_global_time"]
+
+    class Stub(object):
+        pass
+
+    rng = np.random.Generator(np.random.PCG64(404))
+    scripts = []
+    for trial in range(40):
+        stub = Stub()
+        pick = lambda vals: vals[int(rng.integers(0, len(vals)))]  # noqa: E731
+        stub._global_time = pick([0, 1, 50, 9000, 12000, 2 ** 63 - 5000, 2 ** 63 - 1])
+        stub.dispersy_acceptable_global_time_range = pick([10000, 1, 0, 123456])
+        stub.dispersy_enable_bloom_filter_sync = bool(trial % 9 != 4)
+        stub._acceptable_global_time_deadline = 0.0
+        stub._acceptable_global_time_cache = stub._global_time
+        clock.now = 1000.0
+        steps = []
+        for step in range(8):
+            n = int(rng.integers(0, 12))
+            gts = [int(x) for x in rng.integers(0, 20000, size=n)]
+            if step % 3 == 2:
+                gts = [0] * int(rng.integers(0, 4)) + gts  # global_time 0 opinions are ignored
+            cands = [_Candidate(x) for x in gts]
+            stub.dispersy_yield_verified_candidates = lambda c=cands: iter(c)
+            if step % 4 == 3:
+                stub._global_time += int(rng.integers(0, 5000))
+            clock.now += pick([0.0, 1.5, 4.99, 5.01, 20.0])
+            steps.append(dict(now=clock.now, own_global_time=stub._global_time, candidates=gts, result=fn(stub)))
+        scripts.append(dict(enable=stub.dispersy_enable_bloom_filter_sync,
+                            range=stub.dispersy_acceptable_global_time_range, steps=steps))
+    with open(os.path.join(HERE, "acceptable_vectors.json"), "w") as f:
+        json.dump(dict(generator="tests/golden/gen_sync_golden.py acceptable_global_time_vectors",
+                       source="/root/reference/community.py:1015-1058 lifted via ast", scripts=scripts), f,
+                  separators=(",", ":"))
+    return len(scripts)
+
+
 def main(B):
+    acceptable_global_time_vectors()
     schema = reference_schema()
     draws = DrawLog(0)
     funcs, g = lift_methods(B, draws)
