@@ -91,6 +91,8 @@ struct dsy_store {
     uint64_t live_cap = 0;    // entries of d_live_gt / d_live_row when they are the ingest's own buffers
     DupSlot* dup = nullptr;   // (member, global_time) -> row table (dsy_store_index_members), or none
     uint64_t dup_cap = 0, dup_count = 0;
+    DupKey* dup_keys = nullptr;  // every row's (member, global_time), for DELETEs to find the row's slot
+    uint64_t keys_cap = 0;
     uint64_t* spare_gt = nullptr;   // the ingest's second index buffer pair (the next merge's target)
     uint64_t* spare_row = nullptr;
     uint64_t spare_cap = 0;
@@ -756,12 +758,23 @@ int dup_insert(dsy_ctx* c, dsy_store* s, const uint64_t* member, const uint64_t*
     int rc;
     if (!n) return DSY_OK;
     if ((rc = dup_reserve(c, s, s->dup_count + n))) return rc;
+    if (first_row + n > s->keys_cap) {
+        const uint64_t cap = grown(first_row + n, s->keys_cap);
+        void* nk;
+        if (hipMalloc(&nk, cap * sizeof(DupKey)) != hipSuccess) return fail(DSY_ENOMEM, "row keys (%llu rows)", (unsigned long long)cap);
+        if (s->dup_keys && first_row) HIP_TRY(hipMemcpyAsync(nk, s->dup_keys, first_row * sizeof(DupKey), hipMemcpyDeviceToDevice, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        store_release(s, s->dup_keys);
+        s->owned.push_back(nk);
+        s->dup_keys = (DupKey*)nk;
+        s->keys_cap = cap;
+    }
     void* d;
     if ((rc = ws_get(c, "dup_keys", n * 16, &d))) return rc;
     HIP_TRY(hipMemcpyAsync(d, member, n * 8, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync((uint64_t*)d + n, gt, n * 8, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(launch_dup_insert((const uint64_t*)d, (const uint64_t*)d + n, first_row, n, s->dup, s->dup_cap - 1,
-                              c->stream));
+                              s->dup_keys, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     s->dup_count += n;
     return DSY_OK;
@@ -933,6 +946,8 @@ int dsy_store_prune(dsy_ctx* c, dsy_store* s, uint32_t meta, uint64_t max_gt, ui
     HIP_TRY(hipMemcpyAsync(&k, d_k, 8, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (!k) return DSY_OK;
+    // the deleted rows leave the (member, global_time) table too: a later lookup finds nothing (dispersy.py:868)
+    if (s->dup) HIP_TRY(launch_dup_erase(nullptr, s->d_live_row, a, k, s->dup_keys, s->dup, s->dup_cap - 1, c->stream));
     const uint64_t live = s->n_live - k;
     if (s->spare_cap < live) {  // the ingest's second buffer pair is the target, as for a merge
         store_release(s, s->spare_gt);
@@ -976,12 +991,89 @@ int dsy_store_prune(dsy_ctx* c, dsy_store* s, uint32_t meta, uint64_t max_gt, ui
     return DSY_OK;
 }
 
+int dsy_store_delete(dsy_ctx* c, dsy_store* s, const uint64_t* rows, uint64_t k, uint64_t* out_deleted) {
+    if (!c || !s || !out_deleted || (k && !rows)) return fail(DSY_EINVAL, "NULL argument");
+    if (s->ctx != c) return fail(DSY_EINVAL, "store belongs to another context");
+    for (uint64_t i = 0; i < k; ++i)
+        if (rows[i] >= s->n) return fail(DSY_EINVAL, "row %llu out of range (%llu rows)", (unsigned long long)rows[i], (unsigned long long)s->n);
+    *out_deleted = 0;
+    if (!k) return DSY_OK;
+    Guard g(c);
+    // segment bounds (old positions) to remap: every meta's [a, b)
+    std::vector<uint32_t> seg_ids;
+    std::vector<uint64_t> bounds;
+    for (auto& e : s->segs) {
+        seg_ids.push_back(e.first);
+        bounds.push_back(e.second.first);
+        bounds.push_back(e.second.second);
+    }
+    bounds.push_back(s->n_live);
+    const uint64_t words = (s->n + 31) / 32, tiles = (s->n_live + kDelTile - 1) / kDelTile;
+    const size_t b_bits = (words * 4 + 15) / 16 * 16, b_rows = k * 8, b_tiles = (tiles + 1) * 8,
+                 b_bounds = bounds.size() * 8;
+    void* d;
+    int rc;
+    if ((rc = ws_get(c, "delete", b_bits + b_rows + b_tiles + b_bounds, &d))) return rc;
+    uint8_t* p = (uint8_t*)d;
+    uint32_t* d_bits = (uint32_t*)p;
+    uint64_t *d_rows = (uint64_t*)(p + b_bits), *d_tiles = (uint64_t*)(p + b_bits + b_rows),
+             *d_bounds = (uint64_t*)(p + b_bits + b_rows + b_tiles);
+    HIP_TRY(hipMemsetAsync(d_bits, 0, words * 4, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_rows, rows, b_rows, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_bounds, bounds.data(), b_bounds, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(launch_mark_rows(d_rows, k, s->n, d_bits, c->stream));
+    // the deleted rows' (member, global_time) slots become tombstones (also rows outside the live index: undone ones)
+    if (s->dup) HIP_TRY(launch_dup_erase(d_rows, nullptr, 0, k, s->dup_keys, s->dup, s->dup_cap - 1, c->stream));
+    const uint64_t cap_need = std::max<uint64_t>(s->n_live, 1);
+    if (s->spare_cap < cap_need) {  // the ingest's second buffer pair is the target, as for a merge
+        store_release(s, s->spare_gt);
+        store_release(s, s->spare_row);
+        s->spare_gt = s->spare_row = nullptr;
+        s->spare_cap = 0;
+        const uint64_t cap = grown(cap_need, s->n_live);
+        void *pg, *pr;
+        if (hipMalloc(&pg, cap * 8) != hipSuccess) return fail(DSY_ENOMEM, "store live index");
+        s->owned.push_back(pg);
+        if (hipMalloc(&pr, cap * 8) != hipSuccess) { store_release(s, pg); return fail(DSY_ENOMEM, "store live index"); }
+        s->owned.push_back(pr);
+        s->spare_gt = (uint64_t*)pg;
+        s->spare_row = (uint64_t*)pr;
+        s->spare_cap = cap;
+    }
+    HIP_TRY(launch_live_delete(s->d_live_gt, s->d_live_row, s->n_live, d_bits, d_tiles, s->spare_gt, s->spare_row,
+                               d_bounds, (uint32_t)bounds.size(), c->stream));
+    HIP_TRY(hipMemcpyAsync(bounds.data(), d_bounds, b_bounds, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const uint64_t live = bounds.back();
+    *out_deleted = s->n_live - live;
+    if (live == s->n_live) return DSY_OK;  // none of the rows was in the live index: the old index stays
+    uint64_t* prev_gt = const_cast<uint64_t*>(s->d_live_gt);
+    uint64_t* prev_row = const_cast<uint64_t*>(s->d_live_row);
+    const uint64_t prev_cap = s->live_cap;
+    s->d_live_gt = s->spare_gt;
+    s->d_live_row = s->spare_row;
+    s->live_cap = s->spare_cap;
+    if (prev_cap) {
+        s->spare_gt = prev_gt;
+        s->spare_row = prev_row;
+        s->spare_cap = prev_cap;
+    } else {
+        store_release(s, prev_gt);
+        store_release(s, prev_row);
+        s->spare_gt = s->spare_row = nullptr;
+        s->spare_cap = 0;
+    }
+    for (size_t j = 0; j < seg_ids.size(); ++j) s->segs[seg_ids[j]] = {bounds[2 * j], bounds[2 * j + 1]};
+    s->n_live = live;
+    return DSY_OK;
+}
+
 int dsy_store_index_members(dsy_ctx* c, dsy_store* s, const uint64_t* member, const uint64_t* gt, uint64_t n) {
     if (!c || !s || (n && (!member || !gt))) return fail(DSY_EINVAL, "NULL argument");
     if (s->ctx != c) return fail(DSY_EINVAL, "store belongs to another context");
     if (n != s->n) return fail(DSY_EINVAL, "%llu members for a store of %llu rows", (unsigned long long)n, (unsigned long long)s->n);
     Guard g(c);
-    if (s->dup) {  // rebuild from scratch
+    if (s->dup) {  // rebuild from scratch (the row keys are rewritten by the insert)
         store_release(s, s->dup);
         s->dup = nullptr;
         s->dup_cap = s->dup_count = 0;
@@ -1103,8 +1195,12 @@ int dsy_claim_modulo(dsy_ctx* c, const dsy_bloom_params* p, const dsy_store* s, 
     *out_count = 0;
     std::vector<std::pair<uint64_t, uint64_t>> spans;
     uint64_t total = 0;
-    for (uint32_t j = 0; j < nmeta; ++j) {
-        auto it = s->segs.find(meta_ids[j]);
+    // `meta_message IN (...)` counts each row once, however often an id is listed
+    std::vector<uint32_t> ids(meta_ids, meta_ids + nmeta);
+    std::sort(ids.begin(), ids.end());
+    ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+    for (uint32_t id : ids) {
+        auto it = s->segs.find(id);
         if (it == s->segs.end() || it->second.first >= it->second.second) continue;
         spans.push_back(it->second);
         total += it->second.second - it->second.first;
@@ -1120,7 +1216,7 @@ int dsy_claim_modulo(dsy_ctx* c, const dsy_bloom_params* p, const dsy_store* s, 
     HIP_TRY(hipMemsetAsync(dn, 0, 8, c->stream));
     for (auto& sp : spans)
         HIP_TRY(launch_claim_modulo(s->d_live_gt, s->d_live_row, sp.first, sp.second, offset, modulo, (uint64_t*)dr,
-                                    (unsigned long long*)dn, c->max_grid, c->stream));
+                                    total, (unsigned long long*)dn, c->max_grid, c->stream));
     uint64_t n = 0;
     HIP_TRY(hipMemcpyAsync(&n, dn, 8, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));

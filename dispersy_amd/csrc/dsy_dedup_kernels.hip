@@ -6,7 +6,8 @@
 // step (ballot of the first differing byte):
 //   k_dup_insert   one lane per row: claim the first free slot from the key's hash (keys are unique: the table
 //                  mirrors UNIQUE(community, member, global_time), dispersydatabase.py:53-64)
-//   k_dup_rehash   growth: every occupied slot of the old table into the new one
+//   k_dup_rehash   growth: every occupied slot of the old table into the new one (tombstones dropped)
+//   k_dup_erase    DELETE: the deleted rows' slots become tombstones
 //   k_dup_check    verdict per message (DSY_DUP_*), with the stored row
 //   k_rec_scatter  dsy_store_replace: point rows at their replacement packets in the line copy
 #include "dsy_kernels.h"
@@ -21,6 +22,7 @@ __device__ __forceinline__ uint64_t dup_hash(uint64_t member, uint64_t gt) {
     return x;
 }
 
+// (tombstoned slots are never reused: a rehash on growth drops them)
 __device__ __forceinline__ void dup_put(DupSlot* __restrict__ tab, uint64_t mask, uint64_t member, uint64_t gt,
                                         uint64_t row) {
     uint64_t h = dup_hash(member, gt) & mask;
@@ -37,15 +39,41 @@ __device__ __forceinline__ void dup_put(DupSlot* __restrict__ tab, uint64_t mask
 
 __global__ void __launch_bounds__(256) k_dup_insert(const uint64_t* __restrict__ member, const uint64_t* __restrict__ gt,
                                                     uint64_t first_row, uint64_t n, DupSlot* __restrict__ tab,
-                                                    uint64_t mask) {
+                                                    uint64_t mask, DupKey* __restrict__ keys) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < n) dup_put(tab, mask, member[i], gt[i], first_row + i);
+    if (i >= n) return;
+    const uint64_t m = member[i], g = gt[i];
+    keys[first_row + i] = DupKey{m, g};
+    dup_put(tab, mask, m, g, first_row + i);
+}
+
+// DELETE FROM sync (GlobalTimePruning, sequence-number conflicts, LastSync history): the deleted rows' slots become
+// tombstones, so a later (member, global_time) lookup no longer finds them (dispersy.py:868 sees no row after the
+// DELETE).  One lane per deleted row walks its key's probe chain to the slot holding that row.
+__global__ void __launch_bounds__(256) k_dup_erase(const uint64_t* __restrict__ rows, const uint64_t* __restrict__ live_row,
+                                                   uint64_t a, uint64_t k, const DupKey* __restrict__ keys,
+                                                   DupSlot* __restrict__ tab, uint64_t mask) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= k) return;
+    const uint64_t row = rows ? rows[i] : (live_row ? live_row[a + i] : a + i);
+    const DupKey key = keys[row];
+    uint64_t h = dup_hash(key.member, key.gt) & mask;
+    for (uint64_t step = 0; step <= mask; ++step) {
+        const uint64_t r = tab[h].row;
+        if (r == kDupEmpty) return;  // not in the table (deleted before)
+        if (r == row) {
+            tab[h].row = kDupTomb;
+            return;
+        }
+        h = (h + 1) & mask;
+    }
 }
 
 __global__ void __launch_bounds__(256) k_dup_rehash(const DupSlot* __restrict__ old, uint64_t old_cap,
                                                     DupSlot* __restrict__ tab, uint64_t mask) {
     const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < old_cap && old[i].row != kDupEmpty) dup_put(tab, mask, old[i].member, old[i].gt, old[i].row);
+    if (i < old_cap && old[i].row != kDupEmpty && old[i].row != kDupTomb)
+        dup_put(tab, mask, old[i].member, old[i].gt, old[i].row);
 }
 
 // One wave per received message.
@@ -65,7 +93,7 @@ __global__ void __launch_bounds__(256) k_dup_check(const DupSlot* __restrict__ t
     for (uint64_t base = 0; base <= mask; base += 64) {
         const DupSlot sl = tab[(h0 + base + lane) & mask];
         const bool empty = sl.row == kDupEmpty;
-        const uint64_t hit = __ballot(!empty && sl.member == mj && sl.gt == gj);
+        const uint64_t hit = __ballot(!empty && sl.row != kDupTomb && sl.member == mj && sl.gt == gj);
         const uint64_t gap = __ballot(empty);
         if (hit && (!gap || __ffsll((unsigned long long)hit) < __ffsll((unsigned long long)gap))) {
             row = __shfl(sl.row, __ffsll((unsigned long long)hit) - 1, 64);
@@ -124,9 +152,16 @@ __global__ void __launch_bounds__(256) k_rec_scatter(RowRec* __restrict__ rec, c
 static uint32_t grid_of(uint64_t lanes) { return (uint32_t)((lanes + 255) / 256); }
 
 hipError_t launch_dup_insert(const uint64_t* member, const uint64_t* gt, uint64_t first_row, uint64_t n, DupSlot* tab,
-                             uint64_t mask, hipStream_t stream) {
+                             uint64_t mask, DupKey* keys, hipStream_t stream) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_dup_insert, dim3(grid_of(n)), dim3(256), 0, stream, member, gt, first_row, n, tab, mask);
+    hipLaunchKernelGGL(k_dup_insert, dim3(grid_of(n)), dim3(256), 0, stream, member, gt, first_row, n, tab, mask, keys);
+    return hipGetLastError();
+}
+
+hipError_t launch_dup_erase(const uint64_t* rows, const uint64_t* live_row, uint64_t a, uint64_t k, const DupKey* keys,
+                            DupSlot* tab, uint64_t mask, hipStream_t stream) {
+    if (!k) return hipSuccess;
+    hipLaunchKernelGGL(k_dup_erase, dim3(grid_of(k)), dim3(256), 0, stream, rows, live_row, a, k, keys, tab, mask);
     return hipGetLastError();
 }
 

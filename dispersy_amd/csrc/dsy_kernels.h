@@ -188,8 +188,17 @@ hipError_t launch_store_lines(const uint8_t* blob, const uint64_t* offsets, cons
 struct DupSlot {
     uint64_t member, gt, row, pad;
 };
+// A row's (member, global_time) key, kept per store row next to the table so a DELETE can find the row's slot.
+struct DupKey {
+    uint64_t member, gt;
+};
+// row == kDupTomb: a deleted row's slot -- not a match, not empty (probing continues past it); rehash drops it
+static constexpr uint64_t kDupTomb = ~1ull;
 hipError_t launch_dup_insert(const uint64_t* member, const uint64_t* gt, uint64_t first_row, uint64_t n, DupSlot* tab,
-                             uint64_t mask, hipStream_t stream);
+                             uint64_t mask, DupKey* keys, hipStream_t stream);
+// tombstone the slots of rows[k] (or, rows == nullptr, of live_row[a .. a + k) / identity), keys from `keys`
+hipError_t launch_dup_erase(const uint64_t* rows, const uint64_t* live_row, uint64_t a, uint64_t k, const DupKey* keys,
+                            DupSlot* tab, uint64_t mask, hipStream_t stream);
 hipError_t launch_dup_rehash(const DupSlot* old, uint64_t old_cap, DupSlot* tab, uint64_t mask, hipStream_t stream);
 hipError_t launch_dup_check(const DupSlot* tab, uint64_t mask, const uint8_t* lines, const RowRec* rec,
                             const uint64_t* member, const uint64_t* gt, const uint8_t* blob, const uint64_t* offsets,
@@ -212,9 +221,18 @@ hipError_t launch_prune_count(const uint64_t* live_gt, uint64_t a, uint64_t b, u
 hipError_t launch_live_cut(const uint64_t* live_gt, const uint64_t* live_row, uint64_t n_out, uint64_t a, uint64_t k,
                            uint64_t* out_gt, uint64_t* out_row, uint32_t max_grid, hipStream_t stream);
 // claim side, modulo strategy: rows of live segment [a, b) with (gt + offset) % modulo == 0 -> out_rows[*count++]
+// (at most cap rows are written; *count still counts every hit)
 hipError_t launch_claim_modulo(const uint64_t* live_gt, const uint64_t* live_row, uint64_t a, uint64_t b,
-                               uint64_t offset, uint64_t modulo, uint64_t* out_rows, unsigned long long* count,
-                               uint32_t max_grid, hipStream_t stream);
+                               uint64_t offset, uint64_t modulo, uint64_t* out_rows, uint64_t cap,
+                               unsigned long long* count, uint32_t max_grid, hipStream_t stream);
+// DELETE of arbitrary rows (dsy_store_delete): del_bits marks store rows; the live index loses every entry whose row is
+// marked, stable.  Tiles of kDelTile entries: per-tile kept counts -> exclusive scan -> scatter; bounds[nb] (positions in
+// the old index, ascending or not) are mapped to their positions in the new one.  d_tmp: (tiles + 1) u64 + 64 B.
+static constexpr uint64_t kDelTile = 1024;
+hipError_t launch_mark_rows(const uint64_t* rows, uint64_t k, uint64_t n_rows, uint32_t* del_bits, hipStream_t stream);
+hipError_t launch_live_delete(const uint64_t* live_gt, const uint64_t* live_row, uint64_t n_live,
+                              const uint32_t* del_bits, uint64_t* tile_tmp, uint64_t* out_gt, uint64_t* out_row,
+                              uint64_t* bounds, uint32_t nb, hipStream_t stream);
 hipError_t launch_ingest_merge(const uint64_t* live_gt, const uint64_t* live_row, uint64_t n_live,
                                const IngestRow* rows, uint64_t a, uint64_t* rank, uint64_t* out_gt, uint64_t* out_row,
                                uint32_t max_grid, hipStream_t stream);

@@ -145,7 +145,7 @@ __global__ void __launch_bounds__(kIngestThreads) k_claim_modulo(const uint64_t*
                                                                   const uint64_t* __restrict__ live_row, uint64_t a,
                                                                   uint64_t b, uint64_t offset, uint64_t modulo,
                                                                   uint64_t recip, uint64_t* __restrict__ out_rows,
-                                                                  unsigned long long* __restrict__ count) {
+                                                                  uint64_t cap, unsigned long long* __restrict__ count) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t stride = (uint64_t)gridDim.x * kIngestTile;
     // each wave covers kIngestPerThread x 64 consecutive rows per step, all loads issued before the first ballot
@@ -169,20 +169,146 @@ __global__ void __launch_bounds__(kIngestThreads) k_claim_modulo(const uint64_t*
             unsigned long long at = 0;
             if (lane == 0) at = atomicAdd(count, (unsigned long long)__popcll(mask));
             at = __shfl(at, 0);
-            if (hit) out_rows[at + __popcll(mask & ((1ull << lane) - 1))] = live_row ? live_row[i] : i;
+            const uint64_t slot = at + __popcll(mask & ((1ull << lane) - 1));
+            if (hit && slot < cap) out_rows[slot] = live_row ? live_row[i] : i;
         }
     }
 }
 
 hipError_t launch_claim_modulo(const uint64_t* live_gt, const uint64_t* live_row, uint64_t a, uint64_t b,
-                               uint64_t offset, uint64_t modulo, uint64_t* out_rows, unsigned long long* count,
-                               uint32_t max_grid, hipStream_t stream) {
+                               uint64_t offset, uint64_t modulo, uint64_t* out_rows, uint64_t cap,
+                               unsigned long long* count, uint32_t max_grid, hipStream_t stream) {
     if (b <= a) return hipSuccess;
     uint64_t g = (b - a + kIngestTile - 1) / kIngestTile;
     if (g > (uint64_t)max_grid * 4) g = (uint64_t)max_grid * 4;
     const uint64_t recip = ~0ull / modulo;  // floor((2^64 - 1) / modulo): one correction step suffices
     hipLaunchKernelGGL(k_claim_modulo, dim3((uint32_t)g), dim3(kIngestThreads), 0, stream, live_gt, live_row, a, b,
-                       offset, modulo, recip, out_rows, count);
+                       offset, modulo, recip, out_rows, cap, count);
+    return hipGetLastError();
+}
+
+// DELETE FROM sync WHERE id = ? for arbitrary rows (dsy_store_delete: the sequence-number conflict DELETE of
+// dispersy.py:1006, LastSyncDistribution's history pruning :1560-1591): a stable compaction of the live index without
+// the entries whose row is marked in del_bits.  16 B read + 16 B written per indexed row, two passes over a bit per
+// entry (the bitmap is n/8 bytes: L2-resident for small deletes).
+__global__ void __launch_bounds__(256) k_mark_rows(const uint64_t* __restrict__ rows, uint64_t k, uint64_t n_rows,
+                                                   uint32_t* __restrict__ bits) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < k && rows[i] < n_rows) atomicOr(&bits[rows[i] >> 5], 1u << (rows[i] & 31));
+}
+
+__device__ __forceinline__ bool entry_kept(const uint64_t* __restrict__ live_row, const uint32_t* __restrict__ bits,
+                                           uint64_t i) {
+    const uint64_t r = live_row ? live_row[i] : i;
+    return !((bits[r >> 5] >> (r & 31)) & 1u);
+}
+
+// kept entries per tile of kDelTile (256 lanes x 4)
+__global__ void __launch_bounds__(256) k_del_count(const uint64_t* __restrict__ live_row, uint64_t n_live,
+                                                   const uint32_t* __restrict__ bits, uint64_t* __restrict__ tile_cnt) {
+    __shared__ uint32_t part[4];
+    const uint64_t t0 = (uint64_t)blockIdx.x * kDelTile;
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+        const uint64_t i = t0 + u * 256 + threadIdx.x;
+        c += (i < n_live && entry_kept(live_row, bits, i)) ? 1u : 0u;
+    }
+    for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+// exclusive scan of the tile counts, one workgroup (tile_cnt[tiles] receives the total)
+__global__ void __launch_bounds__(1024) k_del_scan(uint64_t* __restrict__ tile_cnt, uint64_t tiles) {
+    __shared__ uint64_t sums[1024];
+    const uint64_t per = (tiles + 1023) / 1024;
+    const uint64_t b0 = threadIdx.x * per, b1 = b0 + per < tiles ? b0 + per : tiles;
+    uint64_t s = 0;
+    for (uint64_t t = b0; t < b1; ++t) s += tile_cnt[t];
+    sums[threadIdx.x] = s;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+        const uint64_t v = threadIdx.x >= d ? sums[threadIdx.x - d] : 0;
+        __syncthreads();
+        sums[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint64_t run = sums[threadIdx.x] - s;
+    for (uint64_t t = b0; t < b1; ++t) {
+        const uint64_t c = tile_cnt[t];
+        tile_cnt[t] = run;
+        run += c;
+    }
+    if (threadIdx.x == 1023) tile_cnt[tiles] = sums[1023];
+}
+
+// each tile writes its kept entries at its scanned offset, in order (wave ballots + a 4-wave LDS prefix per pass)
+__global__ void __launch_bounds__(256) k_del_scatter(const uint64_t* __restrict__ live_gt,
+                                                     const uint64_t* __restrict__ live_row, uint64_t n_live,
+                                                     const uint32_t* __restrict__ bits,
+                                                     const uint64_t* __restrict__ tile_off, uint64_t* __restrict__ out_gt,
+                                                     uint64_t* __restrict__ out_row) {
+    __shared__ uint32_t wsum[4];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t t0 = (uint64_t)blockIdx.x * kDelTile;
+    uint64_t at = tile_off[blockIdx.x];
+    for (uint32_t u = 0; u < 4; ++u) {
+        const uint64_t i = t0 + u * 256 + threadIdx.x;
+        const bool keep = i < n_live && entry_kept(live_row, bits, i);
+        const uint64_t m = __ballot(keep);
+        if (lane == 0) wsum[wave] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t before = 0, total = 0;
+        for (uint32_t w = 0; w < 4; ++w) {
+            before += w < wave ? wsum[w] : 0;
+            total += wsum[w];
+        }
+        if (keep) {
+            const uint64_t o = at + before + __popcll(m & ((1ull << lane) - 1));
+            out_gt[o] = live_gt[i];
+            out_row[o] = live_row ? live_row[i] : i;
+        }
+        at += total;
+        __syncthreads();
+    }
+}
+
+// old index position -> new one (kept entries before it): the tile's offset plus a count inside the tile
+__global__ void k_del_bounds(const uint64_t* __restrict__ live_row, uint64_t n_live, const uint32_t* __restrict__ bits,
+                             const uint64_t* __restrict__ tile_off, uint64_t* __restrict__ bounds, uint32_t nb) {
+    const uint32_t j = blockIdx.x * 64 + threadIdx.x;
+    if (j >= nb) return;
+    const uint64_t x = bounds[j];
+    const uint64_t t = x / kDelTile;
+    uint64_t pos = tile_off[t];
+    for (uint64_t i = t * kDelTile; i < x && i < n_live; ++i) pos += entry_kept(live_row, bits, i) ? 1 : 0;
+    bounds[j] = pos;
+}
+
+hipError_t launch_mark_rows(const uint64_t* rows, uint64_t k, uint64_t n_rows, uint32_t* del_bits, hipStream_t stream) {
+    if (!k) return hipSuccess;
+    hipLaunchKernelGGL(k_mark_rows, dim3((uint32_t)((k + 255) / 256)), dim3(256), 0, stream, rows, k, n_rows, del_bits);
+    return hipGetLastError();
+}
+
+hipError_t launch_live_delete(const uint64_t* live_gt, const uint64_t* live_row, uint64_t n_live,
+                              const uint32_t* del_bits, uint64_t* tile_tmp, uint64_t* out_gt, uint64_t* out_row,
+                              uint64_t* bounds, uint32_t nb, hipStream_t stream) {
+    const uint64_t tiles = (n_live + kDelTile - 1) / kDelTile;
+    if (tiles) {
+        hipLaunchKernelGGL(k_del_count, dim3((uint32_t)tiles), dim3(256), 0, stream, live_row, n_live, del_bits, tile_tmp);
+    }
+    hipLaunchKernelGGL(k_del_scan, dim3(1), dim3(1024), 0, stream, tile_tmp, tiles);
+    if (tiles) {
+        hipLaunchKernelGGL(k_del_scatter, dim3((uint32_t)tiles), dim3(256), 0, stream, live_gt, live_row, n_live,
+                           del_bits, tile_tmp, out_gt, out_row);
+    }
+    if (nb) {
+        hipLaunchKernelGGL(k_del_bounds, dim3((nb + 63) / 64), dim3(64), 0, stream, live_row, n_live, del_bits, tile_tmp,
+                           bounds, nb);
+    }
     return hipGetLastError();
 }
 

@@ -6,18 +6,21 @@ Rows are kept in the order of the reference's `sync_meta_message_undone_global_t
     blob        u8[sum L]   packets back to back        offsets   u64[N+1]
     global_time u64[N]      meta u32[N]                 undone    i64[N]     rowid  i64[N]
     member      u64[N]      (optional: the (member, global_time) duplicate check, dispersy.py:831-918)
+    deleted     bool[N]     rows a DELETE removed (pruning, sequence conflicts, LastSync history)
 
 `undone` is the reference's column: 0, or the id of the undo message whose packet is the proof.
 
-The device copy (dsy_store_upload) holds the packets as a line copy plus a live-row index (undone != 0 excluded)
-with per-meta segments; the host copy of the small columns serves the claim-side range selection
+The device copy (dsy_store_upload) holds the packets as a line copy plus a live-row index (undone != 0 and deleted rows
+excluded) with per-meta segments; the host copy of the small columns serves the claim-side range selection
 (community.py:881-933) and maps responder output rows back to packets.
 
 `append` is the requester-side ingest (`INSERT INTO sync` of Dispersy._store, dispersy.py:1475-1612): received
 packets take the next row positions, in insertion (rowid) order, and join the index by (meta_message,
-global_time, rowid) -- on the device by dsy_store_append's merge, on the host per meta.  Rows past the constructor's
-are therefore no longer in index order; `live_rows` always is.  `dup_check` / `replace_packet` are the duplicate
-check of received packets and its UPDATE (dispersy.py:831-918).
+global_time, rowid) -- on the device by dsy_store_append's merge.  The host side is O(batch): columns grow
+geometrically and the per-meta live arrays take the new rows as a pending delta, merged only when a host-side reader
+asks for that meta's rows (live_rows).  Rows past the constructor's are therefore no longer in index order;
+`live_rows` always is.  `dup_check` / `replace_packet` are the duplicate check of received packets and its UPDATE
+(dispersy.py:831-918); `prune` and `delete_rows` are the DELETEs.
 """
 import ctypes
 
@@ -25,46 +28,77 @@ import numpy as np
 
 from . import _native
 
+_COLUMNS = ("global_time", "meta", "undone", "rowid", "member", "deleted")
+
+
+def _room(buf, used, need):
+    """buf with capacity >= need (geometric growth, the first `used` entries kept)."""
+    if need <= len(buf):
+        return buf
+    out = np.empty(max(need, 2 * len(buf), 1024), dtype=buf.dtype)
+    out[:used] = buf[:used]
+    return out
+
 
 class SyncStore(object):
-    def __init__(self, blob, offsets, global_time, meta, undone=None, rowid=None, ctx=None, member=None):
-        self.offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
-        self.n = len(self.offsets) - 1
+    def __init__(self, blob, offsets, global_time, meta, undone=None, rowid=None, ctx=None, member=None,
+                 communities=None):
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = self.n = len(offsets) - 1
+        self._buf = dict(
+            offsets=offsets.copy(),
+            global_time=np.ascontiguousarray(global_time, dtype=np.uint64).copy(),
+            meta=np.ascontiguousarray(meta, dtype=np.uint32).copy(),
+            undone=(np.zeros(n, dtype=np.int64) if undone is None else np.ascontiguousarray(undone, dtype=np.int64).copy()),
+            rowid=(np.arange(1, n + 1, dtype=np.int64) if rowid is None
+                   else np.ascontiguousarray(rowid, dtype=np.int64).copy()),
+            member=None if member is None else np.ascontiguousarray(member, dtype=np.uint64).copy(),
+            deleted=np.zeros(n, dtype=bool))
         self.blob = blob if isinstance(blob, (bytes, bytearray, memoryview, np.ndarray)) else bytes(blob)
-        self.global_time = np.ascontiguousarray(global_time, dtype=np.uint64)
-        self.meta = np.ascontiguousarray(meta, dtype=np.uint32)
-        self.undone = (np.zeros(self.n, dtype=np.int64) if undone is None
-                       else np.ascontiguousarray(undone, dtype=np.int64))
-        self.rowid = (np.arange(1, self.n + 1, dtype=np.int64) if rowid is None
-                      else np.ascontiguousarray(rowid, dtype=np.int64))
-        self.member = None if member is None else np.ascontiguousarray(member, dtype=np.uint64)
-        assert len(self.global_time) == len(self.meta) == len(self.undone) == len(self.rowid) == self.n
-        assert self.member is None or len(self.member) == self.n
-        if self.n > 1:
+        assert all(len(self._buf[c]) == n for c in _COLUMNS if self._buf[c] is not None)
+        # communities the rows belong to (sync.community): the duplicate table is keyed (member, global_time), which
+        # is the reference's UNIQUE(community, member, global_time) only within one community
+        self.communities = None if communities is None else frozenset(communities)
+        if n > 1:
             m, g = self.meta, self.global_time
             bad = (m[1:] < m[:-1]) | ((m[1:] == m[:-1]) & (g[1:] < g[:-1]))
             if bad.any():
                 raise ValueError("SyncStore rows must be sorted by (meta_message, global_time, rowid)")
         self._ctx = ctx
         self._handle = None
-        self._n_sorted = self.n  # rows in index order, uploaded by dsy_store_upload; later rows are appends
+        self._n_sorted = n  # rows in index order, uploaded by dsy_store_upload; later rows are appends
         self._row_of_id = None
         self._replaced = {}  # row -> packet after an UPDATE (dsy_store_replace); the packed blob keeps the original
         self._dup_indexed = False
-        self._prunes = []  # (meta, max_global_time) DELETEs, replayed on the device after a lazy upload
-        # live (undone == 0) rows per meta, in global_time order: the claim side's index range scans
+        self._ops = []  # ("prune", meta, max_gt, n_at) / ("delete", rows, n_at): replayed on the device after a lazy upload
+        # live (undone == 0, not deleted) rows per meta, in (global_time, row) order, plus appended rows not merged yet
         live = np.flatnonzero(self.undone == 0)
-        self._live = {}
+        self._live, self._pending = {}, {}
+        self._nlive = {}
         if len(live):
             lm = self.meta[live]
             cuts = np.flatnonzero(lm[1:] != lm[:-1]) + 1
             for seg in np.split(live, cuts):
                 self._live[int(self.meta[seg[0]])] = seg
+                self._nlive[int(self.meta[seg[0]])] = len(seg)
         self._empty = np.zeros(0, dtype=np.int64)
+
+    # ------------------------------------------------------------------------------------------ columns
+    def _col(self, name):
+        b = self._buf[name]
+        return None if b is None else b[:self.n]
+
+    offsets = property(lambda self: self._buf["offsets"][:self.n + 1])
+    global_time = property(lambda self: self._col("global_time"))
+    meta = property(lambda self: self._col("meta"))
+    undone = property(lambda self: self._col("undone"))
+    rowid = property(lambda self: self._col("rowid"))
+    member = property(lambda self: self._col("member"))
+    deleted = property(lambda self: self._col("deleted"))
 
     # ------------------------------------------------------------------------------------ constructors
     @classmethod
-    def from_rows(cls, rows, ctx=None):
+    def from_rows(cls, rows, ctx=None, communities=None):
         """rows: iterable of (rowid, global_time, meta_message, undone, packet[, member])."""
         rows = sorted(rows, key=lambda r: (r[2], r[1], r[0]))
         n = len(rows)
@@ -73,18 +107,20 @@ class SyncStore(object):
             np.cumsum([len(r[4]) for r in rows], out=offsets[1:])
         member = [r[5] for r in rows] if rows and len(rows[0]) > 5 else None
         return cls(b"".join(bytes(r[4]) for r in rows), offsets, [r[1] for r in rows], [r[2] for r in rows],
-                   [r[3] for r in rows], [r[0] for r in rows], ctx=ctx, member=member)
+                   [r[3] for r in rows], [r[0] for r in rows], ctx=ctx, member=member, communities=communities)
 
     @classmethod
     def from_sqlite(cls, conn, community=None, ctx=None):
         """Export a Dispersy database's `sync` table (optionally one community) in index order."""
-        sql = "SELECT id, global_time, meta_message, undone, packet, member FROM sync"
+        sql = "SELECT id, global_time, meta_message, undone, packet, member, community FROM sync"
         args = ()
         if community is not None:
             sql += " WHERE community = ?"
             args = (community,)
         sql += " ORDER BY meta_message, global_time, id"
-        return cls.from_rows([(i, g, m, u, bytes(p), mb) for i, g, m, u, p, mb in conn.execute(sql, args)], ctx=ctx)
+        rows = list(conn.execute(sql, args))
+        return cls.from_rows([(i, g, m, u, bytes(p), mb) for i, g, m, u, p, mb, _ in rows], ctx=ctx,
+                             communities={c for *_, c in rows} if rows else ({community} if community is not None else None))
 
     # --------------------------------------------------------------------------------------- accessors
     def packet(self, i):
@@ -92,7 +128,8 @@ class SyncStore(object):
             p = self._replaced.get(int(i))
             if p is not None:
                 return p
-        a, b = int(self.offsets[i]), int(self.offsets[i + 1])
+        off = self._buf["offsets"]
+        a, b = int(off[i]), int(off[i + 1])
         return bytes(self.blob[a:b])
 
     def packets(self, rows):
@@ -101,19 +138,37 @@ class SyncStore(object):
     def length(self, i):
         if self._replaced and int(i) in self._replaced:
             return len(self._replaced[int(i)])
-        return int(self.offsets[i + 1] - self.offsets[i])
+        off = self._buf["offsets"]
+        return int(off[i + 1] - off[i])
 
     def row_of_id(self, rowid):
+        """The row holding `rowid` (KeyError when there is none, or it was deleted: SELECT ... WHERE id = ? is empty)."""
         if self._row_of_id is None:
-            self._row_of_id = {int(r): i for i, r in enumerate(self.rowid)}
+            keep = np.flatnonzero(~self.deleted)
+            self._row_of_id = dict(zip(self.rowid[keep].tolist(), keep.tolist()))
         return self._row_of_id[int(rowid)]
 
     def live_rows(self, meta_id):
-        """Store rows of one meta with undone == 0, in (global_time, rowid) order."""
-        return self._live.get(int(meta_id), self._empty)
+        """Store rows of one meta with undone == 0 (not deleted), in (global_time, rowid) order."""
+        m = int(meta_id)
+        pend = self._pending.pop(m, None)
+        if pend:
+            new = np.concatenate(pend)
+            new = new[np.argsort(self.global_time[new], kind="stable")]  # ties: insertion (rowid) order
+            seg = self._live.get(m, self._empty)
+            # old rows first on equal global times (smaller rowid): insert after every old row with gt <= new gt
+            at = np.searchsorted(self.global_time[seg], self.global_time[new], side="right")
+            self._live[m] = np.insert(seg, at, new)
+        return self._live.get(m, self._empty)
+
+    def live_count(self, meta_id):
+        return self._nlive.get(int(meta_id), 0)
 
     def count_live(self, meta_ids):
-        return int(sum(len(self.live_rows(m)) for m in meta_ids))
+        return int(sum(self.live_count(m) for m in set(int(x) for x in meta_ids)))
+
+    def meta_ids(self):
+        return sorted(set(self._nlive) | set(self._live))
 
     # ------------------------------------------------------------------------------------------ ingest
     def append(self, packets, global_time, meta, rowid=None, member=None):
@@ -121,13 +176,13 @@ class SyncStore(object):
 
         packets: list of bytes; global_time / meta (/ member): one per packet; rowid: increasing ids above every
         stored one (default: the next ids, as SQLite assigns them).  Returns the new rows' positions.  When the store
-        is on the device already, the batch goes there in one dsy_store_append call."""
+        is on the device already, the batch goes there in one dsy_store_append call.  Host work is O(batch)."""
         a = len(packets)
         gts = np.ascontiguousarray(global_time, dtype=np.uint64)
         metas = np.ascontiguousarray(meta, dtype=np.uint32)
         if len(gts) != a or len(metas) != a:
             raise ValueError("append: one global_time and one meta per packet")
-        top = int(self.rowid.max()) if self.n else 0
+        top = self._top_rowid()
         ids = (np.arange(top + 1, top + 1 + a, dtype=np.int64) if rowid is None
                else np.ascontiguousarray(rowid, dtype=np.int64))
         if len(ids) != a or (a and (ids[0] <= top or (a > 1 and (ids[1:] <= ids[:-1]).any()))):
@@ -135,7 +190,8 @@ class SyncStore(object):
         if self.n and (self.member is None) != (member is None):
             raise ValueError("append: give members exactly when the store has a member column")
         mem = None if member is None else np.ascontiguousarray(member, dtype=np.uint64)
-        rows = np.arange(self.n, self.n + a, dtype=np.int64)
+        n0 = self.n
+        rows = np.arange(n0, n0 + a, dtype=np.int64)
         if a == 0:
             return rows
         lens = np.fromiter((len(p) for p in packets), dtype=np.uint64, count=a)
@@ -147,40 +203,56 @@ class SyncStore(object):
             _native.check(lib.dsy_store_append(self.ctx.handle, self._handle, data, len(data), new_off.ctypes.data, a,
                                                gts.ctypes.data, metas.ctypes.data,
                                                mem.ctypes.data if self._dup_indexed else None))
-        # host columns
-        base = self.offsets[-1]
-        self.offsets = np.concatenate([self.offsets, base + new_off[1:]])
-        if isinstance(self.blob, np.ndarray):
-            self.blob = np.concatenate([self.blob, np.frombuffer(data, dtype=np.uint8)])
-        else:
-            if not isinstance(self.blob, bytearray):
-                self.blob = bytearray(self.blob)
-            self.blob += data
-        self.global_time = np.concatenate([self.global_time, gts])
-        self.meta = np.concatenate([self.meta, metas])
-        self.undone = np.concatenate([self.undone, np.zeros(a, dtype=np.int64)])
-        self.rowid = np.concatenate([self.rowid, ids])
+        # host columns: geometric growth, O(batch) per append
+        b = self._buf
+        b["offsets"] = _room(b["offsets"], n0 + 1, n0 + a + 1)
+        b["offsets"][n0 + 1:n0 + a + 1] = b["offsets"][n0] + new_off[1:]
+        for name, vals in (("global_time", gts), ("meta", metas), ("undone", np.zeros(a, dtype=np.int64)),
+                           ("rowid", ids), ("deleted", np.zeros(a, dtype=bool))):
+            b[name] = _room(b[name], n0, n0 + a)
+            b[name][n0:n0 + a] = vals
         if mem is not None:
-            self.member = mem if self.member is None else np.concatenate([self.member, mem])
-        self.n += a
-        self._row_of_id = None
-        # per-meta live rows: old rows first on equal global times (smaller rowid), new ones in insertion order
-        for m in np.unique(metas):
-            seg = np.concatenate([self._live.get(int(m), self._empty).astype(np.int64), rows[metas == m]])
-            self._live[int(m)] = seg[np.argsort(self.global_time[seg], kind="stable")]
+            b["member"] = np.empty(0, dtype=np.uint64) if b["member"] is None else b["member"]
+            b["member"] = _room(b["member"], n0, n0 + a)
+            b["member"][n0:n0 + a] = mem
+        if isinstance(self.blob, np.ndarray):
+            self.blob = bytearray(self.blob.tobytes())
+        elif not isinstance(self.blob, bytearray):
+            self.blob = bytearray(self.blob)
+        self.blob += data
+        self.n = n0 + a
+        self._top = int(ids[-1])
+        if self._row_of_id is not None:
+            self._row_of_id.update(zip(ids.tolist(), rows.tolist()))
+        # per-meta live rows: merged lazily (live_rows)
+        order = np.argsort(metas, kind="stable")
+        sm = metas[order]
+        cuts = np.flatnonzero(sm[1:] != sm[:-1]) + 1
+        for part in np.split(order, cuts):
+            m = int(metas[part[0]])
+            self._pending.setdefault(m, []).append(rows[part])
+            self._nlive[m] = self._nlive.get(m, 0) + len(part)
         return rows
 
+    def _top_rowid(self):
+        if getattr(self, "_top", None) is None:
+            self._top = int(self.rowid.max()) if self.n else 0
+        return self._top
+
+    # ------------------------------------------------------------------------------------------ DELETEs
     def prune(self, meta_id, max_global_time):
         """DELETE FROM sync WHERE meta_message = ? AND global_time <= ? (community.py:1092-1096, GlobalTimePruning):
-        the rows leave the live index (host and device).  Returns the number of rows deleted."""
-        seg = self._live.get(int(meta_id))
-        if seg is None or not len(seg) or max_global_time < 0:
+        the rows leave the live index (host and device) and the duplicate table.  Returns the number of rows deleted."""
+        seg = self.live_rows(meta_id)
+        if not len(seg) or max_global_time < 0:
             return 0
         k = int(np.searchsorted(self.global_time[seg], np.uint64(max_global_time), side="right"))
         if not k:
             return 0
+        self._mark_deleted(seg[:k])
         self._live[int(meta_id)] = seg[k:]
-        self._prunes.append((int(meta_id), int(max_global_time), self.n))
+        self._nlive[int(meta_id)] -= k
+        self._ops.append(("prune", int(meta_id), int(max_global_time), self.n))
         if self._handle is not None:
             out = ctypes.c_uint64()
             _native.check(self.ctx.lib.dsy_store_prune(self.ctx.handle, self._handle, int(meta_id),
@@ -188,18 +260,59 @@ class SyncStore(object):
             assert out.value == k, (out.value, k)
         return k
 
+    def delete_rows(self, rows):
+        """DELETE FROM sync WHERE id = ? for the given store rows (the sequence-number conflict DELETE,
+        dispersy.py:1006-1007, and LastSyncDistribution's history pruning, :1581-1591): they leave the live index, the
+        duplicate table and row_of_id.  Returns the number of rows deleted (already deleted ones not counted)."""
+        rows = np.unique(np.asarray(rows, dtype=np.int64))
+        if not len(rows):
+            return 0
+        if rows[0] < 0 or rows[-1] >= self.n:
+            raise IndexError("delete_rows: row out of range")
+        rows = rows[~self.deleted[rows]]
+        if not len(rows):
+            return 0
+        live = rows[self.undone[rows] == 0]
+        for m in np.unique(self.meta[live]).tolist():
+            seg = self.live_rows(m)
+            drop = live[self.meta[live] == m]
+            self._live[m] = seg[~np.isin(seg, drop, assume_unique=True)]
+            self._nlive[m] -= len(drop)
+        self._mark_deleted(rows)
+        self._ops.append(("delete", rows, self.n))
+        if self._handle is not None:
+            out = ctypes.c_uint64()
+            rws = rows.astype(np.uint64)  # keep the array alive across the call
+            _native.check(self.ctx.lib.dsy_store_delete(self.ctx.handle, self._handle, rws.ctypes.data, len(rws),
+                                                        ctypes.byref(out)))
+            assert out.value == len(live), (out.value, len(live))
+        return len(rows)
+
+    def _mark_deleted(self, rows):
+        self._buf["deleted"][rows] = True
+        if self._row_of_id is not None:
+            for rid in self.rowid[rows].tolist():
+                self._row_of_id.pop(rid, None)
+
     # ------------------------------------------------------------------------------- duplicate check
     def dup_check(self, members, global_times, packets, signature_lengths):
         """(verdict, row) per received message against the stored (member, global_time) rows (dsy_dup_check,
         _is_duplicate_sync_message dispersy.py:831-918): verdicts are _native.DSY_DUP_*; row -1 when new."""
         if self.member is None:
             raise ValueError("dup_check needs the store's member column")
+        if self.communities is not None and len(self.communities) > 1:
+            raise ValueError("dup_check: the store spans communities %s; the (member, global_time) key is unique only "
+                             "within one community (UNIQUE(community, member, global_time))" % sorted(self.communities))
         h = self.handle
         lib = self.ctx.lib
         if not self._dup_indexed:
             _native.check(lib.dsy_store_index_members(self.ctx.handle, h, self.member.ctypes.data,
                                                       self.global_time.ctypes.data, self.n))
             self._dup_indexed = True
+            gone = np.flatnonzero(self.deleted).astype(np.uint64)
+            if len(gone):  # rows deleted before the table existed are not in it
+                out = ctypes.c_uint64()
+                _native.check(lib.dsy_store_delete(self.ctx.handle, h, gone.ctypes.data, len(gone), ctypes.byref(out)))
         m = len(packets)
         mem = np.ascontiguousarray(members, dtype=np.uint64)
         gts = np.ascontiguousarray(global_times, dtype=np.uint64)
@@ -246,26 +359,33 @@ class SyncStore(object):
             blob = self.blob if isinstance(self.blob, bytes) else bytes(self.blob)
             h = ctypes.c_void_p()
             n0 = self._n_sorted
-            blob0 = blob[:int(self.offsets[n0])] if n0 < self.n else blob
-            undone = (self.undone != 0).astype(np.uint8)
-            _native.check(ctx.lib.dsy_store_upload(ctx.handle, blob0, len(blob0), self.offsets.ctypes.data, n0,
-                                                   self.global_time.ctypes.data, self.meta.ctypes.data,
-                                                   undone.ctypes.data, ctypes.byref(h)))
+            offsets = np.ascontiguousarray(self.offsets)
+            blob0 = blob[:int(offsets[n0])] if n0 < self.n else blob
+            undone = (self.undone[:n0] != 0).astype(np.uint8)
+            gts0, metas0 = np.ascontiguousarray(self.global_time[:n0]), np.ascontiguousarray(self.meta[:n0])
+            _native.check(ctx.lib.dsy_store_upload(ctx.handle, blob0, len(blob0), offsets.ctypes.data, n0,
+                                                   gts0.ctypes.data, metas0.ctypes.data, undone.ctypes.data,
+                                                   ctypes.byref(h)))
             self._handle = h
             # rows appended and DELETEs made before the first upload, replayed in their order (a DELETE never
             # reaches rows appended after it)
             done = n0
-            for meta_id, max_gt, n_at in self._prunes + [(None, None, self.n)]:
+            for op in self._ops + [("end", None, None, self.n)]:
+                n_at = op[-1]
                 if n_at > done:
-                    off = np.ascontiguousarray(self.offsets[done:n_at + 1] - self.offsets[done])
-                    tail = blob[int(self.offsets[done]):int(self.offsets[n_at])]
+                    off = np.ascontiguousarray(offsets[done:n_at + 1] - offsets[done])
+                    tail = blob[int(offsets[done]):int(offsets[n_at])]
+                    gts1 = np.ascontiguousarray(self.global_time[done:n_at])
+                    metas1 = np.ascontiguousarray(self.meta[done:n_at])
                     _native.check(ctx.lib.dsy_store_append(ctx.handle, h, tail, len(tail), off.ctypes.data,
-                                                           n_at - done, self.global_time[done:n_at].ctypes.data,
-                                                           self.meta[done:n_at].ctypes.data, None))
+                                                           n_at - done, gts1.ctypes.data, metas1.ctypes.data, None))
                     done = n_at
-                if meta_id is not None:
-                    out = ctypes.c_uint64()
-                    _native.check(ctx.lib.dsy_store_prune(ctx.handle, h, meta_id, max_gt, ctypes.byref(out)))
+                out = ctypes.c_uint64()
+                if op[0] == "prune":
+                    _native.check(ctx.lib.dsy_store_prune(ctx.handle, h, op[1], op[2], ctypes.byref(out)))
+                elif op[0] == "delete":
+                    rws = op[1].astype(np.uint64)
+                    _native.check(ctx.lib.dsy_store_delete(ctx.handle, h, rws.ctypes.data, len(rws), ctypes.byref(out)))
             if self._replaced:  # UPDATEs made before the first upload
                 rows = sorted(self._replaced)
                 self._replace_device(rows, [self._replaced[r] for r in rows])

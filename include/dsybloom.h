@@ -174,10 +174,16 @@ int dsy_store_append(dsy_ctx* ctx, dsy_store* store, const uint8_t* blob, uint64
                      uint64_t a, const uint64_t* global_time, const uint32_t* meta, const uint64_t* member);
 
 /* GlobalTimePruning's DELETE FROM sync WHERE meta_message = ? AND global_time <= ? (community.py:1092-1096, run by
- * update_global_time): the meta's rows up to max_global_time leave the responder's index.  *out_deleted = their
- * number.  (Their (member, global_time) keys stay in the duplicate table: any later message with such a global time
- * is inactive, and _check_full_sync_distribution_batch drops it as pruned before the lookup.) */
+ * update_global_time): the meta's rows up to max_global_time leave the responder's index and, when the store has a
+ * (member, global_time) table, that table.  *out_deleted = their number. */
 int dsy_store_prune(dsy_ctx* ctx, dsy_store* store, uint32_t meta, uint64_t max_global_time, uint64_t* out_deleted);
+
+/* DELETE FROM sync WHERE id = ? for k arbitrary store rows (0-based positions): the conflict DELETE of the
+ * sequence-number check (dispersy.py:1006-1007) and LastSyncDistribution's history pruning (dispersy.py:1581-1591).
+ * The rows leave the responder's live index (a stable compaction on the device) and, when the store has a
+ * (member, global_time) table, that table too (their slots become tombstones).  Rows may repeat, be undone or be
+ * deleted already.  *out_deleted = live index entries removed. */
+int dsy_store_delete(dsy_ctx* ctx, dsy_store* store, const uint64_t* rows, uint64_t k, uint64_t* out_deleted);
 
 /* ------------------------------------------------------------------------------------ duplicate check */
 /* Received sync packets are checked against the store by (member, global_time) before they are stored
