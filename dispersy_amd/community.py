@@ -26,7 +26,7 @@ import numpy as np
 
 from . import _native
 from .bloomfilter import BloomFilter
-from .distribution import GlobalTimePruning, SyncDistribution
+from .distribution import FullSyncDistribution, GlobalTimePruning, LastSyncDistribution, SyncDistribution
 
 MAX_GT = 2 ** 63 - 1  # sqlite's signed 64-bit ceiling (community.py:2545-2548)
 
@@ -43,9 +43,23 @@ class DropMessage(object):
         self.reason = reason
 
 
+class DelayMessageBySequence(object):
+    """message.py:147-166: the message waits until its member's sequence numbers missing_low..missing_high arrive."""
+
+    def __init__(self, delayed, missing_low, missing_high):
+        assert 0 < missing_low <= missing_high, (missing_low, missing_high)
+        self.delayed = delayed
+        self.missing_low = missing_low
+        self.missing_high = missing_high
+
+
 def _member_id(message):
     auth = getattr(message, "authentication", None)
     return int(auth.member.database_id) if auth is not None else int(message.member)
+
+
+def _meta_id(message):
+    return message.database_id if hasattr(message, "database_id") else message.meta.database_id
 
 
 def _signature_length(message, default):
@@ -215,16 +229,21 @@ class SyncCommunity(object):
             cache.bloom_filter.add_keys(packets)
 
     def _check_full_sync_distribution_batch(self, messages):
-        """dispersy.py:921-1065 for a FullSyncDistribution batch without sequence numbers (:1043-1063): every message
-        is returned, in (global_time, packet) order, either as itself (accept) or as DropMessage(message, reason).
+        """dispersy.py:921-1065: every message, in (global_time, packet) order, either as itself (accept),
+        DropMessage(message, reason) or -- sequence-numbered metas only -- DelayMessageBySequence.
         The per-message `_is_duplicate_sync_message` lookups (:831-918) run as ONE hash join on the GPU
         (SyncStore.dup_check); their side effects follow in order: the undo proof of an exact duplicate of an undone
         packet is sent (recorded in self.sent_packets as (candidate, packet, reason)), and a stored packet that
         differs only after the first signature_length bytes and compares lower is replaced (UPDATE, :903).
         A message carries .packet, .distribution.global_time, .candidate, its member's database id
         (.authentication.member.database_id, or .member) and signature length
-        (.authentication.member.signature_length, else the community's), and optionally .meta (its pruning)."""
+        (.authentication.member.signature_length, else the community's), and optionally .meta (its pruning; a
+        FullSyncDistribution with enable_sequence_number selects the sequence-number branch :954-1037, whose messages
+        also carry .distribution.sequence_number and their meta's database id)."""
         messages = sorted(messages, key=lambda m: (m.distribution.global_time, m.packet))
+        meta = getattr(messages[0], "meta", None) if messages else None
+        if meta is not None and getattr(meta.distribution, "enable_sequence_number", False):
+            return self._check_sequence_number_batch(messages)
         acceptable = self.acceptable_global_time
         out, todo, unique = [], [], set()
         for message in messages:
@@ -232,9 +251,7 @@ class SyncCommunity(object):
             if gt > acceptable:
                 out.append(DropMessage(message, "global time is not within acceptable range"))
                 continue
-            meta = getattr(message, "meta", None)
-            pruning = meta.distribution.pruning if meta is not None else None
-            if isinstance(pruning, GlobalTimePruning) and not (self.global_time - gt < pruning.inactive_threshold):
+            if self._is_pruned(message):
                 out.append(DropMessage(message, "message has been pruned"))  # distribution.py:80-81
                 continue
             key = (_member_id(message), gt)
@@ -246,49 +263,177 @@ class SyncCommunity(object):
             todo.append(len(out) - 1)
         if todo:
             checked = [out[i] for i in todo]
-            verdict, rows = self._store.dup_check([_member_id(m) for m in checked],
-                                                  [m.distribution.global_time for m in checked],
-                                                  [m.packet for m in checked],
-                                                  [_signature_length(m, self._signature_length) for m in checked])
-            replace_rows, replace_packets = [], []
+            verdict, rows = self._dup_lookup(checked)
+            replaces = []
             for i, message, v, row in zip(todo, checked, verdict.tolist(), rows.tolist()):
-                if v == _native.DSY_DUP_NEW:
+                if self._duplicate_side_effects(message, v, row, replaces):
+                    out[i] = DropMessage(message, "duplicate message by global_time (2)")
+            self._flush_replaces(replaces)
+        return out
+
+    def _is_pruned(self, message):
+        meta = getattr(message, "meta", None)
+        pruning = meta.distribution.pruning if meta is not None else None
+        return isinstance(pruning, GlobalTimePruning) and not (self.global_time - message.distribution.global_time <
+                                                               pruning.inactive_threshold)
+
+    def _dup_lookup(self, messages):
+        return self._store.dup_check([_member_id(m) for m in messages],
+                                     [m.distribution.global_time for m in messages], [m.packet for m in messages],
+                                     [_signature_length(m, self._signature_length) for m in messages])
+
+    def _duplicate_side_effects(self, message, verdict, row, replaces):
+        """_is_duplicate_sync_message (dispersy.py:868-918) given the GPU lookup's verdict: True when a row with the
+        message's (member, global_time) exists; sends the undo proof / records the UPDATE like the reference."""
+        if verdict == _native.DSY_DUP_NEW:
+            return False
+        if verdict == _native.DSY_DUP_EXACT:
+            undone = int(self._store.undone[row])
+            if undone:
+                try:
+                    proof = self._store.packet(self._store.row_of_id(undone))
+                except KeyError:
+                    proof = None
+                if proof is not None:
+                    self.sent_packets.append((message.candidate, proof, "-caused by duplicate-undo-"))
+        elif verdict == _native.DSY_DUP_REPLACE:
+            # the host copy changes now (a later proof send in this batch reads it), HBM once the batch is done
+            self._store.replace_packet([row], [message.packet], device=False)
+            replaces.append((row, message.packet))
+        return True
+
+    def _flush_replaces(self, replaces):
+        if replaces:
+            self._store.replace_packet([r for r, _ in replaces], [p for _, p in replaces])
+
+    def _highest(self, meta_id, member):
+        """SELECT MAX(global_time), MAX(sequence), COUNT(*) FROM sync WHERE member = ? AND meta_message = ?
+        (dispersy.py:959-961, :1010-1012) -> (last_global_time or 0, last_sequence or 0)."""
+        rows = self._store.member_rows(meta_id, member)
+        if not len(rows):
+            return 0, 0
+        return int(self._store.global_time[rows].max()), int(self._store.sequence[rows].max())
+
+    def _check_sequence_number_batch(self, messages):
+        """dispersy.py:954-1037, messages already in (global_time, packet) order.  The (member, global_time) lookups
+        of every message run up front as one GPU hash join; a row that a DELETE of this batch removed before the
+        message's turn counts as absent (nothing is INSERTed during the check, so this is exactly the sequential
+        lookup).  The reference's generator ends -- silently, the rest of the batch is neither yielded nor dropped --
+        when its `LIMIT 1 OFFSET ?` query finds no row (py2: the StopIteration of `.next()` inside the generator,
+        :986-987): that happens when an earlier message of the batch raised the member's in-memory highest sequence
+        number past the stored rows; the same cut-off is kept here."""
+        st = self._store
+        meta_id = _meta_id(messages[0])
+        acceptable = self.acceptable_global_time
+        highest = {}
+        for message in messages:
+            member = _member_id(message)
+            if member not in highest:
+                highest[member] = self._highest(meta_id, member)
+        verdict, found = self._dup_lookup(messages)
+        out, unique, replaces = [], set(), []
+        for message, v, row in zip(messages, verdict.tolist(), found.tolist()):
+            gt, seq_no = message.distribution.global_time, message.distribution.sequence_number
+            member = _member_id(message)
+            if gt > acceptable:
+                out.append(DropMessage(message, "global time is not within acceptable range (%d, we accept %d)"
+                                       % (gt, acceptable)))
+                continue
+            if self._is_pruned(message):
+                out.append(DropMessage(message, "message has been pruned"))
+                continue
+            key = (member, gt)
+            if key in unique:
+                out.append(DropMessage(message, "duplicate message by member^global_time (1)"))
+                continue
+            unique.add(key)
+            last_global_time, seq = highest[member]
+            if seq >= seq_no:
+                rows = st.member_rows(meta_id, member)
+                if seq_no - 1 >= len(rows):
+                    break  # the OFFSET query's StopIteration ends the reference's generator (see above)
+                have = int(rows[seq_no - 1])
+                have_gt, have_packet = int(st.global_time[have]), st.packet(have)
+                if message.packet == have_packet:
+                    out.append(DropMessage(message, "duplicate message by binary packet"))
                     continue
-                if v == _native.DSY_DUP_EXACT:
-                    undone = int(self._store.undone[row])
-                    if undone:
-                        try:
-                            proof = self._store.packet(self._store.row_of_id(undone))
-                        except KeyError:
-                            proof = None
-                        if proof is not None:
-                            self.sent_packets.append((message.candidate, proof, "-caused by duplicate-undo-"))
-                elif v == _native.DSY_DUP_REPLACE:
-                    # the host copy changes now (a later proof send in this batch reads it), HBM once below
-                    self._store.replace_packet([row], [message.packet], device=False)
-                    replace_rows.append(row)
-                    replace_packets.append(message.packet)
-                out[i] = DropMessage(message, "duplicate message by global_time (2)")
-            if replace_rows:
-                self._store.replace_packet(replace_rows, replace_packets)
+                if (have_gt, have_packet) < (gt, message.packet):
+                    # keep ours and send it back (:996-1002)
+                    self.sent_packets.append((message.candidate, have_packet, "-caused by check_full_sync-"))
+                    out.append(DropMessage(message, "duplicate message by sequence number (1)"))
+                    continue
+                # DELETE FROM sync WHERE member = ? AND meta_message = ? AND global_time >= ? (:1006-1007), then the
+                # highest cache is refreshed (:1010-1012 also rebind last_global_time; the local `seq` keeps its
+                # value, as in the reference)
+                st.delete_rows(rows[st.global_time[rows] >= np.uint64(have_gt)])
+                highest[member] = self._highest(meta_id, member)
+                last_global_time = highest[member][0]
+            elif seq + 1 != seq_no:
+                out.append(DelayMessageBySequence(message, seq + 1, seq_no - 1))
+                continue
+            if row >= 0 and st.deleted[row]:
+                v = _native.DSY_DUP_NEW  # deleted earlier in this batch: the SELECT finds nothing
+            if self._duplicate_side_effects(message, v, row, replaces):
+                out.append(DropMessage(message, "duplicate message by global_time (1)"))
+                continue
+            if last_global_time and gt <= last_global_time:
+                out.append(DropMessage(message, "higher sequence number with lower global time than most recent "
+                                                "message"))
+                continue
+            highest[member] = (gt, seq + 1)
+            out.append(message)
+        self._flush_replaces(replaces)
         return out
 
     def store_messages(self, messages):
         """Dispersy._store (dispersy.py:1475-1612) for the sync table: INSERT the messages' packets (one batched
-        SyncStore.append -> dsy_store_append into HBM), raise the community's global time to the highest stored one,
-        then dispersy_store(messages) updates the cached claim filter.  A message carries .packet,
-        .distribution.global_time and its meta's database id (.database_id, or .meta.database_id).  As in the
-        reference, the caller has already dropped duplicates (dispersy.py:1496-1498); LastSyncDistribution's history
-        pruning (DELETE of older rows, :1560-1604) is not part of this path.  Returns the new store rows."""
+        SyncStore.append -> dsy_store_append into HBM; sequence-numbered FullSync messages store their sequence
+        number, :1529-1531), DELETE what LastSyncDistribution no longer keeps -- each member's rows beyond the newest
+        history_size, or the items its custom_callback names (:1558-1591; one dsy_store_delete) --, raise the
+        community's global time to the highest stored one, then dispersy_store(messages) updates the cached claim
+        filter.  A message carries .packet, .distribution.global_time and its meta's database id (.database_id, or
+        .meta.database_id); .meta.distribution selects the sequence/history handling.  As in the reference, the
+        caller has already dropped duplicates (dispersy.py:1496-1498).  Double-member authentication (the
+        double_signed_sync table) is outside this path.  Returns the new store rows."""
         if not messages:
             return np.zeros(0, dtype=np.int64)
-        metas = [m.database_id if hasattr(m, "database_id") else m.meta.database_id for m in messages]
+        metas = [_meta_id(m) for m in messages]
         gts = [m.distribution.global_time for m in messages]
         members = [_member_id(m) for m in messages] if self._store.member is not None else None
-        rows = self._store.append([m.packet for m in messages], gts, metas, member=members)
+        seqs = []
+        for m in messages:
+            d = getattr(getattr(m, "meta", None), "distribution", None)
+            seqs.append(m.distribution.sequence_number if isinstance(d, FullSyncDistribution) and
+                        d.enable_sequence_number else 0)
+        rows = self._store.append([m.packet for m in messages], gts, metas, member=members, sequence=seqs)
+        self._last_sync_history(messages)
         self.update_global_time(max(gts))
         self.dispersy_store(messages)
         return rows
+
+    def _last_sync_history(self, messages):
+        st = self._store
+        by_meta = OrderedDict()
+        for m in messages:
+            meta = getattr(m, "meta", None)
+            if meta is not None and isinstance(meta.distribution, LastSyncDistribution):
+                by_meta.setdefault(id(meta), (meta, []))[1].append(m)
+        drop = []
+        for meta, msgs in by_meta.values():
+            dist = meta.distribution
+            if dist.custom_callback:
+                for syncid, _ in dist.custom_callback[1](msgs):
+                    try:
+                        drop.append(st.row_of_id(syncid))
+                    except KeyError:
+                        pass
+                continue
+            for member in OrderedDict.fromkeys(_member_id(m) for m in msgs):
+                rows = st.member_rows(meta.database_id, member)
+                if len(rows) > dist.history_size:
+                    drop.extend(rows[:len(rows) - dist.history_size].tolist())
+        if drop:
+            st.delete_rows(drop)
 
     def dispersy_claim_sync_bloom_filter(self, request_cache):
         """community.py:709-758.  Returns (time_low, time_high, modulo, offset, bloom_filter) or None."""

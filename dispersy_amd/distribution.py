@@ -36,8 +36,27 @@ class SyncDistribution(object):
         return {"ASC": 1, "DESC": -1, "RANDOM": 0}[self.synchronization_direction]
 
 
-FullSyncDistribution = SyncDistribution
-LastSyncDistribution = SyncDistribution
+class FullSyncDistribution(SyncDistribution):
+    """distribution.py:245-288: optionally sequence-numbered per member (enable_sequence_number): received messages are
+    then checked against each member's highest stored sequence number (dispersy.py:954-1037)."""
+
+    def __init__(self, synchronization_direction="ASC", priority=127, enable_sequence_number=False, pruning=None):
+        assert isinstance(enable_sequence_number, bool)
+        super(FullSyncDistribution, self).__init__(synchronization_direction, priority, pruning)
+        self.enable_sequence_number = enable_sequence_number
+
+
+class LastSyncDistribution(SyncDistribution):
+    """distribution.py:291-313: only the newest history_size messages per member are kept; Dispersy._store deletes
+    the older ones after every INSERT (dispersy.py:1558-1591).  custom_callback: (check, delete) pair; delete(messages)
+    returns the (id, global_time) items to DELETE instead."""
+
+    def __init__(self, synchronization_direction="ASC", priority=127, history_size=1, pruning=None, custom_callback=None):
+        assert isinstance(history_size, int) and history_size > 0
+        assert not custom_callback or isinstance(custom_callback, tuple)
+        super(LastSyncDistribution, self).__init__(synchronization_direction, priority, pruning)
+        self.history_size = history_size
+        self.custom_callback = custom_callback
 
 
 class DirectDistribution(object):

@@ -6,6 +6,7 @@ Rows are kept in the order of the reference's `sync_meta_message_undone_global_t
     blob        u8[sum L]   packets back to back        offsets   u64[N+1]
     global_time u64[N]      meta u32[N]                 undone    i64[N]     rowid  i64[N]
     member      u64[N]      (optional: the (member, global_time) duplicate check, dispersy.py:831-918)
+    sequence    i64[N]      the sequence number of sequence-numbered FullSync messages, 0 for NULL (dispersy.py:1529)
     deleted     bool[N]     rows a DELETE removed (pruning, sequence conflicts, LastSync history)
 
 `undone` is the reference's column: 0, or the id of the undo message whose packet is the proof.
@@ -28,7 +29,7 @@ import numpy as np
 
 from . import _native
 
-_COLUMNS = ("global_time", "meta", "undone", "rowid", "member", "deleted")
+_COLUMNS = ("global_time", "meta", "undone", "rowid", "member", "sequence", "deleted")
 
 
 def _room(buf, used, need):
@@ -42,7 +43,7 @@ def _room(buf, used, need):
 
 class SyncStore(object):
     def __init__(self, blob, offsets, global_time, meta, undone=None, rowid=None, ctx=None, member=None,
-                 communities=None):
+                 communities=None, sequence=None):
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         n = self.n = len(offsets) - 1
         self._buf = dict(
@@ -53,6 +54,8 @@ class SyncStore(object):
             rowid=(np.arange(1, n + 1, dtype=np.int64) if rowid is None
                    else np.ascontiguousarray(rowid, dtype=np.int64).copy()),
             member=None if member is None else np.ascontiguousarray(member, dtype=np.uint64).copy(),
+            sequence=(np.zeros(n, dtype=np.int64) if sequence is None
+                      else np.ascontiguousarray([x or 0 for x in sequence], dtype=np.int64)),
             deleted=np.zeros(n, dtype=bool))
         self.blob = blob if isinstance(blob, (bytes, bytearray, memoryview, np.ndarray)) else bytes(blob)
         assert all(len(self._buf[c]) == n for c in _COLUMNS if self._buf[c] is not None)
@@ -82,6 +85,8 @@ class SyncStore(object):
                 self._live[int(self.meta[seg[0]])] = seg
                 self._nlive[int(self.meta[seg[0]])] = len(seg)
         self._empty = np.zeros(0, dtype=np.int64)
+        self._groups = None  # (meta, member) -> rows, built on first use (member_rows)
+        self._gpending = {}
 
     # ------------------------------------------------------------------------------------------ columns
     def _col(self, name):
@@ -94,33 +99,36 @@ class SyncStore(object):
     undone = property(lambda self: self._col("undone"))
     rowid = property(lambda self: self._col("rowid"))
     member = property(lambda self: self._col("member"))
+    sequence = property(lambda self: self._col("sequence"))
     deleted = property(lambda self: self._col("deleted"))
 
     # ------------------------------------------------------------------------------------ constructors
     @classmethod
     def from_rows(cls, rows, ctx=None, communities=None):
-        """rows: iterable of (rowid, global_time, meta_message, undone, packet[, member])."""
+        """rows: iterable of (rowid, global_time, meta_message, undone, packet[, member[, sequence]])."""
         rows = sorted(rows, key=lambda r: (r[2], r[1], r[0]))
         n = len(rows)
         offsets = np.zeros(n + 1, dtype=np.uint64)
         if n:
             np.cumsum([len(r[4]) for r in rows], out=offsets[1:])
         member = [r[5] for r in rows] if rows and len(rows[0]) > 5 else None
+        sequence = [r[6] for r in rows] if rows and len(rows[0]) > 6 else None
         return cls(b"".join(bytes(r[4]) for r in rows), offsets, [r[1] for r in rows], [r[2] for r in rows],
-                   [r[3] for r in rows], [r[0] for r in rows], ctx=ctx, member=member, communities=communities)
+                   [r[3] for r in rows], [r[0] for r in rows], ctx=ctx, member=member, communities=communities,
+                   sequence=sequence)
 
     @classmethod
     def from_sqlite(cls, conn, community=None, ctx=None):
         """Export a Dispersy database's `sync` table (optionally one community) in index order."""
-        sql = "SELECT id, global_time, meta_message, undone, packet, member, community FROM sync"
+        sql = "SELECT id, global_time, meta_message, undone, packet, member, community, sequence FROM sync"
         args = ()
         if community is not None:
             sql += " WHERE community = ?"
             args = (community,)
         sql += " ORDER BY meta_message, global_time, id"
         rows = list(conn.execute(sql, args))
-        return cls.from_rows([(i, g, m, u, bytes(p), mb) for i, g, m, u, p, mb, _ in rows], ctx=ctx,
-                             communities={c for *_, c in rows} if rows else ({community} if community is not None else None))
+        return cls.from_rows([(i, g, m, u, bytes(p), mb, sq) for i, g, m, u, p, mb, _, sq in rows], ctx=ctx,
+                             communities={r[6] for r in rows} if rows else ({community} if community is not None else None))
 
     # --------------------------------------------------------------------------------------- accessors
     def packet(self, i):
@@ -170,13 +178,38 @@ class SyncStore(object):
     def meta_ids(self):
         return sorted(set(self._nlive) | set(self._live))
 
+    def member_rows(self, meta_id, member):
+        """Rows of one (meta_message, member) -- undone ones included, deleted ones not -- in global_time order (unique
+        within a member): `SELECT ... FROM sync WHERE member = ? AND meta_message = ? ORDER BY global_time`
+        (dispersy.py:959, :986, :1582-1586)."""
+        if self.member is None:
+            raise ValueError("member_rows needs the store's member column")
+        if self._groups is None:
+            keep = np.flatnonzero(~self.deleted)
+            order = keep[np.lexsort((self.global_time[keep], self.member[keep], self.meta[keep]))]
+            km, kb = self.meta[order], self.member[order]
+            cuts = np.flatnonzero((km[1:] != km[:-1]) | (kb[1:] != kb[:-1])) + 1
+            self._groups = {(int(self.meta[g[0]]), int(self.member[g[0]])): g for g in np.split(order, cuts) if len(g)}
+            self._gpending = {}
+        key = (int(meta_id), int(member))
+        rows = self._groups.get(key, self._empty)
+        pend = self._gpending.pop(key, None)
+        if pend:
+            rows = np.concatenate([rows] + pend)
+        rows = rows[~self.deleted[rows]]
+        if pend:
+            rows = rows[np.argsort(self.global_time[rows], kind="stable")]
+        self._groups[key] = rows
+        return rows
+
     # ------------------------------------------------------------------------------------------ ingest
-    def append(self, packets, global_time, meta, rowid=None, member=None):
+    def append(self, packets, global_time, meta, rowid=None, member=None, sequence=None):
         """INSERT INTO sync of a batch of received packets (dispersy.py:1475-1612), undone = 0.
 
         packets: list of bytes; global_time / meta (/ member): one per packet; rowid: increasing ids above every
-        stored one (default: the next ids, as SQLite assigns them).  Returns the new rows' positions.  When the store
-        is on the device already, the batch goes there in one dsy_store_append call.  Host work is O(batch)."""
+        stored one (default: the next ids, as SQLite assigns them); sequence: the messages' sequence numbers (0 or None:
+        NULL).  Returns the new rows' positions.  When the store is on the device already, the batch goes there in one
+        dsy_store_append call.  Host work is O(batch)."""
         a = len(packets)
         gts = np.ascontiguousarray(global_time, dtype=np.uint64)
         metas = np.ascontiguousarray(meta, dtype=np.uint32)
@@ -207,8 +240,10 @@ class SyncStore(object):
         b = self._buf
         b["offsets"] = _room(b["offsets"], n0 + 1, n0 + a + 1)
         b["offsets"][n0 + 1:n0 + a + 1] = b["offsets"][n0] + new_off[1:]
+        seqs = (np.zeros(a, dtype=np.int64) if sequence is None
+                else np.asarray([x or 0 for x in sequence], dtype=np.int64))
         for name, vals in (("global_time", gts), ("meta", metas), ("undone", np.zeros(a, dtype=np.int64)),
-                           ("rowid", ids), ("deleted", np.zeros(a, dtype=bool))):
+                           ("rowid", ids), ("sequence", seqs), ("deleted", np.zeros(a, dtype=bool))):
             b[name] = _room(b[name], n0, n0 + a)
             b[name][n0:n0 + a] = vals
         if mem is not None:
@@ -224,6 +259,9 @@ class SyncStore(object):
         self._top = int(ids[-1])
         if self._row_of_id is not None:
             self._row_of_id.update(zip(ids.tolist(), rows.tolist()))
+        if self._groups is not None and mem is not None:
+            for r, m, b_ in zip(rows.tolist(), metas.tolist(), mem.tolist()):
+                self._gpending.setdefault((m, b_), []).append(np.asarray([r], dtype=np.int64))
         # per-meta live rows: merged lazily (live_rows)
         order = np.argsort(metas, kind="stable")
         sm = metas[order]

@@ -13,6 +13,8 @@ Restated functions (reference file:line):
   claim_modulo         community.py:908-933
   insert_packets       dispersy.py:1523-1533 (Dispersy._store's INSERT INTO sync, one execute per message)
   check_full_sync_batch  dispersy.py:921-1065 (no sequence numbers) + is_duplicate_sync_message :831-918
+  check_sequence_batch   dispersy.py:954-1037 (the sequence-number branch)
+  store_last_sync        dispersy.py:1475-1612 (_store's INSERT + LastSyncDistribution history DELETE :1558-1591)
   SYNC_SCHEMA          dispersydatabase.py:53-64 (the sync table and its (meta_message, undone, global_time) index)
 """
 import math
@@ -74,6 +76,86 @@ def check_full_sync_batch(conn, community, messages, acceptable_global_time, glo
             continue
         out.append((message["index"], None))
     return out, sends
+
+
+def check_sequence_batch(conn, community, meta_id, messages, acceptable_global_time, global_time):
+    """dispersy.py:954-1037.  messages: dicts (member, gt, seq, packet, signature_length, inactive or None, index).
+    Returns (results, sends, ended_early): results [(index, reason | None | ("delay", low, high))] in the reference's
+    order; ended_early when the LIMIT 1 OFFSET query finds no row -- the py2 StopIteration that silently ends the
+    reference's generator (:986-987)."""
+    def highest_of(member):
+        g, s_, c = conn.execute("SELECT MAX(global_time), MAX(sequence), COUNT(*) FROM sync WHERE member = ? AND "
+                                "meta_message = ?", (member, meta_id)).fetchone()
+        return (g or 0, s_ or 0)
+
+    messages = sorted(messages, key=lambda m: (m["gt"], m["packet"]))
+    highest = {}
+    for m in messages:
+        if m["member"] not in highest:
+            highest[m["member"]] = highest_of(m["member"])
+    out, sends, unique = [], [], set()
+    for m in messages:
+        if m["gt"] > acceptable_global_time:
+            out.append((m["index"], "global time is not within acceptable range (%d, we accept %d)"
+                        % (m["gt"], acceptable_global_time)))
+            continue
+        if m.get("inactive") is not None and not (global_time - m["gt"] < m["inactive"]):
+            out.append((m["index"], "message has been pruned"))
+            continue
+        key = (m["member"], m["gt"])
+        if key in unique:
+            out.append((m["index"], "duplicate message by member^global_time (1)"))
+            continue
+        unique.add(key)
+        last_gt, seq = highest[m["member"]]
+        if seq >= m["seq"]:
+            row = conn.execute("SELECT global_time, packet FROM sync WHERE member = ? AND meta_message = ? "
+                               "ORDER BY global_time, packet LIMIT 1 OFFSET ?", (m["member"], meta_id, m["seq"] - 1)).fetchone()
+            if row is None:
+                return out, sends, True
+            have_gt, have = row[0], bytes(row[1])
+            if m["packet"] == have:
+                out.append((m["index"], "duplicate message by binary packet"))
+                continue
+            if (have_gt, have) < (m["gt"], m["packet"]):
+                sends.append((m["index"], have))
+                out.append((m["index"], "duplicate message by sequence number (1)"))
+                continue
+            conn.execute("DELETE FROM sync WHERE member = ? AND meta_message = ? AND global_time >= ?",
+                         (m["member"], meta_id, have_gt))
+            highest[m["member"]] = highest_of(m["member"])
+            last_gt = highest[m["member"]][0]  # :1010 rebinds last_global_time; `seq` keeps its old value
+        elif seq + 1 != m["seq"]:
+            out.append((m["index"], ("delay", seq + 1, m["seq"] - 1)))
+            continue
+        if is_duplicate_sync_message(conn, community, m, sends):
+            out.append((m["index"], "duplicate message by global_time (1)"))
+            continue
+        if last_gt and m["gt"] <= last_gt:
+            out.append((m["index"], "higher sequence number with lower global time than most recent message"))
+            continue
+        highest[m["member"]] = (m["gt"], seq + 1)
+        out.append((m["index"], None))
+    return out, sends, False
+
+
+def store_last_sync(conn, community, meta_id, history_size, messages):
+    """_store for a LastSyncDistribution meta (dispersy.py:1521-1591): INSERT every message, then for every member of
+    the batch DELETE its rows beyond the newest history_size by global time.  messages: (member, gt, packet).
+    Returns the new row ids."""
+    ids = []
+    for member, gt, packet in messages:
+        cur = conn.execute("INSERT INTO sync (community, member, global_time, meta_message, packet, sequence) "
+                           "VALUES (?, ?, ?, ?, ?, ?)", (community, member, gt, meta_id, packet, None))
+        ids.append(cur.lastrowid)
+    items = []
+    for member in set(m for m, _, _ in messages):
+        all_items = conn.execute("SELECT id, global_time FROM sync WHERE meta_message = ? AND member = ? "
+                                 "ORDER BY global_time", (meta_id, member)).fetchall()
+        if len(all_items) > history_size:
+            items.extend(all_items[:len(all_items) - history_size])
+    conn.executemany("DELETE FROM sync WHERE id = ?", [(i,) for i, _ in items])
+    return ids
 
 
 def insert_packets(conn, community, rows):

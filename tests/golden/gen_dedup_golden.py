@@ -2,15 +2,17 @@
 
 Test infrastructure, run in the build container (where /root/reference exists):
     PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_dedup_golden.py
-`Dispersy._is_duplicate_sync_message` (dispersy.py:831-918) and `Dispersy._check_full_sync_distribution_batch`
-(:921-1065) are lifted unchanged out of dispersy.py's AST, with the same mechanical edits as gen_sync_golden.py
-(`__debug__` -> False, decorators dropped), and run against an sqlite3 `sync` table built from the reference's
-schema string.  Only those two methods' text is parsed (the rest of dispersy.py is Python 2).  Bound in their
+`Dispersy._is_duplicate_sync_message` (dispersy.py:831-918), `Dispersy._check_full_sync_distribution_batch`
+(:921-1065, both the plain branch and the sequence-number branch :954-1037) and `Dispersy._store` (:1475-1612: the
+INSERT and LastSyncDistribution's history pruning) are lifted unchanged out of dispersy.py's AST, with the same
+mechanical edits as gen_sync_golden.py (`__debug__` -> False, decorators dropped), and run against an sqlite3 `sync`
+table built from the reference's schema string.  Only those two methods' text is parsed (the rest of dispersy.py is Python 2).  Bound in their
 globals: `str`/`buffer` -> bytes, `cmp`, `Message.Implementation` (the message stand-in class), and a
 `sorted` that accepts the py2 positional comparison function.  Only the resulting data is committed
-(dedup_vectors.json).
+(dedup_vectors.json, dedup_seq_vectors.json, laststore_vectors.json).
 """
 import ast
+import collections
 import functools
 import json
 import os
@@ -20,7 +22,7 @@ import numpy as np
 
 from gen_sync_golden import REF, _NoDebug, reference_schema
 
-LIFT = ("_is_duplicate_sync_message", "_check_full_sync_distribution_batch")
+LIFT = ("_is_duplicate_sync_message", "_check_full_sync_distribution_batch", "_store")
 
 
 def method_source(text, name):
@@ -32,7 +34,9 @@ def method_source(text, name):
     while end < len(lines) and not (lines[end].startswith("    ") and not lines[end].startswith("     ")
                                     and lines[end].strip()):
         end += 1
-    return "\n".join(l[4:] for l in lines[start:end])
+    # dedent by the class-body indentation only where it is present (the SQL of _store's triple-quoted strings
+    # starts at column 0)
+    return "\n".join(l[4:] if l.startswith("    ") else l for l in lines[start:end])
 
 
 def lift():
@@ -45,7 +49,10 @@ def lift():
         return sorted(seq, key=key, reverse=reverse)
 
     g = dict(str=bytes, buffer=bytes, cmp=lambda a, b: (a > b) - (a < b), sorted=py2_sorted,
-             DropMessage=DropMessage, DelayMessageBySequence=None, Message=_Obj(Implementation=_Obj))
+             DropMessage=DropMessage, DelayMessageBySequence=DelayMessageBySequence,
+             Message=_Obj(Implementation=_Obj), defaultdict=collections.defaultdict,
+             SyncDistribution=_Obj(Implementation=_Dist), FullSyncDistribution=FullSync, LastSyncDistribution=LastSync,
+             MemberAuthentication=_Obj(Implementation=_Auth), DoubleMemberAuthentication=_DoubleAuth)
     funcs = {}
     for node in cls.body:
         if isinstance(node, ast.FunctionDef) and node.name in LIFT:
@@ -62,9 +69,48 @@ class DropMessage(object):
         self.dropped, self.reason = message, reason
 
 
+class DelayMessageBySequence(object):
+    """message.py:147-166."""
+
+    def __init__(self, delayed, missing_low, missing_high):
+        assert 0 < missing_low <= missing_high, (missing_low, missing_high)
+        self.delayed, self.missing_low, self.missing_high = delayed, missing_low, missing_high
+
+
+# stand-ins for the isinstance checks of _store (dispersy.py:1497-1567)
+class _Dist(object):
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+class FullSync(object):
+    pass
+
+
+class LastSync(object):
+    def __init__(self, history_size, custom_callback=None):
+        self.history_size, self.custom_callback = history_size, custom_callback
+
+
+class _Auth(object):
+    encoding = "bin"
+    is_signed = True
+
+    def __init__(self, member):
+        self.member = member
+
+
+class _DoubleAuth(object):
+    class Implementation(object):
+        pass
+
+
 class _Cursor(object):
     def __init__(self, cur):
         self.cur = cur
+
+    def __iter__(self):  # list(execute(...)) (dispersy.py:1571-1586)
+        return iter(self.cur.fetchall())
 
     def next(self):  # py2 iterator protocol the reference calls (dispersy.py:868)
         row = self.cur.fetchone()
@@ -77,8 +123,12 @@ class _DB(object):
     def __init__(self, conn):
         self.conn = conn
 
-    def execute(self, sql, args=()):
-        return _Cursor(self.conn.execute(sql, args))
+    def execute(self, sql, args=(), get_lastrowid=False):
+        cur = self.conn.execute(sql, args)
+        return cur.lastrowid if get_lastrowid else _Cursor(cur)
+
+    def executemany(self, sql, seq):
+        self.conn.executemany(sql, list(seq))
 
 
 class _Log(object):
@@ -95,6 +145,7 @@ class StubDispersy(object):
         self.sent = []
         self._is_duplicate_sync_message = funcs["_is_duplicate_sync_message"].__get__(self)
         self.check = funcs["_check_full_sync_distribution_batch"].__get__(self)
+        self.store = funcs["_store"].__get__(self)
 
     def _send_packets(self, candidates, packets, community, reason):
         for c in candidates:
@@ -178,5 +229,191 @@ def main():
         len(results), sum(1 for _, r in results if r is None), len(d.sent), len(changed)))
 
 
+def _table(conn):
+    return [list(r) for r in conn.execute("SELECT id, member, global_time, meta_message, undone, hex(packet), sequence "
+                                          "FROM sync ORDER BY id")]
+
+
+def seq_main():
+    """The sequence-number branch of _check_full_sync_distribution_batch (dispersy.py:954-1037): per-member highest
+    (global_time, sequence), duplicates by binary packet, conflicting sequence numbers (keep ours and send it back, or
+    DELETE ours and everything after it), gaps (DelayMessageBySequence), lower global time with a higher sequence
+    number, and the duplicate lookup by (member, global_time)."""
+    rng = np.random.Generator(np.random.PCG64(777))
+    sig, gt_now, inactive = 60, 4000, 3500
+    conn = sqlite3.connect(":memory:")
+    conn.executescript(reference_schema())
+    rows, used = [], set()
+
+    def fresh_gt(member, lo=1, hi=gt_now):
+        while True:
+            gt = int(rng.integers(lo, hi))
+            if (member, gt) not in used:
+                used.add((member, gt))
+                return gt
+
+    # meta 1: plain rows (sequence NULL); meta 2: sequence-numbered rows 1..c per member in global-time order
+    for member in range(1, 31):
+        for _ in range(int(rng.integers(0, 4))):
+            gt = fresh_gt(member)
+            rows.append(dict(member=member, gt=gt, meta=1, seq=None))
+        gts = sorted(fresh_gt(member, 1, gt_now - 600) for _ in range(int(rng.integers(0, 9))))
+        for j, gt in enumerate(gts):
+            rows.append(dict(member=member, gt=gt, meta=2, seq=j + 1))
+    for i, r in enumerate(rows):
+        r["id"] = i + 1
+        r["packet"] = (r["id"].to_bytes(4, "big") + rng.bytes(int(rng.integers(sig + 8, 200)) - 4))
+    conn.executemany("INSERT INTO sync (id, community, member, global_time, meta_message, undone, packet, sequence) "
+                     "VALUES (?, 1, ?, ?, ?, 0, ?, ?)",
+                     [(r["id"], r["member"], r["gt"], r["meta"], r["packet"], r["seq"]) for r in rows])
+    community = _Obj(database_id=1, acceptable_global_time=gt_now + 10000, global_time=gt_now)
+    meta = _Obj(distribution=_Obj(enable_sequence_number=True))
+    d = StubDispersy(conn, lift())
+    table0 = _table(conn)
+    batches, idx = [], 0
+    for bno in range(40):
+        seq_rows = {}
+        for rid, member, gt, mid, _, phex, seq in _table(conn):
+            if mid == 2:
+                seq_rows.setdefault(member, []).append(dict(gt=gt, seq=seq, packet=bytes.fromhex(phex)))
+        for v in seq_rows.values():
+            v.sort(key=lambda r: r["gt"])
+        plain = {}
+        for rid, member, gt, mid, *_ in _table(conn):
+            if mid == 1:
+                plain.setdefault(member, []).append(gt)
+        batch = []
+        for j in range(int(rng.integers(4, 30))):
+            member = int(rng.integers(1, 36))  # 31..35: members without stored rows
+            mine = seq_rows.get(member, [])
+            c = len(mine)
+            kind = int(rng.integers(0, 10))
+            seq, gt, packet = c + 1, None, rng.bytes(int(rng.integers(80, 160)))
+            if kind == 0 and c:                      # binary duplicate of a stored sequence number
+                r = mine[int(rng.integers(0, c))]
+                seq, gt, packet = r["seq"], r["gt"], r["packet"]
+            elif kind == 1 and c:                    # same sequence number, different message: (gt, packet) higher
+                r = mine[int(rng.integers(0, c))]
+                seq, gt = r["seq"], r["gt"] + int(rng.integers(0, 3))
+                if gt == r["gt"]:
+                    packet = r["packet"][:sig] + bytes([255]) + rng.bytes(20)
+            elif kind == 2 and c:                    # same sequence number, (gt, packet) lower: ours and later go
+                r = mine[int(rng.integers(0, c))]
+                seq, gt = r["seq"], max(1, r["gt"] - int(rng.integers(1, 40)))
+            elif kind == 3:                          # a gap: delayed
+                seq = c + int(rng.integers(2, 5))
+            elif kind == 4 and c:                    # next sequence number but an older global time
+                gt = max(1, mine[-1]["gt"] - int(rng.integers(0, 50)))
+            elif kind == 5 and plain.get(member):    # next sequence number at the (member, gt) of a plain row
+                gt = plain[member][0]
+            elif kind == 6:                          # beyond the acceptable global time
+                gt = gt_now + 10001 + int(rng.integers(0, 9))
+            elif kind == 7:                          # inactive (pruned)
+                gt = int(rng.integers(1, max(2, gt_now - inactive)))
+            if gt is None:
+                top = mine[-1]["gt"] if c else 0
+                gt = int(rng.integers(top + 1, gt_now + 200))
+            batch.append(dict(index=idx, member=member, gt=int(gt), seq=int(seq), packet=bytes(packet).hex()))
+            idx += 1
+        messages = []
+        for b in batch:
+            active = gt_now - b["gt"] < inactive
+            messages.append(_Obj(index=b["index"], name="seq-sync", community=community, meta=meta, database_id=2,
+                                 packet=bytes.fromhex(b["packet"]), candidate="c%d" % b["index"],
+                                 authentication=_Obj(member=_Obj(database_id=b["member"], signature_length=sig)),
+                                 distribution=_Obj(global_time=b["gt"], sequence_number=b["seq"],
+                                                   pruning=_Obj(is_active=lambda a=active: a))))
+        d.sent = []
+        results, ended = [], False
+        gen = d.check(messages)
+        while True:
+            try:
+                out = next(gen)
+            except StopIteration:
+                break
+            except RuntimeError as e:
+                # py2: a StopIteration inside a generator ends it silently (the `.next()` of a LIMIT 1 OFFSET query
+                # that finds no row, dispersy.py:986-987); py3 turns that into this RuntimeError (PEP 479)
+                assert isinstance(e.__cause__, StopIteration), e
+                ended = True
+                break
+            if isinstance(out, DropMessage):
+                results.append([out.dropped.index, out.reason])
+            elif isinstance(out, DelayMessageBySequence):
+                results.append([out.delayed.index, ["delay", out.missing_low, out.missing_high]])
+            else:
+                results.append([out.index, None])
+        batches.append(dict(batch=batch, results=results, ended_early=ended, sent=d.sent, table_after=_table(conn)))
+    out = dict(signature_length=sig, global_time=gt_now, acceptable_global_time=gt_now + 10000, inactive=inactive,
+               table_before=table0, batches=batches)
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "dedup_seq_vectors.json"), "w") as f:
+        json.dump(out, f, separators=(",", ":"))
+    kinds = collections.Counter(r if r is None or isinstance(r, str) else r[0]
+                                for b in batches for _, r in b["results"])
+    print("seq vectors: %d batches, %d ended early, %d rows deleted" % (
+        len(batches), sum(b["ended_early"] for b in batches), len(table0) - len(batches[-1]["table_after"])),
+        dict(kinds))
+
+
+def laststore_main():
+    """_store (dispersy.py:1475-1612) for a LastSyncDistribution meta: INSERT, then DELETE every member's rows
+    beyond the newest history_size (by global time, :1581-1591); batches in sequence, the table after each."""
+    rng = np.random.Generator(np.random.PCG64(909))
+    conn = sqlite3.connect(":memory:")
+    conn.executescript(reference_schema())
+    used = set()
+    n0 = 0
+    for member in range(1, 25):
+        for gt in sorted(rng.choice(np.arange(1, 500), size=int(rng.integers(0, 3)), replace=False).tolist()):
+            n0 += 1
+            used.add((member, gt))
+            conn.execute("INSERT INTO sync (id, community, member, global_time, meta_message, undone, packet) "
+                         "VALUES (?, 1, ?, ?, 3, 0, ?)", (n0, member, gt, rng.bytes(40)))
+    stored = []
+
+    class Community(object):
+        database_id = 1
+
+        def update_global_time(self, gt):
+            stored.append(["update_global_time", gt])
+
+        def dispersy_store(self, messages):
+            stored.append(["dispersy_store", [m.index for m in messages]])
+
+    community = Community()
+    meta = _Obj(name="last", community=community, database_id=3, authentication=_Obj(),
+                distribution=LastSync(history_size=2))
+    d = StubDispersy(conn, lift())
+    initial = _table(conn)
+    steps, idx = [], 0
+    for b in range(12):
+        msgs, members = [], set()
+        for _ in range(int(rng.integers(1, 12))):
+            member = int(rng.integers(1, 30))
+            gt = int(rng.integers(1, 1000))
+            if (member, gt) in used:
+                continue
+            used.add((member, gt))
+            packet = rng.bytes(int(rng.integers(30, 90))) + b"\x01"
+            m = _Obj(index=idx, name="last", community=community, meta=meta, database_id=3, packet=packet,
+                     authentication=_Auth(_Obj(database_id=member, has_identity=lambda c: True)),
+                     distribution=_Dist(global_time=gt))
+            idx += 1
+            msgs.append(m)
+        if not msgs:
+            continue
+        stored.clear()
+        d.store(msgs)
+        steps.append(dict(messages=[dict(index=m.index, member=m.authentication.member.database_id,
+                                         gt=m.distribution.global_time, packet=m.packet.hex()) for m in msgs],
+                          packet_ids=[m.packet_id for m in msgs], calls=list(stored), table=_table(conn)))
+    out = dict(history_size=2, meta=3, initial_table=initial, steps=steps)
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "laststore_vectors.json"), "w") as f:
+        json.dump(out, f, separators=(",", ":"))
+    print("laststore vectors: %d batches, table %d -> %d rows" % (len(steps), len(initial), len(steps[-1]["table"])))
+
+
 if __name__ == "__main__":
     main()
+    seq_main()
+    laststore_main()

@@ -1,0 +1,160 @@
+"""The sequence-number branch of _check_full_sync_distribution_batch (dispersy.py:954-1037) and LastSyncDistribution's
+history pruning in _store (:1558-1591), against the reference's own methods lifted from dispersy.py's AST
+(tests/golden/gen_dedup_golden.py: dedup_seq_vectors.json -- 40 batches replayed on one table, with the DELETEs of
+conflicting sequence numbers and the py2 generator cut-off --, laststore_vectors.json -- 12 _store batches with
+history_size 2).
+
+CPU: the oracle restatement (oracle/sync_ref.check_sequence_batch / store_last_sync over sqlite3) replays them.
+GPU: SyncCommunity does -- the (member, global_time) lookups as one dsy_dup_check per batch, the DELETEs through
+dsy_store_delete -- and the responder's index and the duplicate table follow the table after every batch."""
+import sqlite3
+
+import numpy as np
+import pytest
+
+from dispersy_amd.community import DelayMessageBySequence, DropMessage, SyncCommunity
+from dispersy_amd.distribution import FullSyncDistribution, GlobalTimePruning, LastSyncDistribution, MetaMessage
+from dispersy_amd.store import SyncStore
+from golden_util import load
+from oracle import sync_ref
+
+SEQ = load("dedup_seq_vectors.json")
+LAST = load("laststore_vectors.json")
+
+
+def sqlite_of(table):
+    conn = sqlite3.connect(":memory:")
+    conn.executescript(sync_ref.SYNC_SCHEMA)
+    conn.executemany("INSERT INTO sync (id, community, member, global_time, meta_message, undone, packet, sequence) "
+                     "VALUES (?, 1, ?, ?, ?, ?, ?, ?)",
+                     [(i, mem, gt, meta, und, bytes.fromhex(p), sq) for i, mem, gt, meta, und, p, sq in table])
+    return conn
+
+
+def table_of(conn):
+    return [list(r) for r in conn.execute("SELECT id, member, global_time, meta_message, undone, hex(packet), sequence "
+                                          "FROM sync ORDER BY id")]
+
+
+def _expect(r):
+    return tuple(r) if isinstance(r, list) else r
+
+
+def test_oracle_sequence_branch_matches_reference():
+    conn = sqlite_of(SEQ["table_before"])
+    assert sum(b["ended_early"] for b in SEQ["batches"]) > 5
+    for b in SEQ["batches"]:
+        msgs = [dict(member=m["member"], gt=m["gt"], seq=m["seq"], packet=bytes.fromhex(m["packet"]),
+                     signature_length=SEQ["signature_length"], inactive=SEQ["inactive"], index=m["index"])
+                for m in b["batch"]]
+        out, sends, ended = sync_ref.check_sequence_batch(conn, 1, 2, msgs, SEQ["acceptable_global_time"],
+                                                          SEQ["global_time"])
+        assert [(i, _expect(r)) for i, r in out] == [(i, _expect(r)) for i, r in b["results"]]
+        assert ended == b["ended_early"]
+        assert [["c%d" % i, p.hex()] for i, p in sends] == [s[:2] for s in b["sent"]]
+        assert table_of(conn) == b["table_after"]
+
+
+def test_oracle_last_sync_store_matches_reference():
+    conn = sqlite_of(LAST["initial_table"])
+    for step in LAST["steps"]:
+        ids = sync_ref.store_last_sync(conn, 1, LAST["meta"], LAST["history_size"],
+                                       [(m["member"], m["gt"], bytes.fromhex(m["packet"])) for m in step["messages"]])
+        assert ids == step["packet_ids"]
+        assert table_of(conn) == step["table"]
+
+
+# ------------------------------------------------------------------------------------------------- GPU
+class _Member(object):
+    def __init__(self, database_id, signature_length):
+        self.database_id, self.signature_length = database_id, signature_length
+
+
+class _Auth(object):
+    def __init__(self, member):
+        self.member = member
+
+
+class _Dist(object):
+    def __init__(self, gt, seq=0):
+        self.global_time, self.sequence_number, self.priority = gt, seq, 128
+
+
+class _Msg(object):
+    def __init__(self, meta, member, gt, packet, index, seq=0, sig=60):
+        self.meta, self.database_id = meta, meta.database_id
+        self.authentication = _Auth(_Member(member, sig))
+        self.distribution = _Dist(gt, seq)
+        self.packet, self.index, self.candidate = packet, index, "c%d" % index
+
+
+def store_of(table):
+    return SyncStore.from_rows([(i, gt, meta, und, bytes.fromhex(p), mem, sq or 0)
+                                for i, mem, gt, meta, und, p, sq in table])
+
+
+def alive(store):
+    keep = np.flatnonzero(~store.deleted)
+    return sorted((int(store.rowid[r]), store.packet(int(r)).hex().upper()) for r in keep)
+
+
+@pytest.mark.gpu
+def test_sequence_branch_matches_reference():
+    store = store_of(SEQ["table_before"])
+    seq_meta = MetaMessage("seq", 2, FullSyncDistribution("ASC", 128, True,
+                                                          GlobalTimePruning(SEQ["inactive"], SEQ["inactive"] + 1)))
+    plain = MetaMessage("plain", 1, FullSyncDistribution("ASC", 128))
+    com = SyncCommunity(store, [plain, seq_meta], global_time=SEQ["global_time"],
+                        signature_length=SEQ["signature_length"])
+    assert com.acceptable_global_time == SEQ["acceptable_global_time"]
+    for b in SEQ["batches"]:
+        msgs = [_Msg(seq_meta, m["member"], m["gt"], bytes.fromhex(m["packet"]), m["index"], m["seq"])
+                for m in b["batch"]]
+        com.sent_packets = []
+        got = []
+        for out in com._check_full_sync_distribution_batch(msgs):
+            if isinstance(out, DropMessage):
+                got.append((out.dropped.index, out.reason))
+            elif isinstance(out, DelayMessageBySequence):
+                got.append((out.delayed.index, ("delay", out.missing_low, out.missing_high)))
+            else:
+                got.append((out.index, None))
+        assert got == [(i, _expect(r)) for i, r in b["results"]]
+        assert [[c, p.hex(), why] for c, p, why in com.sent_packets] == b["sent"]
+        assert alive(store) == sorted((r[0], r[5]) for r in b["table_after"])
+    # the responder's index and the duplicate table after the DELETEs: every remaining (member, gt) is found,
+    # every deleted one is not
+    gone = np.flatnonzero(store.deleted)
+    assert len(gone) > 20
+    keep = np.flatnonzero(~store.deleted)
+    probe = np.concatenate([gone, keep[:200]])
+    verdict, _ = store.dup_check(store.member[probe], store.global_time[probe], [b"?"] * len(probe), [60] * len(probe))
+    assert (verdict[:len(gone)] == 0).all() and (verdict[len(gone):] != 0).all()
+    for m in (1, 2):
+        assert set(store.rowid[store.live_rows(m)].tolist()) == {r[0] for r in SEQ["batches"][-1]["table_after"]
+                                                               if r[3] == m and r[4] == 0}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lazy", [False, True])
+def test_last_sync_history_matches_reference(lazy):
+    store = store_of(LAST["initial_table"])
+    if not lazy:
+        store.handle  # noqa: B018 -- the DELETEs then run on the device index
+    meta = MetaMessage("last", LAST["meta"], LastSyncDistribution("ASC", 128, LAST["history_size"]))
+    com = SyncCommunity(store, [meta], global_time=1)
+    for step in LAST["steps"]:
+        msgs = [_Msg(meta, m["member"], m["gt"], bytes.fromhex(m["packet"]), m["index"]) for m in step["messages"]]
+        rows = com.store_messages(msgs)
+        assert store.rowid[rows].tolist() == step["packet_ids"]
+        assert alive(store) == sorted((r[0], r[5]) for r in step["table"])
+        assert com.global_time == max([1] + [m["gt"] for s in LAST["steps"][:LAST["steps"].index(step) + 1]
+                                             for m in s["messages"]])
+    want = sorted(r[0] for r in LAST["steps"][-1]["table"])
+    assert sorted(store.rowid[store.live_rows(LAST["meta"])].tolist()) == want
+    # the device index: a claim over everything with an empty filter returns exactly the kept rows
+    from dispersy_amd import BloomFilter
+    from dispersy_amd.community import ClaimRequest
+    (got,) = com.respond([ClaimRequest(1, 10 ** 6, 1, 0, BloomFilter(1024, 0.01, b"\x00"))], include_inactive=True,
+                         byte_limit=1 << 40)
+    assert sorted(store.rowid[got].tolist()) == want
