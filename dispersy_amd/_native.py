@@ -13,7 +13,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DSY_LIB", os.path.join(_HERE, "libdsybloom.so"))
 
-DSY_OK, DSY_EINVAL, DSY_EHIP, DSY_ENOMEM, DSY_ECAPACITY, DSY_EUNSORTED = 0, -1, -2, -3, -4, -5
+DSY_OK, DSY_EINVAL, DSY_EHIP, DSY_ENOMEM, DSY_ECAPACITY, DSY_EUNSORTED, DSY_EEMPTY = 0, -1, -2, -3, -4, -5, -6
 DSY_MD5, DSY_SHA1, DSY_SHA256, DSY_SHA384, DSY_SHA512 = range(5)
 HASH_KINDS = {"md5": DSY_MD5, "sha1": DSY_SHA1, "sha256": DSY_SHA256, "sha384": DSY_SHA384, "sha512": DSY_SHA512}
 DSY_ASC, DSY_DESC, DSY_RANDOM = 0, 1, 2
@@ -92,6 +92,7 @@ SIGNATURES = {
     "dsy_store_replace": (ctypes.c_int, [_P, _P, _P, _P, _U64, _P, _U64]),
     "dsy_bloom_add_rows": (ctypes.c_int, [_P, ctypes.POINTER(BloomParams), _P, _P, _U64, _P]),
     "dsy_claim_modulo": (ctypes.c_int, [_P, ctypes.POINTER(BloomParams), _P, _P, _U32, _U64, _U64, _P, _PU64]),
+    "dsy_claim_largest": (ctypes.c_int, [_P, ctypes.POINTER(BloomParams), _P, _P, _U32, _U64, _U64, _U64, _U64, _P, _P]),
     "dsy_sync_respond": (ctypes.c_int, [_P, _P, ctypes.POINTER(Request), _U32, _P, _U64, ctypes.POINTER(Meta), _U32,
                                         _U64, ctypes.c_int, ctypes.c_int64, _U64, _P, _U64, _P]),
     "dsy_sync_respond_dev": (ctypes.c_int, [_P, _P, ctypes.POINTER(Request), _U32, _P, ctypes.POINTER(Meta), _U32,

@@ -162,6 +162,23 @@ class BloomFilter(object):
         self._raw[:] = buf.raw
         return count.value
 
+    def claim_largest(self, store, meta_ids, from_gbtime, capacity, nrsyncpackets, acceptable_global_time):
+        """The largest claim strategy's selection and add_keys on the device (dsy_claim_largest, community.py:783-830
+        after the random draws): returns (time_low, time_high, rows added, nrsyncpackets after); rows added 0 means
+        the empty claim.  IndexError where the reference raises it (community.py:857)."""
+        ids = np.ascontiguousarray(meta_ids, dtype=np.uint32)
+        ctx = store.ctx
+        buf = ctypes.create_string_buffer(bytes(self._raw), len(self._raw))
+        out = (ctypes.c_uint64 * 4)()
+        rc = ctx.lib.dsy_claim_largest(ctx.handle, ctypes.byref(self.params), store.handle, ids.ctypes.data, len(ids),
+                                       int(from_gbtime), int(capacity), int(nrsyncpackets), int(acceptable_global_time),
+                                       buf, out)
+        if rc == _native.DSY_EEMPTY:
+            raise IndexError("list index out of range")
+        _native.check(rc)
+        self._raw[:] = buf.raw
+        return int(out[0]), int(out[1]), int(out[2]), int(out[3])
+
     def clear(self):
         """Set all bits in the filter to zero (bloomfilter.py:196-200)."""
         self._raw[:] = bytes(len(self._raw))

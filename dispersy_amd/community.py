@@ -11,10 +11,9 @@ Kept (same names, argument meaning, return values and statistics):
 and the overridable properties of community.py:599-678, :935-941 (the reference's plugin hooks).
 
 The responder runs as ONE batched call into the HIP library (`respond`): selection, prefix-salted digest, probe
-and byte-limited compaction for every claim of a receive batch.  The claim side's largest strategy selects its
-packet range on the host from the store's index columns (the reference does this in SQLite) and builds the filter on
-the GPU from the store rows already in HBM; the modulo strategy selects and hashes on the device in one call
-(dsy_claim_modulo).
+and byte-limited compaction for every claim of a receive batch.  Both claim strategies select and hash on the device in
+one call each, over the store's live index in HBM: dsy_claim_largest (the pivot ranges of _select_bloomfilter_range /
+_select_and_fix) and dsy_claim_modulo (the residue class).
 """
 import ctypes
 import random as _random_module
@@ -486,30 +485,17 @@ class SyncCommunity(object):
         if from_gbtime < 1:
             from_gbtime = int(self._random.random() * self.global_time)
 
-        if from_gbtime > 1 and self._nrsyncpackets >= capacity:
-            right, rightdata = self._select_bloomfilter_range(request_cache, syncable, from_gbtime - 1, capacity, True)
-            if right[2] == capacity:
-                left, leftdata = self._select_bloomfilter_range(request_cache, syncable, from_gbtime + 1, capacity, False)
-                left_range = (left[1] or self.global_time) - left[0]
-                right_range = (right[1] or self.global_time) - right[0]
-                bloomfilter_range, data = (left, leftdata) if left_range > right_range else (right, rightdata)
-            else:
-                bloomfilter_range, data = right, rightdata
-        else:
-            bloomfilter_range = [1, acceptable_global_time]
-            data, fixed = self._select_and_fix(request_cache, syncable, 0, capacity, True)
-            if len(data) > 0 and fixed:
-                bloomfilter_range[1] = data[-1][0]
-                self._nrsyncpackets = capacity + 1
-
-        if len(data) > 0:
-            bloom.add_store_rows(self._store, [row for _, row in data])
-            return (min(bloomfilter_range[0], acceptable_global_time),
-                    min(bloomfilter_range[1], acceptable_global_time), 1, 0, bloom)
+        # the range selection (_select_bloomfilter_range / _select_and_fix, :783-815) and add_keys (:821) run on the
+        # device over the store's live index, in one call
+        time_low, time_high, added, self._nrsyncpackets = bloom.claim_largest(
+            self._store, syncable, from_gbtime, capacity, self._nrsyncpackets, acceptable_global_time)
+        if added:
+            return (time_low, time_high, 1, 0, bloom)
         return self._empty_claim(acceptable_global_time)
 
     def _select_bloomfilter_range(self, request_cache, syncable, global_time, to_select, higher=True):
-        """community.py:839-879."""
+        """community.py:839-879 over the host index columns (the strategy itself uses the device form,
+        dsy_claim_largest; this mirror keeps the reference's method for callers and tests)."""
         data, fixed = self._select_and_fix(request_cache, syncable, global_time, to_select, higher)
         lowerfixed = higherfixed = True
         if len(data) < to_select:

@@ -1232,6 +1232,189 @@ int dsy_claim_modulo(dsy_ctx* c, const dsy_bloom_params* p, const dsy_store* s, 
     return DSY_OK;
 }
 
+// ------------------------------------------------------------------------------- claim, largest strategy
+namespace {
+
+struct SelData {      // one _select_and_fix result: the rows are spans[J] of the live index (device), ascending gt
+    uint64_t count = 0, first_gt = 0, last_gt = 0;
+    bool fixed = false;
+    uint64_t* d_spans = nullptr;
+};
+
+struct ClaimCtx {
+    dsy_ctx* c;
+    const dsy_store* s;
+    uint64_t* d_segs;     // J x (a, b)
+    uint32_t J;
+    uint64_t* d_cand;     // J x (capacity + 2) scratch
+    uint64_t* d_spans;    // 4 x J x 2: one span set per select call
+    SelResult* d_res;     // 4 results
+    int calls = 0;
+};
+
+int select_and_fix_dev(ClaimCtx& k, uint64_t pivot, uint64_t to_select, bool higher, SelData* out) {
+    dsy_ctx* c = k.c;
+    const int i = k.calls++;
+    out->d_spans = k.d_spans + (size_t)i * k.J * 2;
+    HIP_TRY(launch_select_and_fix(k.s->d_live_gt, k.d_segs, k.J, pivot, to_select, higher ? 1 : 0, k.d_cand,
+                                  out->d_spans, k.d_res + i, c->stream));
+    SelResult r;
+    HIP_TRY(hipMemcpyAsync(&r, k.d_res + i, sizeof r, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    out->count = r.count;
+    out->first_gt = r.first_gt;
+    out->last_gt = r.last_gt;
+    out->fixed = r.fixed != 0;
+    return DSY_OK;
+}
+
+struct RangeData {    // _select_bloomfilter_range's result: [lo, hi, count] and the (one or two) span sets
+    uint64_t lo = 0, hi = 0, count = 0;
+    std::vector<uint64_t*> spans;
+};
+
+// community.py:839-879 (IndexError when no row is selected: DSY_EEMPTY)
+int select_range_dev(ClaimCtx& k, uint64_t gt, uint64_t to_select, bool higher, uint64_t acceptable, RangeData* out) {
+    SelData data, more;
+    int rc = select_and_fix_dev(k, gt, to_select, higher, &data);
+    if (rc) return rc;
+    bool lowerfixed = true, higherfixed = true;
+    bool have_more = false;
+    if (data.count < to_select) {
+        const uint64_t remain = to_select - data.count;
+        if (remain > 25) {
+            if ((rc = select_and_fix_dev(k, higher ? gt + 1 : gt - 1, remain, !higher, &more))) return rc;
+            have_more = true;
+            (higher ? lowerfixed : higherfixed) = more.fixed;
+        }
+    }
+    const uint64_t n = data.count + (have_more ? more.count : 0);
+    if (n == 0) return fail(DSY_EEMPTY, "no rows around global time %llu (community.py:857 raises IndexError)",
+                            (unsigned long long)gt);
+    // data[0] / data[-1]: `more` comes before data (higher: lowerdata + data) or after it (data + higherdata)
+    uint64_t first, last;
+    if (higher) {
+        first = have_more && more.count ? more.first_gt : data.first_gt;
+        last = data.count ? data.last_gt : more.last_gt;
+    } else {
+        first = data.count ? data.first_gt : more.first_gt;
+        last = have_more && more.count ? more.last_gt : data.last_gt;
+    }
+    uint64_t lo = first, hi = last;
+    if (higher) {
+        lo = std::min(lo, gt + 1);
+        if (!data.fixed) hi = acceptable;
+        if (!lowerfixed) lo = 1;
+    } else {
+        hi = std::max(hi, gt - 1);
+        if (!data.fixed) lo = 1;
+        if (!higherfixed) hi = acceptable;
+    }
+    out->lo = lo;
+    out->hi = hi;
+    out->count = n;
+    out->spans.push_back(data.d_spans);
+    if (have_more) out->spans.push_back(more.d_spans);
+    return DSY_OK;
+}
+
+}  // namespace
+
+int dsy_claim_largest(dsy_ctx* c, const dsy_bloom_params* p, const dsy_store* s, const uint32_t* meta_ids,
+                      uint32_t nmeta, uint64_t from_gbtime, uint64_t capacity, uint64_t nrsyncpackets,
+                      uint64_t acceptable_global_time, uint8_t* filter_inout, uint64_t* out_claim) {
+    if (!c || !s || !filter_inout || !out_claim || (nmeta && !meta_ids)) return fail(DSY_EINVAL, "NULL argument");
+    if (s->ctx != c) return fail(DSY_EINVAL, "store belongs to another context");
+    if (capacity == 0) return fail(DSY_EINVAL, "capacity must be positive");
+    int rc = check_params(p);
+    if (rc) return rc;
+    // the syncable metas' live segments (`meta_message IN (...)`: each id once)
+    std::vector<uint32_t> ids(meta_ids, meta_ids + nmeta);
+    std::sort(ids.begin(), ids.end());
+    ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
+    std::vector<uint64_t> segs;
+    for (uint32_t id : ids) {
+        auto it = s->segs.find(id);
+        if (it == s->segs.end() || it->second.first >= it->second.second) continue;
+        segs.push_back(it->second.first);
+        segs.push_back(it->second.second);
+    }
+    const uint32_t J = (uint32_t)(segs.size() / 2);
+    Guard g(c);
+    out_claim[0] = out_claim[1] = out_claim[2] = 0;
+    out_claim[3] = nrsyncpackets;
+    const size_t b_segs = (size_t)J * 16, b_cand = (size_t)J * (capacity + 2) * 8, b_spans = (size_t)4 * J * 16,
+                 b_res = 4 * sizeof(SelResult);
+    void* d;
+    if ((rc = ws_get(c, "claim_largest", b_segs + b_cand + b_spans + b_res, &d))) return rc;
+    uint8_t* q = (uint8_t*)d;
+    ClaimCtx k{c, s, (uint64_t*)q, J, (uint64_t*)(q + b_segs), (uint64_t*)(q + b_segs + b_cand),
+               (SelResult*)(q + b_segs + b_cand + b_spans)};
+    HIP_TRY(hipMemcpyAsync(k.d_segs, segs.data(), b_segs, hipMemcpyHostToDevice, c->stream));
+    // community.py:783-830, after the random draws (the caller passes from_gbtime)
+    RangeData chosen;
+    std::vector<uint64_t*> spans;
+    uint64_t lo, hi, count;
+    if (from_gbtime > 1 && nrsyncpackets >= capacity) {
+        RangeData right;
+        if ((rc = select_range_dev(k, from_gbtime - 1, capacity, true, acceptable_global_time, &right))) return rc;
+        if (right.count == capacity) {
+            RangeData left;
+            if ((rc = select_range_dev(k, from_gbtime + 1, capacity, false, acceptable_global_time, &left))) return rc;
+            // `(left[1] or self.global_time) - left[0]`: the bounds are >= 1 here, so the `or` never applies
+            const int64_t left_range = (int64_t)left.hi - (int64_t)left.lo, right_range = (int64_t)right.hi - (int64_t)right.lo;
+            chosen = left_range > right_range ? left : right;
+        } else {
+            chosen = right;
+        }
+        lo = chosen.lo;
+        hi = chosen.hi;
+        count = chosen.count;
+        spans = chosen.spans;
+    } else {
+        SelData data;
+        if ((rc = select_and_fix_dev(k, 0, capacity, true, &data))) return rc;
+        lo = 1;
+        hi = acceptable_global_time;
+        if (data.count && data.fixed) {
+            hi = data.last_gt;
+            out_claim[3] = capacity + 1;
+        }
+        count = data.count;
+        spans.push_back(data.d_spans);
+    }
+    if (count == 0) return DSY_OK;  // the empty claim
+    // add_keys over the selected rows (community.py:821), hashed from the store's line copy
+    void* dr;
+    if ((rc = ws_get(c, "rows", (count + 1) * 8, &dr))) return rc;
+    uint64_t at = 0;
+    for (uint64_t* sp : spans) {
+        // one span set's rows, after the previous set's: compact copy of J spans
+        HIP_TRY(launch_span_rows(s->d_live_row, sp, J, (uint64_t*)dr + at, c->stream));
+        std::vector<uint64_t> h(2 * J);
+        HIP_TRY(hipMemcpyAsync(h.data(), sp, 16 * J, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        for (uint32_t j = 0; j < J; ++j) at += h[2 * j + 1] - h[2 * j];
+    }
+    if (at != count) return fail(DSY_EHIP, "claim selection: %llu rows gathered, %llu selected", (unsigned long long)at,
+                                 (unsigned long long)count);
+    const uint64_t nbytes = p->m_bits / 8, words = filter_words(p->m_bits);
+    void* df;
+    if ((rc = ws_get(c, "filter", words * 4, &df))) return rc;
+    HIP_TRY(hipMemsetAsync(df, 0, words * 4, c->stream));
+    HIP_TRY(hipMemcpyAsync(df, filter_inout, nbytes, hipMemcpyHostToDevice, c->stream));
+    if ((rc = run_bloom(c, BloomOp::Add, p, s->d_lines, nullptr, (uint64_t*)dr, count, (uint32_t*)df, nullptr, nullptr,
+                        s->d_rec)))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(filter_inout, df, nbytes, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    timers_collect_lazy(c);
+    out_claim[0] = std::min(lo, acceptable_global_time);
+    out_claim[1] = std::min(hi, acceptable_global_time);
+    out_claim[2] = count;
+    return DSY_OK;
+}
+
 // -------------------------------------------------------------------------------------------- responder
 // The window pool holds kWindow pairs per claim of the call, and at least kMinSlots claims' worth (16 M pairs,
 // 400 MB of workspace); each window the active claims share it evenly, from kWindow up to kMaxWindow pairs each.

@@ -225,6 +225,26 @@ hipError_t launch_live_cut(const uint64_t* live_gt, const uint64_t* live_row, ui
 hipError_t launch_claim_modulo(const uint64_t* live_gt, const uint64_t* live_row, uint64_t a, uint64_t b,
                                uint64_t offset, uint64_t modulo, uint64_t* out_rows, uint64_t cap,
                                unsigned long long* count, uint32_t max_grid, hipStream_t stream);
+// Claim side, largest strategy: _select_and_fix (community.py:881-903) over the live segments of the syncable metas:
+// up to to_select + 1 rows strictly above (higher) / below the pivot in global-time order across the metas; when
+// over-full, the trailing equal-global-time group is dropped.  The result is a global-time interval: per meta the
+// selected live-index span out_spans[2j .. 2j+1], and the counts below.  cand: scratch of J x (to_select + 1) u64
+// (candidates ranked in it when the metas are more than one); cand_lds != 0: it fits LDS (dynamic shared memory).
+struct SelResult {
+    uint64_t count;     // rows selected (len(data))
+    uint64_t first_gt;  // data[0] global time (ascending order), valid when count > 0
+    uint64_t last_gt;   // data[-1] global time
+    uint64_t total;     // candidates on the pivot's side
+    uint32_t fixed;     // the selection was over-full (and the trailing group dropped)
+    uint32_t pad;
+};
+hipError_t launch_select_and_fix(const uint64_t* live_gt, const uint64_t* spans, uint32_t J, uint64_t pivot,
+                                 uint64_t to_select, int higher, uint64_t* cand, uint64_t* out_spans, SelResult* res,
+                                 hipStream_t stream);
+// rows of live-index spans (n_spans x (x, y)) -> out_rows, in span order; *total rows
+hipError_t launch_span_rows(const uint64_t* live_row, const uint64_t* spans, uint32_t n_spans, uint64_t* out_rows,
+                            hipStream_t stream);
+
 // DELETE of arbitrary rows (dsy_store_delete): del_bits marks store rows; the live index loses every entry whose row is
 // marked, stable.  Tiles of kDelTile entries: per-tile kept counts -> exclusive scan -> scatter; bounds[nb] (positions in
 // the old index, ascending or not) are mapped to their positions in the new one.  d_tmp: (tiles + 1) u64 + 64 B.

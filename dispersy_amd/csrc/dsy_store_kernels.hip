@@ -313,3 +313,171 @@ hipError_t launch_live_delete(const uint64_t* live_gt, const uint64_t* live_row,
 }
 
 }  // namespace dsy
+
+namespace dsy {
+
+// ---------------------------------------------------------------------------------------------------------
+// Claim side, largest strategy: _select_and_fix (community.py:881-903) on the device.  The reference runs
+//   SELECT global_time, packet FROM sync WHERE meta_message IN (..) AND undone = 0 AND global_time > ?
+//   ORDER BY global_time ASC LIMIT to_select + 1            (or < ? ... DESC)
+// and, when it got to_select + 1 rows, drops the last global time's whole group.  The rows it keeps are therefore
+// exactly those strictly between the pivot and the (to_select+1)-th candidate's global time g -- a global-time
+// interval, whatever order SQLite gives equal global times -- or every candidate when there are at most to_select.
+// One workgroup: per-meta bounds by binary search, then g: with one meta it is an index; with several, every
+// candidate's rank across the metas (binary searches over the others' first to_select+1 candidates, held in LDS
+// when they fit) finds the one of rank to_select+1.
+static constexpr uint32_t kSelThreads = 1024;
+
+__device__ __forceinline__ uint64_t lower_bound_gt(const uint64_t* __restrict__ g, uint64_t lo, uint64_t hi, uint64_t v) {
+    while (lo < hi) {
+        const uint64_t mid = lo + ((hi - lo) >> 1);
+        if (g[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ uint64_t upper_bound_gt(const uint64_t* __restrict__ g, uint64_t lo, uint64_t hi, uint64_t v) {
+    while (lo < hi) {
+        const uint64_t mid = lo + ((hi - lo) >> 1);
+        if (g[mid] <= v) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(kSelThreads) k_select_and_fix(const uint64_t* __restrict__ live_gt,
+                                                                 const uint64_t* __restrict__ spans, uint32_t J,
+                                                                 uint64_t pivot, uint64_t to_select, int higher,
+                                                                 uint64_t* __restrict__ cand_global,
+                                                                 uint32_t cand_lds, uint64_t* __restrict__ out_spans,
+                                                                 SelResult* __restrict__ res) {
+    extern __shared__ uint64_t cand_shared[];
+    __shared__ unsigned long long s_total, s_cands, s_cut, s_count;
+    __shared__ unsigned long long s_first, s_last;
+    const uint64_t L = to_select + 1;
+    if (threadIdx.x == 0) {
+        s_total = 0;
+        s_cut = higher ? ~0ull : 0ull;
+        s_count = 0;
+        s_first = ~0ull;
+        s_last = 0;
+    }
+    __syncthreads();
+    // 1. each meta's candidates: higher [s, b) ascending; lower [a, s) (taken from its end)
+    for (uint32_t j = threadIdx.x; j < J; j += blockDim.x) {
+        const uint64_t a = spans[2 * j], b = spans[2 * j + 1];
+        const uint64_t sj = higher ? upper_bound_gt(live_gt, a, b, pivot) : lower_bound_gt(live_gt, a, b, pivot);
+        out_spans[2 * j] = sj;
+        out_spans[2 * j + 1] = higher ? b - sj : sj - a;  // available candidates
+        atomicAdd(&s_total, (unsigned long long)(higher ? b - sj : sj - a));
+    }
+    __syncthreads();
+    const uint64_t total = s_total;
+    const bool fixed = total >= L;
+    if (fixed) {
+        if (J == 1) {
+            if (threadIdx.x == 0) s_cut = higher ? live_gt[out_spans[0] + L - 1] : live_gt[out_spans[0] - L];
+        } else {
+            uint64_t* cand = cand_lds ? cand_shared : cand_global;
+            // offsets of each meta's first min(avail, L) candidates (single thread: J is small)
+            if (threadIdx.x == 0) {
+                uint64_t at = 0;
+                for (uint32_t j = 0; j < J; ++j) {
+                    const uint64_t m = out_spans[2 * j + 1] < L ? out_spans[2 * j + 1] : L;
+                    out_spans[2 * j + 1] = at;  // reuse: the meta's offset into cand
+                    at += m;
+                }
+                s_cands = at;
+            }
+            __syncthreads();
+            const uint64_t C = s_cands;
+            for (uint64_t i = threadIdx.x; i < C; i += blockDim.x) {
+                uint32_t j = 0;
+                while (j + 1 < J && out_spans[2 * (j + 1) + 1] <= i) ++j;
+                const uint64_t t = i - out_spans[2 * j + 1];
+                const uint64_t sj = out_spans[2 * j];
+                const uint64_t mj = (j + 1 < J ? out_spans[2 * (j + 1) + 1] : C) - out_spans[2 * j + 1];
+                cand[i] = higher ? live_gt[sj + t] : live_gt[sj - mj + t];  // ascending within the meta
+            }
+            __syncthreads();
+            // rank: higher -> the L-th smallest v: #(< v) < L <= #(<= v); lower -> the L-th largest: #(> v) < L <= #(>= v)
+            for (uint64_t i = threadIdx.x; i < C; i += blockDim.x) {
+                const uint64_t v = cand[i];
+                uint64_t lt = 0, le = 0;
+                for (uint32_t j = 0; j < J; ++j) {
+                    const uint64_t o = out_spans[2 * j + 1], e = j + 1 < J ? out_spans[2 * (j + 1) + 1] : C;
+                    lt += lower_bound_gt(cand, o, e, v) - o;
+                    le += upper_bound_gt(cand, o, e, v) - o;
+                }
+                const bool hit = higher ? (lt < L && L <= le) : (C - le < L && L <= C - lt);
+                if (hit) s_cut = v;  // every hit carries the same value
+            }
+            __syncthreads();
+            // restore the search starts
+            if (threadIdx.x == 0) {
+                for (uint32_t j = 0; j < J; ++j) {
+                    const uint64_t a = spans[2 * j], b = spans[2 * j + 1];
+                    out_spans[2 * j] = higher ? upper_bound_gt(live_gt, a, b, pivot) : lower_bound_gt(live_gt, a, b, pivot);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const uint64_t cut = s_cut;
+    // 2. the kept rows per meta: strictly between the pivot and the cut (or every candidate when not over-full)
+    for (uint32_t j = threadIdx.x; j < J; j += blockDim.x) {
+        const uint64_t a = spans[2 * j], b = spans[2 * j + 1], sj = out_spans[2 * j];
+        uint64_t x, y;
+        if (higher) {
+            x = sj;
+            y = fixed ? lower_bound_gt(live_gt, sj, b, cut) : b;
+        } else {
+            x = fixed ? upper_bound_gt(live_gt, a, sj, cut) : a;
+            y = sj;
+        }
+        out_spans[2 * j] = x;
+        out_spans[2 * j + 1] = y;
+        if (y > x) {
+            atomicAdd(&s_count, (unsigned long long)(y - x));
+            atomicMin(&s_first, (unsigned long long)live_gt[x]);
+            atomicMax(&s_last, (unsigned long long)live_gt[y - 1]);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        res->count = s_count;
+        res->first_gt = s_first;
+        res->last_gt = s_last;
+        res->total = total;
+        res->fixed = fixed ? 1u : 0u;
+        res->pad = 0;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_span_rows(const uint64_t* __restrict__ live_row,
+                                                   const uint64_t* __restrict__ spans, uint32_t n_spans,
+                                                   uint64_t* __restrict__ out_rows) {
+    // one workgroup per span; its rows land after the earlier spans' (prefix by a short serial sum)
+    const uint32_t j = blockIdx.x;
+    uint64_t at = 0;
+    for (uint32_t i = 0; i < j; ++i) at += spans[2 * i + 1] - spans[2 * i];
+    const uint64_t x = spans[2 * j], y = spans[2 * j + 1];
+    for (uint64_t i = x + threadIdx.x; i < y; i += 256) out_rows[at + (i - x)] = live_row ? live_row[i] : i;
+}
+
+hipError_t launch_select_and_fix(const uint64_t* live_gt, const uint64_t* spans, uint32_t J, uint64_t pivot,
+                                 uint64_t to_select, int higher, uint64_t* cand, uint64_t* out_spans, SelResult* res,
+                                 hipStream_t stream) {
+    const uint64_t cap = (uint64_t)J * (to_select + 1);
+    const bool lds = J > 1 && cap * 8 <= 64 * 1024;
+    hipLaunchKernelGGL(k_select_and_fix, dim3(1), dim3(kSelThreads), lds ? (size_t)cap * 8 : 0, stream, live_gt, spans,
+                       J, pivot, to_select, higher, cand, lds ? 1u : 0u, out_spans, res);
+    return hipGetLastError();
+}
+
+hipError_t launch_span_rows(const uint64_t* live_row, const uint64_t* spans, uint32_t n_spans, uint64_t* out_rows,
+                            hipStream_t stream) {
+    if (!n_spans) return hipSuccess;
+    hipLaunchKernelGGL(k_span_rows, dim3(n_spans), dim3(256), 0, stream, live_row, spans, n_spans, out_rows);
+    return hipGetLastError();
+}
+
+}  // namespace dsy

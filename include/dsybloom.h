@@ -38,6 +38,7 @@ extern "C" {
 #define DSY_ENOMEM -3    /* device allocation failed */
 #define DSY_ECAPACITY -4 /* output capacity too small; the required size is returned through the count pointer */
 #define DSY_EUNSORTED -5 /* store rows are not in (meta, global_time) order */
+#define DSY_EEMPTY -6    /* the reference raises IndexError: a claim range over no rows (community.py:857) */
 
 /* hash families, selected exactly as bloomfilter.py:134-156 does from (m, k) */
 #define DSY_MD5 0
@@ -217,6 +218,20 @@ int dsy_bloom_add_rows(dsy_ctx* ctx, const dsy_bloom_params* p, const dsy_store*
  * 0 <= offset < modulo, else DSY_EINVAL. */
 int dsy_claim_modulo(dsy_ctx* ctx, const dsy_bloom_params* p, const dsy_store* store, const uint32_t* meta_ids,
                      uint32_t nmeta, uint64_t offset, uint64_t modulo, uint8_t* filter_inout, uint64_t* out_count);
+
+/* Claim side, largest strategy (the default, community.py:763-837): everything after the random draws -- the pivot
+ * from_gbtime (:776-780) is the caller's, like the filter's random prefix.  Selects the rows of the given syncable
+ * metas around the pivot exactly as _select_bloomfilter_range / _select_and_fix do (:839-903: up to capacity rows
+ * above and below it in global-time order, the trailing equal-global-time group dropped when over-full, the side
+ * with the wider range kept; or, when nrsyncpackets < capacity or the pivot is <= 1, the first capacity rows), on
+ * the device over the live index, and ORs their packets into filter_inout (:821).
+ * out_claim[0..3] = time_low, time_high (both already min(., acceptable_global_time)), rows added (0: the caller
+ * returns the empty claim of :837), and the new _nrsyncpackets (capacity + 1 when the first-rows branch was
+ * over-full, :810-815, else nrsyncpackets).  DSY_EEMPTY where the reference raises IndexError (a stale
+ * nrsyncpackets over a store with no rows on the pivot's side, :857). */
+int dsy_claim_largest(dsy_ctx* ctx, const dsy_bloom_params* p, const dsy_store* store, const uint32_t* meta_ids,
+                      uint32_t nmeta, uint64_t from_gbtime, uint64_t capacity, uint64_t nrsyncpackets,
+                      uint64_t acceptable_global_time, uint8_t* filter_inout, uint64_t* out_claim);
 
 /* ------------------------------------------------------------------------------------------- responder */
 /* Batched responder: replaces _get_packets_for_bloomfilters (community.py:2746-2811) plus the byte-limited
