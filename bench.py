@@ -33,6 +33,53 @@ PEAK_INT32_TOPS = 78.64        # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz: one 32-bi
 OPS_PER_BLOCK = {"md5": 500, "sha1": 961, "sha256": 2168, "sha384": 5504, "sha512": 5504}  # SURVEY §8d canonical
 
 
+# ------------------------------------------------------------------------------------------- CPU legs
+def cpu_info():
+    """(CPU model, cores this process may use).  On the GPU box the affinity mask shows the whole machine; the
+    box's share is OMP_NUM_THREADS (16 per GPU), so that caps the worker count."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    avail = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS") or avail)
+    # forked workers inherit the parent's open device files: stay below the box's 16-process GPU guard
+    return model, max(1, min(avail, share, 15))
+
+
+_PAR = {}
+
+
+def _par_worker(i):
+    """One forked worker: pure CPU work over data the parent set up before forking (never touches the GPU)."""
+    t0 = time.perf_counter()
+    units = _PAR["fn"](_PAR["shards"][i])
+    return units, time.perf_counter() - t0
+
+
+def cpu_parallel(fn, shards):
+    """Run fn(shard) for every shard in len(shards) forked processes at once; returns (units, wall seconds of the
+    slowest): the N-core rate is units / seconds.  fn must be CPU-only (hashlib / sqlite / numpy)."""
+    import multiprocessing as mp
+    _PAR.update(fn=fn, shards=shards)
+    with mp.get_context("fork").Pool(len(shards)) as pool:
+        res = pool.map(_par_worker, range(len(shards)))
+    _PAR.clear()
+    return sum(u for u, _ in res), max(t for _, t in res)
+
+
+def n_core_leg(fn, shards, unit, sample):
+    model, cores = cpu_info()
+    units, secs = cpu_parallel(fn, shards)
+    return {"value": round(units / secs, 1), "unit": unit, "cores": len(shards), "cpu_model": model,
+            "sample": sample, "seconds": round(secs, 2)}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -51,11 +98,12 @@ def parse():
     ap.add_argument("--sim-initial", type=int, default=100)
     ap.add_argument("--sim-rounds", type=int, default=10)
     ap.add_argument("--sim-warmup", type=int, default=2)
-    ap.add_argument("--extra", default="claim,dedup,ingest,1,3,4,5",
+    ap.add_argument("--extra", default="claim,dropin,dedup,ingest,1,3,4,5",
                     help="BASELINE configs measured beside the headline (config 2): 1 single filter, 3 gossip "
                          "simulator, 4 large filters, 5 heavy-tailed packets, ingest: received packets appended to "
-                         "the headline store, dedup: duplicate check of received packets against it, claim: modulo claims built "
-                         "over it on the device; '' for none")
+                         "the headline store, dedup: duplicate check of received packets against it, claim: modulo and "
+                         "largest claims built over it on the device, dropin: SyncCommunity.respond / store_messages "
+                         "over it (host buffers); '' for none")
     ap.add_argument("--large-keys", type=int, default=100_000_000, help="config 4: keys added per filter")
     ap.add_argument("--large-tests", type=int, default=10_000_000, help="config 4: keys tested per filter")
     return ap.parse_args()
@@ -234,8 +282,11 @@ def main():
     ingest = None
     dedup = None
     claim = None
+    dropin = None
     if "claim" in extra:
         claim = claim_bench(args, ctx, lib, store, N, capacity, total_bytes / N, cpu_leg=rank == 0 and world == 1)
+    if "dropin" in extra:
+        dropin = dropin_bench(args, ctx, lib, store, offsets, N, claims)
     if "dedup" in extra:
         dedup = dedup_bench(args, ctx, lib, store, blob, offsets, N, cpu_leg=rank == 0 and world == 1)
     if "ingest" in extra:
@@ -290,12 +341,74 @@ def main():
             "ingest": ingest,
             "dedup": dedup,
             "claim_modulo": claim,
+            "dropin": dropin,
         }
         print(json.dumps(line))
     if store is not None:
         lib.dsy_store_free(store)
     if dist:
         dist.destroy_process_group()
+
+
+def dropin_bench(args, ctx, lib, store, offsets, N, claims, reps=5, batch=10_000, batches=5):
+    """The drop-in surface a Dispersy caller hits, over the headline's 10 M-packet store in HBM:
+    - SyncCommunity.respond: the headline's 1024 claims as ClaimRequests with BloomFilter objects -> dsy_sync_respond
+      (host buffers: the filters go up the bus, the responses come back) -> per-claim row lists;
+    - SyncCommunity.store_messages: batches of received messages INSERTed (SyncStore.append: O(batch) host columns,
+      dsy_store_append into HBM) with the community's global time raised (Dispersy._store).
+    Wall time per call, PCIe and Python included."""
+    from dispersy_amd.bloomfilter import BloomFilter
+    from dispersy_amd.community import ClaimRequest, SyncCommunity
+    from dispersy_amd.distribution import MetaMessage, SyncDistribution
+    from dispersy_amd.store import SyncStore
+    lengths = (offsets[1:] - offsets[:-1]).cpu().numpy().astype(np.uint64)
+    n0 = int(lib.dsy_store_rows(store))
+    st = SyncStore.attach(ctx, store, np.arange(1, n0 + 1, dtype=np.uint64), np.ones(n0, dtype=np.uint32), lengths)
+    com = SyncCommunity(st, [MetaMessage("bench", 1, SyncDistribution("ASC", 128))], global_time=N)
+    reqs = [ClaimRequest(lo, hi, modulo, offset, BloomFilter(raw, kf, prefix))
+            for lo, hi, offset, modulo, kf, prefix, raw in claims]
+    com.respond(reqs, byte_limit=args.byte_limit, random_seed=99)
+    times, rows = [], 0
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        got = com.respond(reqs, byte_limit=args.byte_limit, random_seed=99)
+        times.append(time.perf_counter() - t0)
+        rows = sum(len(g) for g in got)
+    ms = sorted(times)[len(times) // 2] * 1e3
+    respond = {"call": "SyncCommunity.respond(1024 ClaimRequests) -> dsy_sync_respond (host buffers)",
+               "median_ms_per_batch": round(ms, 3), "claims_per_s": round(len(reqs) / (ms / 1e3), 1),
+               "rows_returned": rows}
+
+    class Dist(object):
+        def __init__(self, gt):
+            self.global_time, self.priority = gt, 128
+
+    class Msg(object):
+        database_id = 1
+
+        def __init__(self, gt, packet):
+            self.distribution, self.packet, self.candidate = Dist(gt), packet, None
+
+    rng = np.random.Generator(np.random.PCG64(314))
+    work = []
+    for b in range(batches + 1):
+        lens = rng.integers(100, 1501, size=batch)
+        data = rng.bytes(int(lens.sum()))
+        cuts = np.concatenate([[0], np.cumsum(lens)])
+        base = n0 + b * batch
+        # global time = row + 1, as every row of the headline store (the duplicate-check leg keys rows that way)
+        work.append([Msg(base + j + 1, data[int(cuts[j]):int(cuts[j + 1])]) for j in range(batch)])
+    com.store_messages(work[0])
+    times = []
+    for msgs in work[1:]:
+        t0 = time.perf_counter()
+        com.store_messages(msgs)
+        times.append(time.perf_counter() - t0)
+    ms2 = sorted(times)[len(times) // 2] * 1e3
+    store_msgs = {"call": "SyncCommunity.store_messages(%d messages) -> SyncStore.append -> dsy_store_append" % batch,
+                  "median_ms_per_batch": round(ms2, 3), "messages_per_s": round(batch / (ms2 / 1e3), 1),
+                  "store_rows_after": int(lib.dsy_store_rows(store))}
+    return {"respond": respond, "store_messages": store_msgs}
 
 
 def dedup_bench(args, ctx, lib, store, blob, offsets, N, batch=10_000, reps=10, cpu_leg=True):
@@ -306,10 +419,11 @@ def dedup_bench(args, ctx, lib, store, blob, offsets, N, batch=10_000, reps=10, 
     64-byte packet compares).  Wall time per call, PCIe upload of the messages included."""
     import torch
     rng = np.random.Generator(np.random.PCG64(123))
-    member = (np.arange(N, dtype=np.uint64) % np.uint64(65536))  # with global_time = row + 1: unique keys
-    gt = np.arange(1, N + 1, dtype=np.uint64)
+    n_rows = int(lib.dsy_store_rows(store))  # the headline's rows plus what the drop-in leg stored (gt = row + 1)
+    member = (np.arange(n_rows, dtype=np.uint64) % np.uint64(65536))  # with global_time = row + 1: unique keys
+    gt = np.arange(1, n_rows + 1, dtype=np.uint64)
     t0 = time.perf_counter()
-    _native.check(lib.dsy_store_index_members(ctx.handle, store, member.ctypes.data, gt.ctypes.data, N))
+    _native.check(lib.dsy_store_index_members(ctx.handle, store, member.ctypes.data, gt.ctypes.data, n_rows))
     build_ms = (time.perf_counter() - t0) * 1e3
 
     def make():
@@ -401,9 +515,10 @@ def claim_bench(args, ctx, lib, store, N, capacity, mean_len, reps=20, cpu_leg=T
     ms = sorted(times)[len(times) // 2] * 1e3
     hit = float(np.mean(hits))
     alg_bytes = 8.0 * N + hit * (8 + mean_len)
-    cpu = None
+    cpu = cpu_largest = None
     if cpu_leg and args.cpu_claims > 0:  # the reference's SELECT (community.py:918) in sqlite + hashlib add_keys
         import sqlite3
+        from oracle import sync_ref
         from oracle.bloom_ref import OracleBloom
         from oracle.sync_ref import SYNC_SCHEMA
         pre = 1_000_000
@@ -422,14 +537,63 @@ def claim_bench(args, ctx, lib, store, N, capacity, mean_len, reps=20, cpu_leg=T
                 "SELECT sync.packet FROM sync WHERE meta_message IN (1) AND sync.undone = 0 "
                 "AND (sync.global_time + ?) % ? = 0", (c, cmod))])
         dt = time.perf_counter() - t0
+        # the largest strategy's reference path on the same table: its SELECT ... ORDER BY global_time LIMIT
+        # (community.py:884-888) twice per claim + add_keys, through oracle/sync_ref.claim_largest
+        import random as _r
+        lmetas = [dict(name="bench", id=1, direction="ASC", priority=128, pruning=None)]
+        t1 = time.perf_counter()
+        n_large = 20
+        for c in range(n_large):
+            sync_ref.claim_largest(conn, lmetas, args.filter_bits, args.error_rate, pre, pre + 10000, pre,
+                                   _r.Random(c), OracleBloom)
+        dt_large = time.perf_counter() - t1
         conn.close()
+        model, _ = cpu_info()
         cpu = {"value": round(nclaims * pre / dt, 1), "unit": "indexed rows/s", "cores": 1, "kind": "port",
-               "sample": "%d modulo claims (modulo %d) through the reference's SELECT (community.py:918) on an in-memory "
-                         "sqlite3 sync table of %d rows + hashlib add_keys of the hits" % (nclaims, cmod, pre)}
+               "cpu_model": model,
+               "sample": "row-rate comparison, not the same workload: %d modulo claims (modulo %d) through the "
+                         "reference's SELECT (community.py:918) on an in-memory sqlite3 sync table of %d rows + hashlib "
+                         "add_keys of the hits; the GPU line scans a %d-row store, so compare indexed rows/s"
+                         % (nclaims, cmod, pre, N)}
+        cpu_largest = {"value": round(n_large / dt_large, 2), "unit": "largest claims/s", "cores": 1, "kind": "port",
+                       "cpu_model": model,
+                       "sample": "%d claims through oracle/sync_ref.claim_largest (the reference's ORDER BY global_time "
+                                 "LIMIT capacity+1 SELECTs, community.py:839-903, + hashlib add_keys) over the %d-row "
+                                 "sqlite3 table; the SELECTs walk the (meta, undone, global_time) index, so their cost "
+                                 "does not grow with the table" % (n_large, pre)}
+    largest = claim_largest_bench(args, ctx, lib, store, N, capacity, cpu_largest)
     return {"metric": "modulo claims built/sec", "store_rows": N, "modulo": modulo, "mean_hits": round(hit, 1),
             "median_ms_per_claim": round(ms, 3), "claims_per_s": round(1e3 / ms, 1),
             "indexed_rows_per_s": round(N / (ms / 1e3), 1),
-            "achieved_gbs": round(alg_bytes / (ms / 1e3) / 1e9, 1), "cpu_baseline": cpu}
+            "achieved_gbs": round(alg_bytes / (ms / 1e3) / 1e9, 1), "cpu_baseline": cpu, "largest": largest}
+
+
+def claim_largest_bench(args, ctx, lib, store, N, capacity, cpu, reps=20):
+    """The default (largest) claim strategy on the device (dsy_claim_largest, community.py:763-903): pivots drawn as
+    the reference draws them (gt - expovariate(2 / gt)) over the 10 M-row store, capacity rows selected on each side,
+    the wider range's rows hashed into the MTU filter.  Wall time per call (filter over the bus included)."""
+    import random as _r
+    from dispersy_amd.bloomfilter import BloomFilter
+    rng = _r.Random(2718)
+    ids = np.asarray([1], dtype=np.uint32)
+    out = (ctypes.c_uint64 * 4)()
+    times, added = [], []
+    for r in range(reps + 2):
+        bf = BloomFilter(args.filter_bits, args.error_rate, bytes([rng.randrange(256)]))
+        buf = ctypes.create_string_buffer(bytes(bf._raw), len(bf._raw))
+        pivot = N - int(rng.expovariate(1.0 / (N / 2.0)))
+        if pivot < 1:
+            pivot = int(rng.random() * N)
+        t0 = time.perf_counter()
+        _native.check(lib.dsy_claim_largest(ctx.handle, ctypes.byref(bf.params), store, ids.ctypes.data, 1, pivot,
+                                            capacity, N, N + 10000, buf, out))
+        if r >= 2:
+            times.append(time.perf_counter() - t0)
+            added.append(out[2])
+    ms = sorted(times)[len(times) // 2] * 1e3
+    return {"metric": "largest claims built/sec", "store_rows": N, "median_ms_per_claim": round(ms, 3),
+            "claims_per_s": round(1e3 / ms, 1), "mean_rows_hashed": round(float(np.mean(added)), 1),
+            "cpu_baseline": cpu}
 
 
 def ingest_bench(args, ctx, lib, store, step, pairs, N, batch=10_000, batches=10, cpu_leg=True):
@@ -521,6 +685,9 @@ def gossip_sim(args, ctx, dev, rank, world, dist):
     held0 = sim.global_stats()[0]
     for r in range(args.sim_warmup):
         sim.round(r)
+    eng.sync()
+    ctx.reset_timing()
+    ctx.set_timing(True, only=[_native.TIME_SIM_BUILD, _native.TIME_SIM_RESPOND])
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -532,6 +699,20 @@ def gossip_sim(args, ctx, dev, rank, world, dist):
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
+    ctx.set_timing(False)
+    kernels = {}
+    for name, cls in (("k_sim_build_claims<md5>", _native.TIME_SIM_BUILD), ("k_sim_respond<md5>", _native.TIME_SIM_RESPOND)):
+        kt, wk = ctx.kernel_time(cls), ctx.work(cls)
+        secs = kt["ms"] / 1e3
+        kernels[name] = {
+            "ms_per_round": round(kt["ms"] / max(args.sim_rounds, 1), 3),
+            "gblocks_per_s": round(wk["blocks"] / secs / 1e9, 2) if secs else None,
+            "valu_int32": {"achieved": round(wk["blocks"] * OPS_PER_BLOCK["md5"] / secs / 1e12, 2) if secs else None,
+                           "peak": PEAK_INT32_TOPS, "unit": "Tops/s",
+                           "frac": round(wk["blocks"] * OPS_PER_BLOCK["md5"] / secs / 1e12 / PEAK_INT32_TOPS, 4)
+                           if secs else None},
+            "lane_utilization": round(wk["blocks"] / max(wk["lane_slots"], 1), 4),
+            "blocks_per_round": int(wk["blocks"] / max(args.sim_rounds, 1))}
     if dist:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -543,7 +724,39 @@ def gossip_sim(args, ctx, dev, rank, world, dist):
             "config": {"peers": args.sim_peers, "universe": args.sim_universe, "initial_packets": args.sim_initial,
                        "filter": "m=%d k=%d md5" % (cfg.m_bits, cfg.k), "byte_limit": cfg.byte_limit},
             "packets_held_start": held0, "packets_held_end": held, "store_checksum": "%016x" % chk,
-            "exchange_bytes_rank0": sim.exchanged_bytes}
+            "exchange_bytes_rank0": sim.exchanged_bytes, "kernels": kernels,
+            "cpu_baseline": gossip_cpu(args, blob, offs) if rank == 0 and world == 1 and args.cpu_claims > 0 else None}
+
+
+def gossip_cpu(args, blob, offs, peers=10_000):
+    """oracle/sim_ref's CPU engine (hashlib + Python, the reference's per-packet work) runs ONE round of a
+    `peers`-peer simulation from the seeded state; a round of the benchmarked args.sim_peers peers is that work
+    times args.sim_peers / peers (stated as an extrapolation).  N cores: one independent
+    `peers`-peer round per process."""
+    from dispersy_amd.sim import EpidemicSim, make_config
+    from oracle.sim_ref import OracleEngine
+    scale = args.sim_peers / float(peers)
+
+    def one_round(seed):
+        cfg = make_config(peers, args.sim_universe, 0, 1, seed=seed)
+        eng = OracleEngine(cfg, blob, offs, arrays="numpy")
+        eng.seed(args.sim_initial)
+        sim = EpidemicSim(eng, cfg)
+        t0 = time.perf_counter()
+        sim.round(0)
+        return time.perf_counter() - t0, sim.tested
+
+    dt, tested = one_round(11)
+    model, cores = cpu_info()
+    ncore = n_core_leg(lambda seed: one_round(seed) and 1, [11 + w for w in range(cores)], "rounds of %d peers/s" % peers,
+                       "one %d-peer round per process" % peers)
+    return {"value": round(1.0 / (dt * scale), 5), "unit": "rounds/s (extrapolated to %d peers)" % args.sim_peers,
+            "cores": 1, "kind": "port", "cpu_model": model,
+            "sample": "one round of a %d-peer simulation (universe %d, %d initial packets per peer) through "
+                      "oracle/sim_ref.OracleEngine: %.2f s, %d (claim, packet) pairs tested; x %g for %d peers"
+                      % (peers, args.sim_universe, args.sim_initial, dt, tested, scale, args.sim_peers),
+            "n_core": dict(ncore, value_extrapolated=round(ncore["value"] / scale, 5),
+                           unit_extrapolated="rounds/s (extrapolated to %d peers)" % args.sim_peers)}
 
 
 def _blocks(lengths, plen, hash_name):
@@ -630,8 +843,19 @@ def single_filter_cpu(blob, offsets):
         t2 = time.perf_counter()
         res[name] = {"add_keys_per_s": round(n_add / (t1 - t0), 1), "test_keys_per_s": round(n_test / (t2 - t1), 1),
                      "present": hits}
-    return {"kind": "port", "cores": 1, "sample": "%d adds + %d tests of the same packets per filter" % (n_add, n_test),
-            "results": res}
+    model, cores = cpu_info()
+    for name, m, f, prefix in (("md5", 10160, 0.01, b"\x00\x01\x02\x03"), ("sha1", 4096, 0.001, b"x")):
+        ob = OracleBloom.from_m_f(m, f, prefix)
+        ob.add_keys(keys[:n_add])
+
+        def test(idx, ob=ob):
+            for i in idx:
+                keys[i] in ob  # noqa: B015 -- the membership test is the work
+            return len(idx)
+        res[name]["n_core"] = n_core_leg(test, [range(n_test)] * cores, "tests/s",
+                                         "the %d tests in every process, one process per core" % n_test)
+    return {"kind": "port", "cores": 1, "cpu_model": model,
+            "sample": "%d adds + %d tests of the same packets per filter" % (n_add, n_test), "results": res}
 
 
 def large_filter(args, ctx, lib, dev, rank, world, dist=None):
@@ -729,9 +953,18 @@ def large_filter_cpu(blob, offsets):
     t1 = time.perf_counter()
     sum(1 for k in keys[n_add:] if k in ob)
     t2 = time.perf_counter()
-    return {"kind": "port", "cores": 1, "filter": "2^20",
+    model, cores = cpu_info()
+
+    def adds(idx):
+        mine = OracleBloom.from_m_f(1 << 20, 0.01, b"\x07")  # each process its own partial filter, as a sharded build
+        mine.add_keys(keys[i] for i in idx)
+        return len(idx)
+    ncore = n_core_leg(adds, [[(w * 997 + j) % n_add for j in range(n_add)] for w in range(cores)], "adds/s",
+                       "%d adds per process into its own 2^20 filter" % n_add)
+    return {"kind": "port", "cores": 1, "filter": "2^20", "cpu_model": model,
             "sample": "%d adds + %d tests, extrapolated per key" % (n_add, n_test),
-            "add_keys_per_s": round(n_add / (t1 - t0), 1), "test_keys_per_s": round(n_test / (t2 - t1), 1)}
+            "add_keys_per_s": round(n_add / (t1 - t0), 1), "test_keys_per_s": round(n_test / (t2 - t1), 1),
+            "n_core": ncore}
 
 
 def heavy_tail(args, ctx, lib, dev, rank, world, dist):
@@ -770,7 +1003,7 @@ def heavy_tail(args, ctx, lib, dev, rank, world, dist):
     cap = BloomFilter(args.filter_bits, args.error_rate).get_capacity(args.error_rate)
     modulo_m = int(math.ceil(N / float(cap)))
     reqs = (_native.Request * R)()
-    filters, off, sel_rows = [], 0, 0
+    filters, off, sel_rows, claims = [], 0, 0, []
     for i in range(R):
         if i % 2 == 0:
             a = int(rng.integers(0, N))
@@ -800,8 +1033,10 @@ def heavy_tail(args, ctx, lib, dev, rank, world, dist):
         q.prefix_len = 1
         q.prefix[0] = prefix[0]
         filters.append(raw)
+        claims.append((lo, hi, offset, modulo, bf.functions, prefix, buf.raw))
         off += len(raw)
-    d_filters = torch.frombuffer(bytearray(b"".join(filters) + bytes(64)), dtype=torch.uint8).to(dev)
+    fblob = b"".join(filters)
+    d_filters = torch.frombuffer(bytearray(fblob + bytes(64)), dtype=torch.uint8).to(dev)
     metas = (_native.Meta * 1)()
     metas[0].meta_id, metas[0].direction = 1, _native.DSY_ASC
     p_out, p_off, pairs = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
@@ -829,8 +1064,21 @@ def heavy_tail(args, ctx, lib, dev, rank, world, dist):
     ctx.set_timing(False)
     kt = ctx.kernel_time(_native.TIME_PAIR_TEST)
     work = ctx.work(_native.TIME_PAIR_TEST)
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_claims > 0:
+        cpu = heavy_tail_cpu(args, lib, ctx, store, reqs, claims, fblob, blob, offsets, total, h_gt, G_MAX)
     lib.dsy_store_free(store)
+    secs = kt["ms"] / 1e3
     out = {"metric": "packets hashed+tested/sec", "value": round(work["useful_pairs"] / dt, 1), "unit": "packets/s",
+           "cpu_baseline": cpu,
+           "roofline": {"kernel": "k_pair_test<md5>", "bound": "valu+hbm",
+                        "valu_int32": {"achieved": round(work["blocks"] * OPS_PER_BLOCK["md5"] / secs / 1e12, 2)
+                                       if secs else None, "peak": PEAK_INT32_TOPS, "unit": "Tops/s",
+                                       "frac": round(work["blocks"] * OPS_PER_BLOCK["md5"] / secs / 1e12 /
+                                                     PEAK_INT32_TOPS, 4) if secs else None},
+                        "hbm": {"achieved": round(work["bytes"] / secs / 1e9, 1) if secs else None,
+                                "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                                "frac": round(work["bytes"] / secs / 1e9 / PEAK_HBM_GBS, 4) if secs else None}},
            "pairs_hashed_per_s": round(hashed / dt, 1), "ms_per_step": round(dt / steps * 1e3, 3), "steps": steps,
            "stored_packets": N, "stored_bytes": total, "mean_packet_bytes": round(total / N, 1),
            "max_packet_bytes": int(lengths.max().item()), "selected_rows_per_step": int(sel_rows),
@@ -842,6 +1090,54 @@ def heavy_tail(args, ctx, lib, dev, rank, world, dist):
     del blob_full, blob, offsets, lengths, gt, meta, d_filters
     torch.cuda.empty_cache()
     return out
+
+
+def heavy_tail_cpu(args, lib, ctx, store, reqs, claims, fblob, blob, offsets, total, h_gt, g_max, n_sample=24):
+    """cfg5's CPU legs: the oracle's array-form responder (numpy range/modulo selection + hashlib not_filter loop
+    exactly as the reference) on the first n_sample claims, 1 core, with the GPU's answers for those claims checked
+    against it (host-buffer dsy_sync_respond); then one process per core over disjoint claim shards."""
+    from oracle import sync_ref
+    from oracle.bloom_ref import OracleBloom
+    host_blob = memoryview(blob[:total].cpu().numpy())
+    host_off = offsets.cpu().numpy()
+    N = len(h_gt)
+    gt_by_meta = {1: (np.arange(N, dtype=np.int64), h_gt.astype(np.uint64))}
+    packet_of = lambda r: host_blob[int(host_off[r]):int(host_off[r + 1])]  # noqa: E731
+    metas = [dict(name="bench", id=1, direction="ASC", priority=128, pruning=None)]
+
+    def run(idx, cnt):
+        outs = []
+        for i in idx:
+            lo, hi, offset, modulo, kf, prefix, raw = claims[i]
+            outs.append(sync_ref.respond_arrays(packet_of, gt_by_meta, metas, (lo, hi, offset, modulo),
+                                                OracleBloom.from_bytes(raw, kf, prefix), g_max, args.byte_limit, False,
+                                                cnt))
+        return outs
+    sample = list(range(min(n_sample, len(claims))))
+    counter = [0]
+    t0 = time.perf_counter()
+    outs = run(sample, counter)
+    dt = time.perf_counter() - t0
+    sub = (type(reqs[0]) * len(sample))(*[reqs[i] for i in sample])
+    out_off = np.zeros(len(sample) + 1, dtype=np.uint64)
+    out = np.zeros(1 << 22, dtype=np.uint64)
+    _native.check(lib.dsy_sync_respond(ctx.handle, store, sub, len(sample), fblob, len(fblob),
+                                       (_native.Meta * 1)(_native.Meta(1, 0, 0, 0, 0)), 1, g_max, 0, args.byte_limit,
+                                       99, out.ctypes.data, len(out), out_off.ctypes.data))
+    gpu = [out[int(out_off[j]):int(out_off[j + 1])].tolist() for j in range(len(sample))]
+    model, cores = cpu_info()
+
+    def shard(idx):
+        cnt = [0]
+        run(idx, cnt)
+        return cnt[0]
+    per = max(1, n_sample // 2)
+    ncore = n_core_leg(shard, [[(w * per + j) % len(claims) for j in range(per)] for w in range(cores)], "packets/s",
+                       "%d claims per process, one process per core, same port" % per)
+    return {"value": round(counter[0] / dt, 1), "unit": "packets/s", "cores": 1, "kind": "port", "cpu_model": model,
+            "sample": "%d of the step's claims (%d pairs hashed lazily) through oracle/sync_ref.respond_arrays + "
+                      "oracle/bloom_ref (hashlib), %.1f s" % (len(sample), counter[0], dt),
+            "gpu_matches_cpu_on_sample": gpu == outs, "n_core": ncore}
 
 
 def cpu_baseline(args, ctx, lib, store, reqs, claims, blob, offsets, total_bytes, N, fblob):
@@ -875,11 +1171,23 @@ def cpu_baseline(args, ctx, lib, store, reqs, claims, blob, offsets, total_bytes
                                        (_native.Meta * 1)(_native.Meta(1, 0, 0, 0, 0)), 1, N, 0, args.byte_limit, 99,
                                        out.ctypes.data, len(out), out_off.ctypes.data))
     gpu = [out[int(out_off[j]):int(out_off[j + 1])].tolist() for j in range(len(sample))]
-    return {"value": round(counter[0] / dt, 1), "unit": "packets/s", "cores": 1, "kind": "port",
+    model, cores = cpu_info()
+
+    def shard(idx):
+        cnt = [0]
+        for i in idx:
+            lo, hi, offset, modulo, kf, prefix, raw = claims[i]
+            sync_ref.respond_arrays(packet_of, gt_by_meta, metas, (lo, hi, offset, modulo),
+                                    OracleBloom.from_bytes(raw, kf, prefix), N, args.byte_limit, False, cnt)
+        return cnt[0]
+    per = max(1, k // 2)
+    ncore = n_core_leg(shard, [[(w * per + j) % len(claims) for j in range(per)] for w in range(cores)], "packets/s",
+                       "%d claims per process, one process per core, same port" % per)
+    return {"value": round(counter[0] / dt, 1), "unit": "packets/s", "cores": 1, "kind": "port", "cpu_model": model,
             "sample": "%d of the step's claims (%d pairs hashed lazily, as the reference stops at the byte limit) "
                       "through oracle/sync_ref.respond_arrays + oracle/bloom_ref (hashlib), %.1f s"
                       % (len(sample), counter[0], dt),
-            "gpu_matches_cpu_on_sample": gpu == outs}
+            "gpu_matches_cpu_on_sample": gpu == outs, "n_core": ncore}
 
 
 from dispersy_amd import _native  # noqa: E402  (module-level name used in cpu_baseline)

@@ -24,7 +24,7 @@ BLOB_GUARD = 256
 SYNC_HEADER = 24  # DSY_SYNC_HEADER: '>QQHHBH' + the 1-byte prefix (conversion.py:727-728)
 
 # the ctx timer classes of dsy_ctx_kernel_time
-TIME_PAIR_TEST, TIME_BLOOM, TIME_SELECT, TIME_COMPACT = 0, 1, 2, 3
+TIME_PAIR_TEST, TIME_BLOOM, TIME_SELECT, TIME_COMPACT, TIME_SIM_BUILD, TIME_SIM_RESPOND = 0, 1, 2, 3, 4, 5
 
 
 class NativeUnavailable(RuntimeError):

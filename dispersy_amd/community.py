@@ -28,6 +28,7 @@ from .bloomfilter import BloomFilter
 from .distribution import FullSyncDistribution, GlobalTimePruning, LastSyncDistribution, SyncDistribution
 
 MAX_GT = 2 ** 63 - 1  # sqlite's signed 64-bit ceiling (community.py:2545-2548)
+_REQUEST_DTYPE = np.dtype(_native.Request)  # the dsy_request layout, as a numpy record
 
 # the sync part of an introduction-request payload (payload.py:31-153): time_high == 0 means "up to the
 # responder's global time"
@@ -616,25 +617,42 @@ class SyncCommunity(object):
 
     def respond(self, requests, include_inactive=False, byte_limit=None, random_seed=None):
         """Batched responder (community.py:2531-2572): for each ClaimRequest (time_high already resolved), the store
-        rows the reference would send, in send order.  One call into the HIP library for the whole batch."""
+        rows the reference would send, in send order.  One call into the HIP library for the whole batch; the
+        dsy_request records are filled column by column (numpy view of the ctypes layout), not one ctypes field at
+        a time."""
         R = len(requests)
-        reqs = (_native.Request * max(R, 1))()
-        filters, off = [], 0
-        for i, q in enumerate(requests):
-            bf = q.bloom_filter
-            raw = bf.bytes
-            raw += b"\x00" * ((-len(raw)) % 4)
-            r = reqs[i]
-            r.time_low, r.time_high = min(q.time_low, MAX_GT), min(q.time_high, MAX_GT)
-            r.modulo, r.offset = q.modulo, q.offset
-            r.filter_offset = off
-            r.m_bits, r.k = bf.size, bf.functions
-            r.hash_kind, r.chunk_bytes = _native.HASH_KINDS[bf.hash_name], bf.chunk_bytes
-            r.prefix_len = len(bf.prefix)
-            ctypes.memmove(r.prefix, bf.prefix, len(bf.prefix))
-            filters.append(raw)
-            off += len(raw)
-        return self._respond_requests(reqs, R, b"".join(filters), include_inactive, byte_limit, random_seed)
+        reqs = np.zeros(max(R, 1), dtype=_REQUEST_DTYPE)
+        if R:
+            blooms = [q.bloom_filter for q in requests]
+            raws = [bf.bytes for bf in blooms]
+            sizes = np.fromiter(((len(r) + 3) & ~3 for r in raws), dtype=np.uint64, count=R)
+            reqs["filter_offset"][:R] = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+            reqs["time_low"][:R] = [min(q.time_low, MAX_GT) for q in requests]
+            reqs["time_high"][:R] = [min(q.time_high, MAX_GT) for q in requests]
+            reqs["modulo"][:R] = [q.modulo for q in requests]
+            reqs["offset"][:R] = [q.offset for q in requests]
+            reqs["m_bits"][:R] = [bf.size for bf in blooms]
+            reqs["k"][:R] = [bf.functions for bf in blooms]
+            reqs["hash_kind"][:R] = [_native.HASH_KINDS[bf.hash_name] for bf in blooms]
+            reqs["chunk_bytes"][:R] = [bf.chunk_bytes for bf in blooms]
+            prefixes = [bf.prefix for bf in blooms]
+            plen = np.fromiter((len(p) for p in prefixes), dtype=np.uint32, count=R)
+            reqs["prefix_len"][:R] = plen
+            if (plen == 1).all():
+                reqs["prefix"][:R, 0] = [p[0] for p in prefixes]
+            else:
+                for i, p in enumerate(prefixes):
+                    reqs["prefix"][i, :len(p)] = np.frombuffer(p, dtype=np.uint8)
+            first = len(raws[0])
+            if all(len(r) == first for r in raws):  # one filter size (the MTU claim): pad every row at once
+                rows = np.zeros((R, (first + 3) & ~3), dtype=np.uint8)
+                rows[:, :first] = np.frombuffer(b"".join(raws), dtype=np.uint8).reshape(R, first)
+                blob = rows.tobytes()
+            else:
+                blob = b"".join(r + b"\x00" * ((-len(r)) % 4) for r in raws)
+        else:
+            blob = b""
+        return self._respond_requests(reqs, R, blob, include_inactive, byte_limit, random_seed)
 
     def respond_wire(self, blocks, include_inactive=False, byte_limit=None, random_seed=None):
         """on_introduction_request's sync half for a receive batch of raw sync blocks: decode (conversion.py:732-799,
@@ -650,7 +668,9 @@ class SyncCommunity(object):
             # DropPacket/DelayPacket): no claim of the batch is answered
             raise_for_status(DECODE_ASSERT, int(asserting[0]))
         good = np.flatnonzero(batch.status == 0)
-        sub = (_native.Request * max(len(good), 1))(*[batch.requests[int(i)] for i in good])
+        sub = np.zeros(max(len(good), 1), dtype=_REQUEST_DTYPE)
+        if len(good):
+            sub[:len(good)] = np.ctypeslib.as_array(batch.requests)[good]
         rows = self._respond_requests(sub, len(good), batch.filters, include_inactive, byte_limit, random_seed)
         out = [DropPacket(DROP_REASONS.get(int(st), "Invalid sync block")) for st in batch.status]
         for i, r in zip(good, rows):
@@ -675,7 +695,8 @@ class SyncCommunity(object):
         cap = 1 << 16
         while True:
             out = np.zeros(cap, dtype=np.uint64)
-            rc = ctx.lib.dsy_sync_respond(ctx.handle, st.handle, reqs, R, blob, len(blob), mt, len(metas),
+            rc = ctx.lib.dsy_sync_respond(ctx.handle, st.handle, reqs.ctypes.data_as(ctypes.POINTER(_native.Request)),
+                                          R, blob, len(blob), mt, len(metas),
                                           self.global_time, 1 if include_inactive else 0, int(byte_limit), seed,
                                           out.ctypes.data, cap, out_off.ctypes.data)
             if rc == _native.DSY_ECAPACITY and int(out_off[R]) > cap:

@@ -43,7 +43,8 @@ struct DevBuf {
     size_t bytes = 0;
 };
 
-enum TimerClass { kTimePairTest = 0, kTimeBuild = 1, kTimeSelect = 2, kTimeCompact = 3, kTimeClasses = 4 };
+enum TimerClass { kTimePairTest = 0, kTimeBuild = 1, kTimeSelect = 2, kTimeCompact = 3, kTimeSimBuild = 4,
+                  kTimeSimRespond = 5, kTimeClasses = 6 };
 
 struct PendingTimer {
     int cls;
@@ -61,12 +62,12 @@ struct dsy_ctx {
     uint32_t timing = 0;  // bit i: bracket class i with events
     std::vector<PendingTimer> pending;
     std::vector<hipEvent_t> event_pool;
-    double time_ms[kTimeClasses] = {0, 0, 0, 0};
-    uint64_t launches[kTimeClasses] = {0, 0, 0, 0};
-    uint64_t blocks[kTimeClasses] = {0, 0, 0, 0};
-    uint64_t bytes[kTimeClasses] = {0, 0, 0, 0};
-    uint64_t useful[kTimeClasses] = {0, 0, 0, 0};  // pairs the reference would have hashed (responder)
-    uint64_t slots[kTimeClasses] = {0, 0, 0, 0};   // lane-block slots of the hashing waves (load balance)
+    double time_ms[kTimeClasses] = {};
+    uint64_t launches[kTimeClasses] = {};
+    uint64_t blocks[kTimeClasses] = {};
+    uint64_t bytes[kTimeClasses] = {};
+    uint64_t useful[kTimeClasses] = {};  // pairs the reference would have hashed (responder)
+    uint64_t slots[kTimeClasses] = {};   // lane-block slots of the hashing waves (load balance)
     void* pinned = nullptr;  // small pinned staging for flags/counters
     uint64_t window_cap = 0; // dsy_ctx_set_window: upper bound on the responder's window (0: the default 2^18)
     void* stage = nullptr;   // grow-only pinned staging of the responder's uploads and status read-backs
@@ -1842,11 +1843,21 @@ int dsy_sim_build_claims(dsy_ctx* c, const dsy_sim_config* cfg, uint32_t round, 
     if ((rc = ws_get(c, "sim_slots", 4 * std::max<uint64_t>(cfg->peer_end - cfg->peer_begin, 1), &ds))) return rc;
     L.slots = (uint32_t*)ds;
     HIP_TRY(launch_sim(kSimClaimSlots, L));
+    void* dw;
+    if ((rc = ws_get(c, "sim_work", 32 * kSimTestedSlots, &dw))) return rc;
+    HIP_TRY(hipMemsetAsync(dw, 0, 32 * kSimTestedSlots, c->stream));
+    L.work = (unsigned long long*)dw;
     PendingTimer t;
-    timer_begin(c, &t, kTimeBuild);
+    timer_begin(c, &t, kTimeSimBuild);
     HIP_TRY(launch_sim(kSimBuild, L));
     timer_end(c, &t);
+    uint64_t* h = (uint64_t*)c->pinned + 256;
+    HIP_TRY(hipMemcpyAsync(h, dw, 32 * kSimTestedSlots, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    for (uint32_t i = 0; i < kSimTestedSlots; ++i) {
+        c->blocks[kTimeSimBuild] += h[4 * i];
+        c->slots[kTimeSimBuild] += h[4 * i + 1];
+    }
     timers_collect_lazy(c);
     return DSY_OK;
 }
@@ -1887,16 +1898,27 @@ int dsy_sim_respond(dsy_ctx* c, const dsy_sim_config* cfg, const uint8_t* d_ublo
     if ((rc = ws_get(c, "sim_slots", 4 * std::max<uint64_t>(n_claims, 1), &ds))) return rc;
     L.slots = (uint32_t*)ds;
     HIP_TRY(launch_sim(kSimRespSlots, L));
+    void* dw;
+    if ((rc = ws_get(c, "sim_work", 32 * kSimTestedSlots, &dw))) return rc;
+    HIP_TRY(hipMemsetAsync(dw, 0, 32 * kSimTestedSlots, c->stream));
+    L.work = (unsigned long long*)dw;
     PendingTimer t;
-    timer_begin(c, &t, kTimePairTest);
+    timer_begin(c, &t, kTimeSimRespond);
     HIP_TRY(launch_sim(kSimRespond, L));
     timer_end(c, &t);
     uint64_t* h = (uint64_t*)c->pinned + 128;
+    uint64_t* hw = (uint64_t*)c->pinned + 256;
     HIP_TRY(hipMemcpyAsync(h, dt, 8 * kSimTestedSlots, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(hw, dw, 32 * kSimTestedSlots, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     timers_collect_lazy(c);
     uint64_t tested = 0;
-    for (uint32_t i = 0; i < kSimTestedSlots; ++i) tested += h[i];
+    for (uint32_t i = 0; i < kSimTestedSlots; ++i) {
+        tested += h[i];
+        c->blocks[kTimeSimRespond] += hw[4 * i + 2];
+        c->slots[kTimeSimRespond] += hw[4 * i + 3];
+    }
+    c->useful[kTimeSimRespond] += tested;
     if (out_tested) *out_tested = tested;
     return DSY_OK;
 }

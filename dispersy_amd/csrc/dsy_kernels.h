@@ -279,6 +279,7 @@ struct SimLaunch {
     uint32_t* counts;
     unsigned long long* tested;
     unsigned long long* stats;
+    unsigned long long* work;  // [kSimTestedSlots][4]: build blocks, build lane-block slots, respond blocks, respond slots
     hipStream_t stream;
 };
 

@@ -130,6 +130,26 @@ __global__ void k_sim_resp_slots(dsy_sim_config c, const uint8_t* __restrict__ c
 
 static constexpr uint32_t kSimListCap = 2048;
 
+// per-wave work counters (compression blocks hashed; 64 x the longest lane's blocks = lane-block slots), spread
+// over kSimTestedSlots copies; one atomic pair per wave at its end
+__device__ __forceinline__ void wave_work(uint32_t lane_blocks, uint64_t& blocks, uint64_t& slots) {
+    uint32_t sum = lane_blocks, mx = lane_blocks;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        sum += __shfl_xor(sum, d, 64);
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
+    }
+    blocks += sum;
+    slots += 64ull * mx;
+}
+__device__ __forceinline__ void work_flush(unsigned long long* work, int which, uint64_t blocks, uint64_t slots) {
+    if (work && (threadIdx.x & 63) == 0) {
+        unsigned long long* w = work + ((blockIdx.x * 4 + (threadIdx.x >> 6)) & (kSimTestedSlots - 1)) * 4 + which;
+        atomicAdd(w, (unsigned long long)blocks);
+        atomicAdd(w + 1, (unsigned long long)slots);
+    }
+}
+
 // LDS of one requester wave in k_sim_build_claims: id list, the same ids sorted by block count, a 64-bin
 // histogram, the prefix byte and the filter (sized by m at launch)
 __host__ __device__ constexpr uint32_t sim_build_wave_lds(uint32_t nwords) {
@@ -143,7 +163,8 @@ __host__ __device__ constexpr uint32_t sim_build_wave_lds(uint32_t nwords) {
 template <class H, int CHUNK>
 __global__ void __launch_bounds__(256) k_sim_build_claims(dsy_sim_config c, uint32_t round, const uint8_t* __restrict__ ublob,
                                                           const uint64_t* __restrict__ uoff, const uint32_t* __restrict__ bits,
-                                                          uint8_t* __restrict__ out, const uint32_t* __restrict__ slots) {
+                                                          uint8_t* __restrict__ out, const uint32_t* __restrict__ slots,
+                                                          unsigned long long* __restrict__ work) {
     extern __shared__ __attribute__((aligned(16))) uint8_t sim_lds[];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t lp = (uint64_t)blockIdx.x * 4 + wv;
@@ -192,8 +213,10 @@ __global__ void __launch_bounds__(256) k_sim_build_claims(dsy_sim_config c, uint
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
+    uint64_t wblocks = 0, wslots = 0;
     for (uint32_t i0 = 0; i0 < n; i0 += 64) {
         const uint32_t i = i0 + lane;
+        wave_work(i < n ? n_blocks(1 + (uint32_t)(uoff[sorted[i] + 1] - uoff[sorted[i]]), blk, lenb) : 0u, wblocks, wslots);
         if (i < n) {
             const uint32_t id = sorted[i];
             KeyView kv{ublob + uoff[id], (uint32_t)(uoff[id + 1] - uoff[id]), pre, 1};
@@ -210,6 +233,7 @@ __global__ void __launch_bounds__(256) k_sim_build_claims(dsy_sim_config c, uint
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
+    work_flush(work, 0, wblocks, wslots);
     const uint64_t q = sim_partner(c, round, p);
     uint8_t* rec = out + (uint64_t)slots[lp] * c.claim_bytes;
     if (lane == 0) {
@@ -243,7 +267,8 @@ __global__ void __launch_bounds__(256) k_sim_respond(dsy_sim_config c, const uin
                                                      const uint64_t* __restrict__ uoff, const uint32_t* __restrict__ bits,
                                                      const uint8_t* __restrict__ claims, uint64_t n_claims,
                                                      uint8_t* __restrict__ out, const uint32_t* __restrict__ slots,
-                                                     unsigned long long* __restrict__ tested) {
+                                                     unsigned long long* __restrict__ tested,
+                                                     unsigned long long* __restrict__ work) {
     __shared__ uint16_t lists[4][kSimListCap];
     __shared__ uint32_t filt[4][kSimFilterWordsMax];
     __shared__ uint8_t pre[4][4];
@@ -264,11 +289,14 @@ __global__ void __launch_bounds__(256) k_sim_respond(dsy_sim_config c, const uin
     uint32_t sent = 0;
     int64_t spent = 0;
     uint32_t ntested = 0;
+    uint64_t wblocks = 0, wslots = 0;
     for (uint32_t i0 = 0; i0 < n; i0 += 64) {
         const uint32_t i = i0 + lane;
         const uint32_t id = i < n ? lists[wv][i] : 0u;
         // range [1, time_high]: global_time = id + 1
         const bool sel = i < n && (uint64_t)id + 1 <= h.time_high;
+        wave_work(sel ? n_blocks(1 + (uint32_t)(uoff[id + 1] - uoff[id]), H::block_bytes, H::len_bytes) : 0u, wblocks,
+                  wslots);
         bool miss = false;
         int64_t len = 0;
         if (sel) {
@@ -304,6 +332,7 @@ __global__ void __launch_bounds__(256) k_sim_respond(dsy_sim_config c, const uin
         sent += nin;
         if (sent > 0 && spent >= c.byte_limit) break;
     }
+    work_flush(work, 2, wblocks, wslots);
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
     uint8_t* o = out + (uint64_t)slots[ci] * c.resp_bytes;
@@ -354,11 +383,11 @@ static hipError_t sim_family(int op, const SimLaunch& L) {
         if (!local) return hipSuccess;
         const size_t lds = 4 * (size_t)sim_build_wave_lds((uint32_t)((L.cfg.m_bits + 31) / 32));
         hipLaunchKernelGGL((k_sim_build_claims<H, CHUNK>), dim3((uint32_t)((local + 3) / 4)), dim3(256), lds, L.stream, L.cfg,
-                           L.round, L.ublob, L.uoff, L.bits, L.out, L.slots);
+                           L.round, L.ublob, L.uoff, L.bits, L.out, L.slots, L.work);
     } else {
         if (!L.n_in) return hipSuccess;
         hipLaunchKernelGGL((k_sim_respond<H, CHUNK>), dim3((uint32_t)((L.n_in + 3) / 4)), dim3(256), 0, L.stream, L.cfg,
-                           L.ublob, L.uoff, L.bits, L.in, L.n_in, L.out, L.slots, L.tested);
+                           L.ublob, L.uoff, L.bits, L.in, L.n_in, L.out, L.slots, L.tested, L.work);
     }
     return hipGetLastError();
 }

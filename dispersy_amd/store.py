@@ -87,6 +87,8 @@ class SyncStore(object):
         self._empty = np.zeros(0, dtype=np.int64)
         self._groups = None  # (meta, member) -> rows, built on first use (member_rows)
         self._gpending = {}
+        self._blob_base = 0  # offsets[] of the host blob's first byte (attach: earlier packets are device-only)
+        self._owns_handle = True
 
     # ------------------------------------------------------------------------------------------ columns
     def _col(self, name):
@@ -130,6 +132,20 @@ class SyncStore(object):
         return cls.from_rows([(i, g, m, u, bytes(p), mb, sq) for i, g, m, u, p, mb, _, sq in rows], ctx=ctx,
                              communities={r[6] for r in rows} if rows else ({community} if community is not None else None))
 
+    @classmethod
+    def attach(cls, ctx, handle, global_time, meta, lengths, member=None):
+        """A store exported straight into HBM (dsy_store_attach / dsy_store_upload made by the caller): the host keeps
+        the small columns only (rows in index order, all live), the packets of these rows stay on the device --
+        packet() serves only rows appended later.  `handle` is the dsy_store* (the caller keeps ownership)."""
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint64)
+        offsets = np.zeros(len(lengths) + 1, dtype=np.uint64)
+        np.cumsum(lengths, out=offsets[1:])
+        st = cls(bytearray(), offsets, global_time, meta, ctx=ctx, member=member)
+        st._blob_base = int(offsets[-1])
+        st._handle = handle if isinstance(handle, ctypes.c_void_p) else ctypes.c_void_p(handle)
+        st._owns_handle = False
+        return st
+
     # --------------------------------------------------------------------------------------- accessors
     def packet(self, i):
         if self._replaced:
@@ -137,7 +153,9 @@ class SyncStore(object):
             if p is not None:
                 return p
         off = self._buf["offsets"]
-        a, b = int(off[i]), int(off[i + 1])
+        a, b = int(off[i]) - self._blob_base, int(off[i + 1]) - self._blob_base
+        if a < 0:
+            raise KeyError("row %d's packet lives only on the device (SyncStore.attach)" % int(i))
         return bytes(self.blob[a:b])
 
     def packets(self, rows):
@@ -235,7 +253,7 @@ class SyncStore(object):
             lib = self.ctx.lib
             _native.check(lib.dsy_store_append(self.ctx.handle, self._handle, data, len(data), new_off.ctypes.data, a,
                                                gts.ctypes.data, metas.ctypes.data,
-                                               mem.ctypes.data if self._dup_indexed else None))
+                                               mem.ctypes.data if mem is not None else None))
         # host columns: geometric growth, O(batch) per append
         b = self._buf
         b["offsets"] = _room(b["offsets"], n0 + 1, n0 + a + 1)
@@ -430,7 +448,7 @@ class SyncStore(object):
         return self._handle
 
     def close(self):
-        if self._handle is not None and self._ctx is not None and self._ctx.handle:
+        if self._handle is not None and self._owns_handle and self._ctx is not None and self._ctx.handle:
             self._ctx.lib.dsy_store_free(self._handle)
         self._handle = None
 

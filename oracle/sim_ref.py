@@ -42,10 +42,23 @@ CLAIM_HDR = struct.Struct("<QQQII")
 RESP_HDR = struct.Struct("<QII")
 
 
+class _NumpyBuffers(object):
+    """The two torch calls the engine makes, over numpy (bench.py's forked CPU workers stay out of torch)."""
+
+    @staticmethod
+    def frombuffer(buf, dtype=None):
+        return np.frombuffer(buf, dtype=np.uint8)
+
+    uint8 = None
+
+
 class OracleEngine(object):
-    def __init__(self, cfg, blob, offsets):
-        import torch
-        self.torch = torch
+    def __init__(self, cfg, blob, offsets, arrays="torch"):
+        if arrays == "torch":
+            import torch
+            self.torch = torch
+        else:
+            self.torch = _NumpyBuffers
         self.c = cfg
         self.packets = [blob[int(offsets[i]):int(offsets[i + 1])] for i in range(cfg.universe)]
         self.local = cfg.peer_end - cfg.peer_begin
@@ -87,10 +100,18 @@ class OracleEngine(object):
             CLAIM_HDR.pack_into(buf, at, p, q, time_high, pre, len(ids))
             raw = bf.to_bytes()
             buf[at + 32:at + 32 + len(raw)] = raw
-        return self.torch.frombuffer(buf, dtype=self.torch.uint8).clone()
+        return self._out(buf)
+
+    def _out(self, buf):
+        t = self.torch.frombuffer(buf, dtype=self.torch.uint8)
+        return t.copy() if isinstance(t, np.ndarray) else t.clone()
+
+    @staticmethod
+    def _raw(t):
+        return (t if isinstance(t, np.ndarray) else t.numpy()).tobytes()
 
     def _claims(self, claims, n):
-        raw = claims.numpy().tobytes()
+        raw = self._raw(claims)
         for i in range(n):
             at = i * self.c.claim_bytes
             yield CLAIM_HDR.unpack_from(raw, at), raw[at + 32:at + 32 + self.c.m_bits // 8]
@@ -125,10 +146,10 @@ class OracleEngine(object):
             cursor[d] += 1
             RESP_HDR.pack_into(buf, at, req, min(len(sent), 64), int(len(sent) > 64))
             struct.pack_into("<%dH" % min(len(sent), 64), buf, at + 16, *sent[:64])
-        return self.torch.frombuffer(buf, dtype=self.torch.uint8).clone(), tested[0]
+        return self._out(buf), tested[0]
 
     def merge(self, resps, n):
-        raw = resps.numpy().tobytes()
+        raw = self._raw(resps)
         for i in range(n):
             at = i * self.c.resp_bytes
             req, cnt, ovf = RESP_HDR.unpack_from(raw, at)
