@@ -126,6 +126,7 @@ def main():
 
     from dispersy_amd import _native
     from dispersy_amd.bloomfilter import BloomFilter
+    from dispersy_amd.shard import Collectives
 
     ctx = _native.Context(torch.cuda.current_device())
     lib = ctx.lib
@@ -228,12 +229,9 @@ def main():
     sel = ctx.kernel_time(_native.TIME_SELECT)
     cmp_ = ctx.kernel_time(_native.TIME_COMPACT)
     if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        p = torch.tensor([total_pairs], device=dev, dtype=torch.int64)
-        dist.all_reduce(p, op=dist.ReduceOp.SUM)
-        total_pairs = int(p.item())
+        coll = Collectives(dist)
+        elapsed = float(coll.scalar(elapsed, "max", device=dev))
+        total_pairs = int(coll.scalar(int(total_pairs), "sum", device=dev))
 
     # ---------------------------------------------------------------- roofline of the dominant kernel
     launches = max(kt["launches"], 1)
@@ -269,9 +267,7 @@ def main():
     useful = work["useful_pairs"]
     roofline["lane_utilization"] = round(work["blocks"] / max(work["lane_slots"], 1), 4)
     if dist:
-        u = torch.tensor([useful], device=dev, dtype=torch.int64)
-        dist.all_reduce(u, op=dist.ReduceOp.SUM)
-        useful = int(u.item())
+        useful = int(coll.scalar(int(useful), "sum", device=dev))
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_claims > 0:
@@ -713,10 +709,8 @@ def gossip_sim(args, ctx, dev, rank, world, dist):
                            if secs else None},
             "lane_utilization": round(wk["blocks"] / max(wk["lane_slots"], 1), 4),
             "blocks_per_round": int(wk["blocks"] / max(args.sim_rounds, 1))}
-    if dist:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+    if sim.coll is not None:
+        dt = float(sim.coll.scalar(dt, "max", device=dev))
     held, chk = sim.global_stats()
     return {"metric": "gossip sync rounds/sec", "value": round(args.sim_rounds / dt, 3), "unit": "rounds/s",
             "n_gpus": world, "scaling": "strong", "rounds": args.sim_rounds, "warmup_rounds": args.sim_warmup,
@@ -867,6 +861,7 @@ def large_filter(args, ctx, lib, dev, rank, world, dist=None):
     rank then probes with its own test packets."""
     import torch
     from dispersy_amd.bloomfilter import BloomFilter
+    from dispersy_amd.shard import Collectives, union_filter
     G = _native.BLOB_GUARD
     n_add, n_test = args.large_keys, args.large_tests
     n = n_add + n_test
@@ -897,29 +892,22 @@ def large_filter(args, ctx, lib, dev, rank, world, dist=None):
         union = None
         if dist is not None and world > 1:
             # the whole build as a job: every rank adds its shard, then all-gather + OR of the partial filters
-            words = filt.numel()
-            parts = torch.empty(world * words, dtype=torch.int32, device=dev)
-            union = torch.empty_like(filt)
+            coll = Collectives(dist)
             filt.zero_()
             torch.cuda.synchronize()
-            dist.barrier()
+            coll.barrier()
             t0 = time.perf_counter()
             add()
-            ctx.synchronize()
-            dist.all_gather_into_tensor(parts, filt)
-            torch.cuda.synchronize()
-            _native.check(lib.dsy_filter_or_reduce(ctx.handle, parts.data_ptr(), world, words, union.data_ptr()))
-            ctx.synchronize()
-            t_job = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
-            dist.all_reduce(t_job, op=dist.ReduceOp.MAX)
+            union = union_filter(ctx, coll, filt)
+            t_job = coll.scalar(time.perf_counter() - t0, "max", device=dev)
             filt.copy_(union)
             torch.cuda.synchronize()
         k_test, _ = _timed_bloom(ctx, test, 3)
-        ones = int(torch.bitwise_count(filt).sum().item()) if hasattr(torch, "bitwise_count") else None
+        ones = int(np.unpackbits(filt.cpu().numpy().view(np.uint8)[:m // 8]).sum())
         if union is not None:
             out.setdefault("sharded_build", {})["2^%d" % bits] = {
-                "ranks": world, "keys_all_ranks": world * n_add, "job_s": round(float(t_job.item()), 4),
-                "add_keys_per_s_all_ranks": round(world * n_add / float(t_job.item()), 1),
+                "ranks": world, "keys_all_ranks": world * n_add, "job_s": round(t_job, 4),
+                "add_keys_per_s_all_ranks": round(world * n_add / t_job, 1),
                 "exchange": "RCCL all_gather_into_tensor of %d x %d B partial filters + dsy_filter_or_reduce"
                             % (world, 4 * filt.numel())}
         out["filters"]["2^%d" % bits] = {

@@ -107,7 +107,10 @@ __global__ void __launch_bounds__(256) k_len_scatter(LenSort s, const uint64_t* 
 
 // ------------------------------------------------------------------------------------- hash + probe / set
 // OP 0: add (OR k bits per key into the filter), OP 1: test (present[key] = all k bits set).
-template <class H, int CHUNK, int OP, bool DMA>
+// DIAG (DMA path, 2-byte chunks only): 0 = the product kernel; 1 = no packet loads (the stage is hashed as left in
+// LDS: the compute ceiling); 2 = packet loads without the compression (the gather ceiling).  Diagnostics only, selected
+// by the ctx's DSY_BLOOM_DIAG environment knob (tools/hash_sweep.py); results are meaningless for DIAG != 0.
+template <class H, int CHUNK, int OP, bool DMA, int DIAG = 0>
 __global__ void __launch_bounds__(256) k_bloom(const DevParams* __restrict__ prm, const uint8_t* __restrict__ blob,
                                                const uint64_t* __restrict__ offsets, const uint64_t* __restrict__ rows,
                                                const RowRec* __restrict__ rec, const PairTask* __restrict__ tasks, uint64_t n,
@@ -147,7 +150,7 @@ __global__ void __launch_bounds__(256) k_bloom(const DevParams* __restrict__ prm
             }
         }
         H st;
-        if constexpr (DMA) hash_key_dma_reg<H, kDmaS>(kv, st, my_dma);
+        if constexpr (DMA) hash_key_dma_reg<H, kDmaS, DIAG>(kv, st, my_dma);
         else hash_key<H>(kv, st);
         if (active) {
             uint32_t ok = 1;
@@ -255,6 +258,14 @@ static hipError_t launch_op(const BloomLaunch& L, uint32_t grid) {
                      (!L.use_lds || L.nwords * 4 <= 16 * 1024);
     const size_t lds = (dma ? 4 * kDmaWaveBytes : 0) + (L.use_lds ? (size_t)L.nwords * 4 : 0);
     if (dma) {
+        if constexpr (H::block_bytes == 64 && CHUNK == 2) {
+            if (L.diag == 1 || L.diag == 2) {
+                auto kern = L.diag == 1 ? k_bloom<H, CHUNK, OP, true, 1> : k_bloom<H, CHUNK, OP, true, 2>;
+                hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, L.stream, L.prm, L.blob, L.offsets, L.rows, L.rec,
+                                   L.tasks, L.n, L.filter, L.nwords, L.use_lds, L.present);
+                return hipGetLastError();
+            }
+        }
         if constexpr (H::block_bytes == 64)
             hipLaunchKernelGGL((k_bloom<H, CHUNK, OP, true>), dim3(grid), dim3(256), lds, L.stream, L.prm, L.blob,
                                L.offsets, L.rows, L.rec, L.tasks, L.n, L.filter, L.nwords, L.use_lds, L.present);

@@ -59,6 +59,7 @@ struct dsy_ctx {
     std::mutex mu;
     std::map<std::string, DevBuf> ws;
     uint32_t max_grid = 2048;
+    int bloom_diag = 0;  // DSY_BLOOM_DIAG at creation: single-filter ceiling diagnostics (k_bloom DIAG)
     uint32_t timing = 0;  // bit i: bracket class i with events
     std::vector<PendingTimer> pending;
     std::vector<hipEvent_t> event_pool;
@@ -287,6 +288,7 @@ int run_bloom(dsy_ctx* c, BloomOp op, const dsy_bloom_params* p, const uint8_t* 
     L.indices = d_idx;
     L.max_grid = c->max_grid;
     L.stream = c->stream;
+    L.diag = c->bloom_diag;
     // Large batches hash in length-bucketed order (a wave's 64 lanes then run the same number of blocks); the
     // sort costs ~40 B of traffic per key next to the key bytes themselves.
     if (op != BloomOp::Indices && n >= kLenSortMin) {
@@ -346,6 +348,7 @@ int dsy_ctx_create(int device, dsy_ctx** out) {
     int cus = 256;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     c->max_grid = (uint32_t)std::max(cus, 1) * 8;
+    if (const char* v = getenv("DSY_BLOOM_DIAG")) c->bloom_diag = atoi(v);
     hipHostMalloc(&c->pinned, 4096, hipHostMallocDefault);
     *out = c;
     return DSY_OK;

@@ -53,6 +53,7 @@ struct BloomLaunch {
     uint64_t* indices;
     uint32_t max_grid;
     hipStream_t stream;
+    int diag;               // k_bloom DIAG: 0 = the product kernel, 1 / 2 = compute / gather ceiling diagnostics
 };
 
 hipError_t launch_bloom(const BloomLaunch& L);

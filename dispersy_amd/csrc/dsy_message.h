@@ -199,6 +199,45 @@ struct DmaGeometry {
 // kDmaPrio -- raise the wave's issue priority while it issues a stage's loads.
 enum { kDmaSkipDead = 1, kDmaPrio = 2 };
 
+// Message words of block b as loaded (little-endian, x[16]) -> the hash's input: the bytes past the message
+// zeroed, the 0x80 terminator placed, byte-swapped for the big-endian hashes, the bit length in the final block.
+// `full` (wave-uniform) says every lane's block lies wholly inside its message -- the common case with
+// length-sorted lanes --, which leaves only the byte swap: no per-word compares or exec-mask branches.  The
+// partial path is branch-free too (selects), so lanes of one wave with different lengths do not diverge.
+template <class H>
+__device__ __forceinline__ void finish_block(uint32_t* x, uint32_t o0, uint32_t total, bool last, bool full) {
+    if (!full) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int rel = (int)total - (int)o0 - 4 * i;  // message bytes left at word i
+            const uint32_t sh = (uint32_t)(rel & 3) * 8u;
+            const uint32_t part = (x[i] & ((1u << sh) - 1u)) | (0x80u << sh);
+            x[i] = rel >= 4 ? x[i] : (rel < 0 ? 0u : part);
+        }
+    }
+    if (H::big_endian) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[i] = bswap32(x[i]);
+    }
+    if (!full) {
+        const uint64_t bits = (uint64_t)total * 8u;
+        if (H::big_endian) {
+            x[14] = last ? (uint32_t)(bits >> 32) : x[14];
+            x[15] = last ? (uint32_t)bits : x[15];
+        } else {
+            x[14] = last ? (uint32_t)bits : x[14];
+            x[15] = last ? (uint32_t)(bits >> 32) : x[15];
+        }
+    }
+}
+
+// wave minimum of a lane value
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, d, 64));
+    return v;
+}
+
 template <class H, int S = 2, int NB = 2, int FLAGS = 0>
 __device__ __forceinline__ void hash_key_dma(const KeyView& kv, H& st, uint8_t* lds_wave) {
     static_assert(H::block_bytes == 64, "LDS-DMA staging is for 64-byte blocks");
@@ -211,6 +250,7 @@ __device__ __forceinline__ void hash_key_dma(const KeyView& kv, H& st, uint8_t* 
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, d, 64));
     const uint32_t nst = (nbmax + S - 1) / S;
+    const uint32_t tmin = wave_min_u32(total);
     uint32_t preword = 0;
     for (uint32_t j = 0; j < r; ++j) preword |= (uint32_t)kv.pre[j] << (8 * j);
     const uint64_t base = (uint64_t)(uintptr_t)kv.key - r;  // window of block b starts at base + 64 b
@@ -262,23 +302,7 @@ __device__ __forceinline__ void hash_key_dma(const KeyView& kv, H& st, uint8_t* 
             if (b < nb) {
                 const uint32_t o0 = b * 64;
                 if (b == 0 && r) w[0] = (w[0] & ~low_bytes_mask(r)) | preword;
-                if (o0 + 64 > total) {
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const int rel = (int)total - (int)o0 - 4 * i;
-                        if (rel <= 0) w[i] = rel == 0 ? 0x80u : 0u;
-                        else if (rel < 4) w[i] = (w[i] & ((1u << (8 * rel)) - 1u)) | (0x80u << (8 * rel));
-                    }
-                }
-                if (H::big_endian) {
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) w[i] = bswap32(w[i]);
-                }
-                if (b + 1 == nb) {
-                    const uint64_t bits = (uint64_t)total * 8u;
-                    if (H::big_endian) { w[14] = (uint32_t)(bits >> 32); w[15] = (uint32_t)bits; }
-                    else { w[14] = (uint32_t)bits; w[15] = (uint32_t)(bits >> 32); }
-                }
+                finish_block<H>(w, o0, total, b + 1 == nb, o0 + 64 <= tmin);
                 st.compress(w);
             }
         }
@@ -291,7 +315,9 @@ __device__ __forceinline__ void hash_key_dma(const KeyView& kv, H& st, uint8_t* 
 // copied to registers as soon as it lands, and the next stage's DMA into the same buffer is issued before the
 // blocks are compressed from the registers.  Half the LDS of the double-buffered form for the same amount in
 // flight, so twice the waves fit a CU.  Dead lanes (key already ended) issue nothing; every wait is vmcnt(0).
-template <class H, int S = 1>
+// MODE (k_bloom DIAG diagnostics only): 0 = the product path, 1 = no packet loads (compress whatever the LDS buffer holds),
+// 2 = loads only (no compress)
+template <class H, int S = 1, int MODE = 0>
 __device__ __forceinline__ void hash_key_dma_reg(const KeyView& kv, H& st, uint8_t* lds_wave) {
     static_assert(H::block_bytes == 64, "LDS-DMA staging is for 64-byte blocks");
     using G = DmaGeometry<S, 1>;
@@ -303,6 +329,7 @@ __device__ __forceinline__ void hash_key_dma_reg(const KeyView& kv, H& st, uint8
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, d, 64));
     const uint32_t nst = (nbmax + S - 1) / S;
+    const uint32_t tmin = wave_min_u32(total);
     uint32_t preword = 0;
     for (uint32_t j = 0; j < r; ++j) preword |= (uint32_t)kv.pre[j] << (8 * j);
     const uint64_t base = (uint64_t)(uintptr_t)kv.key - r;
@@ -314,7 +341,7 @@ __device__ __forceinline__ void hash_key_dma_reg(const KeyView& kv, H& st, uint8
             const uint32_t pend = __shfl((int)total, p, 64);
             const uint32_t c = ((lane % G::kChunks) + ((uint32_t)p >> G::kShift)) % G::kChunks;
             const uint64_t b64 = ((uint64_t)bhi << 32) | blo;
-            if (s * (S * 64) < pend)
+            if (MODE != 1 && s * (S * 64) < pend)
                 __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)(b64 + s * (S * 64) + 16 * c),
                                                  (__attribute__((address_space(3))) void*)(lds_wave + i * 1024), 16, 0, 0);
         }
@@ -346,24 +373,9 @@ __device__ __forceinline__ void hash_key_dma_reg(const KeyView& kv, H& st, uint8
                 uint32_t* x = w[bb];
                 const uint32_t o0 = b * 64;
                 if (b == 0 && r) x[0] = (x[0] & ~low_bytes_mask(r)) | preword;
-                if (o0 + 64 > total) {
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const int rel = (int)total - (int)o0 - 4 * i;
-                        if (rel <= 0) x[i] = rel == 0 ? 0x80u : 0u;
-                        else if (rel < 4) x[i] = (x[i] & ((1u << (8 * rel)) - 1u)) | (0x80u << (8 * rel));
-                    }
-                }
-                if (H::big_endian) {
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) x[i] = bswap32(x[i]);
-                }
-                if (b + 1 == nb) {
-                    const uint64_t bits = (uint64_t)total * 8u;
-                    if (H::big_endian) { x[14] = (uint32_t)(bits >> 32); x[15] = (uint32_t)bits; }
-                    else { x[14] = (uint32_t)bits; x[15] = (uint32_t)(bits >> 32); }
-                }
-                st.compress(x);
+                finish_block<H>(x, o0, total, b + 1 == nb, o0 + 64 <= tmin);
+                if (MODE != 2) st.compress(x);
+                else st.h[0] ^= x[0] ^ x[5] ^ x[10] ^ x[15];
             }
         }
     }
@@ -389,6 +401,7 @@ __device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uin
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, d, 64));
     const uint32_t nst = (nbmax + 1) / 2;
+    const uint32_t tmin = wave_min_u32(total);
     uint32_t preword = 0;
     for (uint32_t j = 0; j < r; ++j) preword |= (uint32_t)kv.pre[j] << (8 * j);
     const uint64_t base = (uint64_t)(uintptr_t)kv.key;  // 128-byte aligned
@@ -443,23 +456,7 @@ __device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uin
                     for (int i = 0; i < 16; ++i) x[i] = __builtin_amdgcn_alignbyte(d[1 + 16 * bb + i], d[16 * bb + i], sh);
                 }
                 const uint32_t o0 = b * 64;
-                if (o0 + 64 > total) {
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const int rel = (int)total - (int)o0 - 4 * i;
-                        if (rel <= 0) x[i] = rel == 0 ? 0x80u : 0u;
-                        else if (rel < 4) x[i] = (x[i] & ((1u << (8 * rel)) - 1u)) | (0x80u << (8 * rel));
-                    }
-                }
-                if (H::big_endian) {
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) x[i] = bswap32(x[i]);
-                }
-                if (b + 1 == nb) {
-                    const uint64_t bits = (uint64_t)total * 8u;
-                    if (H::big_endian) { x[14] = (uint32_t)(bits >> 32); x[15] = (uint32_t)bits; }
-                    else { x[14] = (uint32_t)bits; x[15] = (uint32_t)(bits >> 32); }
-                }
+                finish_block<H>(x, o0, total, b + 1 == nb, o0 + 64 <= tmin);
                 st.compress(x);
             }
         }

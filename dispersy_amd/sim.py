@@ -24,6 +24,7 @@ import numpy as np
 
 from . import _native
 from .bloomfilter import BloomFilter
+from .shard import Collectives
 
 
 class SimConfig(ctypes.Structure):
@@ -134,6 +135,7 @@ class EpidemicSim(object):
 
     def __init__(self, engine, cfg, rank=0, world=1, dist=None, device=None):
         self.e, self.cfg, self.rank, self.world, self.dist = engine, cfg, rank, world, dist
+        self.coll = Collectives(dist) if dist is not None and world > 1 else None
         self.device = device
         self.tested = 0
         self.exchanged_bytes = 0
@@ -144,7 +146,7 @@ class EpidemicSim(object):
         import torch
         send = torch.tensor(counts, dtype=torch.int64, device=self.device)
         recv = torch.empty_like(send)
-        self.dist.all_to_all_single(recv, send)
+        self.coll.all_to_all_single(recv, send)
         return recv.cpu().numpy()
 
     def _alltoall_records(self, buf, send_counts, recv_counts, rec_bytes):
@@ -159,8 +161,7 @@ class EpidemicSim(object):
             buf = buf[:0]
         else:
             buf = buf[:sum(in_splits)]
-        self.dist.all_to_all_single(out[:sum(out_splits)] if sum(out_splits) else out[:0], buf,
-                                    output_split_sizes=out_splits, input_split_sizes=in_splits)
+        self.coll.all_to_all_single(out[:sum(out_splits)] if sum(out_splits) else out[:0], buf, out_splits, in_splits)
         if self.device is not None and self.device.type == "cuda":
             torch.cuda.current_stream(self.device).synchronize()
         self.exchanged_bytes += sum(in_splits)
@@ -188,11 +189,10 @@ class EpidemicSim(object):
         if self.world == 1:
             return held, chk
         import torch
-        t = torch.tensor([held], dtype=torch.int64, device=self.device)
-        self.dist.all_reduce(t)
-        parts = [torch.zeros(1, dtype=torch.int64, device=self.device) for _ in range(self.world)]
-        self.dist.all_gather(parts, torch.tensor([chk & 0x7fffffffffffffff], dtype=torch.int64, device=self.device))
+        held = self.coll.scalar(held, "sum", device=self.device)
+        parts = torch.zeros(self.world, dtype=torch.int64, device=self.device)
+        self.coll.all_gather_into(parts, torch.tensor([chk], dtype=torch.int64, device=self.device))
         x = 0
-        for p in parts:
-            x ^= int(p.item())
-        return int(t.item()), x
+        for p in parts.tolist():
+            x ^= int(p)
+        return int(held), x

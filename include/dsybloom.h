@@ -109,8 +109,9 @@ int dsy_ctx_synchronize(dsy_ctx* ctx);
 void* dsy_ctx_stream(dsy_ctx* ctx);
 /* Kernel timing: when enabled, HIP events bracket every launch of the hash kernels on the ctx stream.
  * dsy_ctx_kernel_time returns the accumulated milliseconds and launch count of kernel class `which`
- * (0 = hash/test of the responder, 1 = single-filter bloom kernels, 2 = selection, 3 = compaction) and, for
- * class 0, the algorithmic work those launches did: compression blocks and packet bytes hashed.
+ * (0 = hash/test of the responder, 1 = single-filter bloom kernels, 2 = selection, 3 = compaction, 4 = the
+ * simulator's claim build, 5 = the simulator's respond) and, for classes 0, 4 and 5, the algorithmic work those
+ * launches did: compression blocks and packet bytes hashed.
  * enable: 0 off, 1 every class, or DSY_TIME_ONLY(mask) to bracket only the classes whose bit is set in mask (each
  * event pair is a marker packet on the stream: timing just the dominant kernel keeps the others' dispatch tight). */
 #define DSY_TIME_ONLY(mask) (0x100 | ((mask)&0xff))

@@ -185,3 +185,28 @@ def test_filter_or_reduce_is_the_union_of_shards():
         ref.add_keys(keys)
         got = d_out.cpu().numpy().tobytes()[:m // 8]
         assert got == whole.bytes == ref.to_bytes()
+
+
+def test_largest_filter_2_24_against_oracle():
+    """cfg4's largest filter, BloomFilter(2**24, 0.01, b"\\x07") (SHA-256, 'L' chunks, k = 7): 200 k adds and 100 k
+    probes against the oracle's bit positions (OracleBloom.indices, bloomfilter.py:150-160).  The positions are set
+    in a numpy byte array in the filter's little-endian bit order (bloomfilter.py:288-298): the oracle's big-int OR
+    costs O(m) per bit at 2 MB."""
+    m = 1 << 24
+    blob, off = random_packets(2424, 300_000, 100, 1500)
+    n_add = 200_000
+    bf = BloomFilter(m, 0.01, b"\x07")
+    assert (bf.hash_name, bf.functions, bf.chunk_bytes) == ("sha256", 7, 4)
+    bf.add_packed(blob[:int(off[n_add])], off[:n_add + 1])
+    ref = OracleBloom.from_m_f(m, 0.01, b"\x07")
+    pos = np.array([p for i in range(n_add) for p in ref.indices(blob[int(off[i]):int(off[i + 1])])], dtype=np.int64)
+    want = np.zeros(m // 8, dtype=np.uint8)
+    np.bitwise_or.at(want, pos >> 3, (1 << (pos & 7)).astype(np.uint8))
+    assert bf.bytes == want.tobytes()
+    assert bf.bits_checked == int(np.unpackbits(want).sum())
+    probes = [blob[int(off[i]):int(off[i + 1])] for i in range(n_add - 1000, len(off) - 1)]
+    got = bf.contains_many(probes)
+    bits = np.unpackbits(want, bitorder="little")
+    expect = [all(bits[p] for p in ref.indices(k)) for k in probes]
+    assert got.astype(bool).tolist() == expect
+    assert got[:1000].all() and sum(expect[1000:]) < 10

@@ -1,0 +1,76 @@
+"""The sharded jobs (dispersy_amd/shard.py) with two ranks on the MI355X: tests/shard_worker.py is
+started twice as a child process (gloo over 127.0.0.1, both ranks on cuda:0 -- the exchange is staged through host
+memory, the hashing, OR-reduce, responder and simulator kernels run on the GPU), and every job must equal the
+single-process run: cfg4's union filter bytes (MD5, SHA-1, SHA-256 at 2^20 and 2^24), cfg2's answers in claim
+order, cfg3's per-round (packets held, checksum) history."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.fixture(scope="module")
+def two_ranks(tmp_path_factory):
+    tmp = tmp_path_factory.mktemp("shard")
+    port = str(_free_port())
+    procs, outs = [], []
+    for rank in range(2):
+        out = str(tmp / ("rank%d.json" % rank))
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=port, SHARD_OUT=out)
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "shard_worker.py")], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+        outs.append(out)
+    logs = []
+    for p in procs:
+        try:
+            logs.append(p.communicate(timeout=100)[0].decode(errors="replace"))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    for p, log in zip(procs, logs):
+        assert p.returncode == 0, log[-3000:]
+    res = []
+    for out in outs:
+        with open(out) as f:
+            res.append(json.load(f))
+    return res
+
+
+def test_cfg4_union_equals_single_build(two_ranks):
+    r0, r1 = two_ranks
+    for name, row in r0["cfg4"].items():
+        assert row["equal_single"], name
+        assert row["sha"] == r1["cfg4"][name]["sha"], name  # every rank holds the same union
+        assert row["bits"] >= max(row["partial_bits"], r1["cfg4"][name]["partial_bits"]), name
+
+
+def test_cfg2_claims_sharded_equal_single(two_ranks):
+    r0, r1 = two_ranks
+    assert r0["cfg2"]["equal_single"]
+    assert r0["cfg2"]["claims"][1] == r1["cfg2"]["claims"][0] and r1["cfg2"]["claims"][1] == 48
+    assert r0["cfg2"]["rows_sent"] + r1["cfg2"]["rows_sent"] == r0["cfg2"]["rows_all"] > 0
+
+
+def test_cfg3_sim_two_ranks_equal_one(two_ranks):
+    r0, r1 = two_ranks
+    assert r0["cfg3"]["equal_single"]
+    assert r0["cfg3"]["history"] == r1["cfg3"]["history"]
+    assert r0["cfg3"]["history"][-1][0] > r0["cfg3"]["history"][0][0]
+    assert r0["cfg3"]["exchanged_bytes"] > 0 and r1["cfg3"]["exchanged_bytes"] > 0
