@@ -98,7 +98,7 @@ def parse():
     ap.add_argument("--sim-initial", type=int, default=100)
     ap.add_argument("--sim-rounds", type=int, default=10)
     ap.add_argument("--sim-warmup", type=int, default=2)
-    ap.add_argument("--extra", default="claim,dropin,dedup,ingest,1,3,4,5",
+    ap.add_argument("--extra", default="claim,dropin,dedup,ingest,sha1,1,3,4,5",
                     help="BASELINE configs measured beside the headline (config 2): 1 single filter, 3 gossip "
                          "simulator, 4 large filters, 5 heavy-tailed packets, ingest: received packets appended to "
                          "the headline store, dedup: duplicate check of received packets against it, claim: modulo and "
@@ -151,40 +151,9 @@ def main():
 
     # ---------------------------------------------------------------- the claims (seed 7 + rank)
     rng = np.random.Generator(np.random.PCG64(args.seed + 1000 * rank))
+    reqs, claims, fblob, d_filters, capacity = make_claims(ctx, lib, store, N, R, rng, args.filter_bits,
+                                                           args.error_rate, None, dev)
     cap_probe = BloomFilter(args.filter_bits, args.error_rate)
-    capacity = cap_probe.get_capacity(args.error_rate)
-    modulo_m = int(math.ceil(N / float(capacity)))
-    reqs = (_native.Request * R)()
-    filters, claims = [], []
-    off = 0
-    for i in range(R):
-        if i % 2 == 0:  # largest-style: modulo 1, ~capacity consecutive global times
-            lo = int(rng.integers(1, N - capacity + 1))
-            hi, modulo, offset = lo + capacity - 1, 1, 0
-            rows = np.arange(lo - 1, hi, dtype=np.uint64)
-        else:  # modulo-style: the whole store, one residue class
-            lo, hi, modulo = 1, N, modulo_m
-            offset = int(rng.integers(0, modulo))
-            first = (modulo - offset) % modulo or modulo  # smallest gt >= 1 with (gt + offset) % modulo == 0
-            rows = np.arange(first, N + 1, modulo, dtype=np.uint64) - 1
-        prefix = bytes([int(rng.integers(0, 256))])
-        bf = BloomFilter(args.filter_bits, args.error_rate, prefix)
-        known = rows[rng.random(len(rows)) >= 0.01]  # the requester misses 1 % of its range
-        buf = ctypes.create_string_buffer(bf.bytes, len(bf.bytes))
-        _native.check(lib.dsy_bloom_add_rows(ctx.handle, ctypes.byref(bf.params), store, known.ctypes.data,
-                                             len(known), buf))
-        raw = buf.raw + b"\x00" * ((-len(buf.raw)) % 4)
-        q = reqs[i]
-        q.time_low, q.time_high, q.modulo, q.offset = lo, hi, modulo, offset
-        q.filter_offset, q.m_bits, q.k = off, bf.size, bf.functions
-        q.hash_kind, q.chunk_bytes = _native.HASH_KINDS[bf.hash_name], bf.chunk_bytes
-        q.prefix_len = 1
-        q.prefix[0] = prefix[0]
-        filters.append(raw)
-        claims.append((lo, hi, offset, modulo, bf.functions, prefix, buf.raw))
-        off += len(raw)
-    fblob = b"".join(filters)
-    d_filters = torch.frombuffer(bytearray(fblob + bytes(64)), dtype=torch.uint8).to(dev)
     metas = (_native.Meta * 1)()
     metas[0].meta_id, metas[0].direction = 1, _native.DSY_ASC
 
@@ -275,6 +244,11 @@ def main():
 
     extra = set(x for x in args.extra.split(",") if x and x != "none")
 
+    # before the legs that append to the store (dropin, dedup, ingest): its CPU check reads the store as generated
+    sha1 = None
+    if "sha1" in extra:
+        sha1 = sha1_respond(args, ctx, lib, store, N, dev, blob, offsets, total_bytes, metas, rank, world, dist)
+
     ingest = None
     dedup = None
     claim = None
@@ -338,12 +312,108 @@ def main():
             "dedup": dedup,
             "claim_modulo": claim,
             "dropin": dropin,
+            "sha1_respond": sha1,
         }
         print(json.dumps(line))
     if store is not None:
         lib.dsy_store_free(store)
     if dist:
         dist.destroy_process_group()
+
+
+def sha1_respond(args, ctx, lib, store, N, dev, blob, offsets, total_bytes, metas, rank, world, dist):
+    """The headline step with SHA-1 claim filters: BloomFilter(512 * 8, 0.001, prefix="x") -- the filter the
+    reference's own test node puts in every introduction request (tests/debugcommunity/node.py:617), k = 10, SHA-1
+    '2-byte' chunks -- over the same 10 M-packet store, --claims claims (half largest-style, half modulo-style, 1 %
+    of each range missing).  Roofline of k_pair_test<sha1> (INT32 VALU: 961 ops per block), the oracle on a sample
+    of the claims beside it."""
+    rng = np.random.Generator(np.random.PCG64(args.seed + 1 + 1000 * rank))
+    R = args.claims
+    reqs, claims, fblob, d_filters, capacity = make_claims(ctx, lib, store, N, R, rng, 512 * 8, 0.001, b"x", dev)
+    p_out, p_off, pairs = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
+
+    def step():
+        _native.check(lib.dsy_sync_respond_dev(ctx.handle, store, reqs, R, d_filters.data_ptr(), metas, 1, N, 0,
+                                               args.byte_limit, 99, ctypes.byref(p_out), ctypes.byref(p_off),
+                                               ctypes.byref(pairs)))
+    for _ in range(args.warmup):
+        step()
+    ctx.synchronize()
+    ctx.reset_timing()
+    ctx.set_timing(True, only=[_native.TIME_PAIR_TEST])
+    t0 = time.perf_counter()
+    total = 0
+    steps = max(args.steps, 1)
+    for _ in range(steps):
+        step()
+        total += pairs.value
+    ctx.synchronize()
+    elapsed = time.perf_counter() - t0
+    ctx.set_timing(False)
+    kt = ctx.kernel_time(_native.TIME_PAIR_TEST)
+    work = ctx.work(_native.TIME_PAIR_TEST)
+    launches = max(kt["launches"], 1)
+    avg_s = kt["ms"] / 1e3 / launches
+    blocks = kt["blocks"] / launches
+    out = {"filter": "BloomFilter(4096, 0.001, b'x'): sha1 k=10, capacity %d" % capacity, "claims": R,
+           "ms_per_step": round(elapsed / steps * 1e3, 3),
+           "pairs_per_s": round(total / elapsed, 1), "useful_pairs_per_s": round(work["useful_pairs"] / elapsed, 1),
+           "pairs_per_step": int(total / steps),
+           "roofline": {"kernel": "k_pair_test<sha1>", "bound": "valu", "unit": "Tops/s", "peak": PEAK_INT32_TOPS,
+                        "achieved": round(blocks * OPS_PER_BLOCK["sha1"] / avg_s / 1e12, 2),
+                        "frac": round(blocks * OPS_PER_BLOCK["sha1"] / avg_s / 1e12 / PEAK_INT32_TOPS, 4),
+                        "avg_launch_us": round(avg_s * 1e6, 2), "launches": kt["launches"],
+                        "gblocks_per_s": round(blocks / avg_s / 1e9, 2),
+                        "hbm_gbs": round((kt["bytes"] / launches + total / steps * 17) / avg_s / 1e9, 1),
+                        "lane_utilization": round(work["blocks"] / max(work["lane_slots"], 1), 4)}}
+    if rank == 0 and world == 1 and args.cpu_claims > 0:
+        out["cpu_baseline"] = cpu_baseline(args, ctx, lib, store, reqs, claims, blob, offsets, total_bytes, N, fblob)
+    return out
+
+
+def make_claims(ctx, lib, store, N, R, rng, bits, error_rate, prefix, dev):
+    """R claims over the store (global time = row + 1): even ones largest-style (modulo 1, ~capacity consecutive
+    global times), odd ones modulo-style (the whole store, one residue class); each filter holds its range but a
+    random 1 % (the packets the requester misses).  prefix None: one random byte per claim (community.py:2549),
+    else that prefix for every claim.  Returns (dsy_request array, oracle claim tuples, packed filters on the host
+    and in HBM, capacity)."""
+    import torch
+    from dispersy_amd.bloomfilter import BloomFilter
+    capacity = BloomFilter(bits, error_rate).get_capacity(error_rate)
+    modulo_m = int(math.ceil(N / float(capacity)))
+    reqs = (_native.Request * R)()
+    filters, claims = [], []
+    off = 0
+    for i in range(R):
+        if i % 2 == 0:  # largest-style: modulo 1, ~capacity consecutive global times
+            lo = int(rng.integers(1, N - capacity + 1))
+            hi, modulo, offset = lo + capacity - 1, 1, 0
+            rows = np.arange(lo - 1, hi, dtype=np.uint64)
+        else:  # modulo-style: the whole store, one residue class
+            lo, hi, modulo = 1, N, modulo_m
+            offset = int(rng.integers(0, modulo))
+            first = (modulo - offset) % modulo or modulo  # smallest gt >= 1 with (gt + offset) % modulo == 0
+            rows = np.arange(first, N + 1, modulo, dtype=np.uint64) - 1
+        pre = bytes([int(rng.integers(0, 256))]) if prefix is None else prefix
+        bf = BloomFilter(bits, error_rate, pre)
+        known = rows[rng.random(len(rows)) >= 0.01]  # the requester misses 1 % of its range
+        buf = ctypes.create_string_buffer(bf.bytes, len(bf.bytes))
+        _native.check(lib.dsy_bloom_add_rows(ctx.handle, ctypes.byref(bf.params), store, known.ctypes.data,
+                                             len(known), buf))
+        raw = buf.raw + b"\x00" * ((-len(buf.raw)) % 4)
+        q = reqs[i]
+        q.time_low, q.time_high, q.modulo, q.offset = lo, hi, modulo, offset
+        q.filter_offset, q.m_bits, q.k = off, bf.size, bf.functions
+        q.hash_kind, q.chunk_bytes = _native.HASH_KINDS[bf.hash_name], bf.chunk_bytes
+        q.prefix_len = len(pre)
+        for j, c in enumerate(pre):
+            q.prefix[j] = c
+        filters.append(raw)
+        claims.append((lo, hi, offset, modulo, bf.functions, pre, buf.raw))
+        off += len(raw)
+    fblob = b"".join(filters)
+    d_filters = torch.frombuffer(bytearray(fblob + bytes(64)), dtype=torch.uint8).to(dev)
+    return reqs, claims, fblob, d_filters, capacity
 
 
 def dropin_bench(args, ctx, lib, store, offsets, N, claims, reps=5, batch=10_000, batches=5):

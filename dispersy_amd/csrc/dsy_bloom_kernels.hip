@@ -107,6 +107,20 @@ __global__ void __launch_bounds__(256) k_len_scatter(LenSort s, const uint64_t* 
 
 // ------------------------------------------------------------------------------------- hash + probe / set
 // OP 0: add (OR k bits per key into the filter), OP 1: test (present[key] = all k bits set).
+// The k probes of one key: OP 0 sets the bits (atomic OR), OP 1 returns 1 when all are set.
+template <class H, int CHUNK, int OP>
+__device__ __forceinline__ uint32_t probe_filter(uint32_t* fb, const H& st, uint32_t k, uint64_t m) {
+    if constexpr (OP == 1) return filter_has_all<H, CHUNK>(fb, st, k, m);
+#pragma unroll
+    for (int j = 0; j < ChunkLimit<H, CHUNK>::kmax; ++j) {
+        if (j < (int)k) {
+            const uint64_t pos = bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, j), m);
+            atomicOr(&fb[pos >> 5], 1u << (pos & 31));
+        }
+    }
+    return 1;
+}
+
 // DIAG (DMA path, 2-byte chunks only): 0 = the product kernel; 1 = no packet loads (the stage is hashed as left in
 // LDS: the compute ceiling); 2 = packet loads without the compression (the gather ceiling).  Diagnostics only, selected
 // by the ctx's DSY_BLOOM_DIAG environment knob (tools/hash_sweep.py); results are meaningless for DIAG != 0.
@@ -125,7 +139,6 @@ __global__ void __launch_bounds__(256) k_bloom(const DevParams* __restrict__ prm
         for (uint32_t i = threadIdx.x; i < nwords; i += blockDim.x) lds_filter[i] = OP == 0 ? 0u : filter[i];
         __syncthreads();
     }
-    uint32_t* fbits = use_lds ? lds_filter : filter;
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t waves = (n + 63) / 64;
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
@@ -153,15 +166,11 @@ __global__ void __launch_bounds__(256) k_bloom(const DevParams* __restrict__ prm
         if constexpr (DMA) hash_key_dma_reg<H, kDmaS, DIAG>(kv, st, my_dma);
         else hash_key<H>(kv, st);
         if (active) {
-            uint32_t ok = 1;
-#pragma unroll
-            for (int j = 0; j < ChunkLimit<H, CHUNK>::kmax; ++j) {
-                if (j < (int)k) {
-                    const uint64_t pos = bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, j), m);
-                    if (OP == 0) atomicOr(&fbits[pos >> 5], 1u << (pos & 31));
-                    else ok &= (fbits[pos >> 5] >> (pos & 31)) & 1u;
-                }
-            }
+            // two call sites, so each sees where its filter lives: ds_or / ds_read on the LDS copy, global atomics /
+            // loads on the HBM one (one pointer picked at run time would be a flat pointer: every probe a flat
+            // atomic or load behind its own vmcnt(0) wait -- 30 % of the SHA-1 add kernel)
+            const uint32_t ok = use_lds ? probe_filter<H, CHUNK, OP>(lds_filter, st, k, m)
+                                        : probe_filter<H, CHUNK, OP>(filter, st, k, m);
             if (OP == 1) present[slot] = (uint8_t)ok;
         }
     }

@@ -494,4 +494,27 @@ __device__ __forceinline__ uint64_t bit_position(uint64_t chunk, uint64_t m) {
     return (uint32_t)chunk % (uint32_t)m;
 }
 
+// Membership of one key: 1 when all k probed bits are set (bloomfilter.py:185-197).  Every chunk the digest holds
+// is looked up -- no branch per probe, so the k loads go out together behind one wait instead of one round trip
+// each -- and the ones past k do not count (their positions are < m, so the reads stay inside the filter).
+template <class H, int CHUNK, class W>
+__device__ __forceinline__ uint32_t filter_has_all(W* fb, const H& st, uint32_t k, uint64_t m) {
+    constexpr int kmax = ChunkLimit<H, CHUNK>::kmax;
+    uint32_t w[kmax], sh[kmax];
+#pragma unroll
+    for (int j = 0; j < kmax; ++j) {
+        const uint64_t pos = bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, j), m);
+        w[j] = fb[pos >> 5];
+        sh[j] = (uint32_t)pos & 31u;
+    }
+    // the words are needed here, in order: every load has been issued before the first wait (left to itself the
+    // scheduler interleaves load, wait, test to save registers)
+#pragma unroll
+    for (int j = 0; j < kmax; ++j) asm volatile("" : "+v"(w[j])::"memory");
+    uint32_t ok = 1;
+#pragma unroll
+    for (int j = 0; j < kmax; ++j) ok &= (w[j] >> sh[j]) | (uint32_t)(j >= (int)k);
+    return ok & 1u;
+}
+
 }  // namespace dsy

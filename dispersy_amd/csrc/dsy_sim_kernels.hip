@@ -303,14 +303,7 @@ __global__ void __launch_bounds__(256) k_sim_respond(dsy_sim_config c, const uin
             KeyView kv{ublob + uoff[id], (uint32_t)(uoff[id + 1] - uoff[id]), pre[wv], 1};
             H st;
             hash_key<H>(kv, st);
-            uint32_t ok = 1;
-#pragma unroll
-            for (int j = 0; j < ChunkLimit<H, CHUNK>::kmax; ++j) {
-                if (j < (int)c.k) {
-                    const uint64_t pos = bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, j), c.m_bits);
-                    ok &= (filt[wv][pos >> 5] >> (pos & 31)) & 1u;
-                }
-            }
+            const uint32_t ok = filter_has_all<H, CHUNK>(filt[wv], st, c.k, c.m_bits);
             miss = !ok;
             len = miss ? (int64_t)kv.len : 0;
         }

@@ -648,14 +648,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         }
         const uint32_t* filt = (const uint32_t*)(L.filters + q.filter_offset);
         const uint64_t m = q.m_bits;
-        uint32_t ok = 1;
-#pragma unroll
-        for (int jj = 0; jj < ChunkLimit<H, CHUNK>::kmax; ++jj) {
-            if (jj < (int)q.k) {
-                const uint64_t pos = bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, jj), m);
-                ok &= (filt[pos >> 5] >> (pos & 31)) & 1u;
-            }
-        }
+        const uint32_t ok = filter_has_all<H, CHUNK>(filt, st, q.k, m);
         const uint32_t nb = active ? n_blocks(kv.plen + kv.len, H::block_bytes, H::len_bytes) : 0u;
         if (active) {
             // misses are rare (the requester holds most of its range): one atomic bit per missing pair
