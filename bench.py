@@ -56,10 +56,11 @@ _PAR = {}
 
 
 def _par_worker(i):
-    """One forked worker: pure CPU work over data the parent set up before forking (never touches the GPU)."""
+    """One forked worker: pure CPU work over data the parent set up before forking (never touches the GPU).  fn
+    returns the units done, or (units, seconds) when it times its own measured part (after a private setup)."""
     t0 = time.perf_counter()
-    units = _PAR["fn"](_PAR["shards"][i])
-    return units, time.perf_counter() - t0
+    r = _PAR["fn"](_PAR["shards"][i])
+    return r if isinstance(r, tuple) else (r, time.perf_counter() - t0)
 
 
 def cpu_parallel(fn, shards):
@@ -545,11 +546,33 @@ def dedup_bench(args, ctx, lib, store, blob, offsets, N, batch=10_000, reps=10, 
         for m_ in sample:
             is_duplicate_sync_message(conn, 1, m_, sends)
         dt = time.perf_counter() - t0
+        model, cores = cpu_info()
+
         conn.close()
-        cpu = {"value": round(batch / dt, 1), "unit": "messages/s", "cores": 1, "kind": "port",
+
+        def table():
+            c = sqlite3.connect(":memory:")
+            c.executescript(SYNC_SCHEMA)
+            r = np.random.Generator(np.random.PCG64(6))
+            c.executemany("INSERT INTO sync (community, member, global_time, meta_message, packet) VALUES (1, ?, ?, 1, ?)",
+                          ((int(member[i]), int(gt[i]), r.bytes(int(l)))
+                           for i, l in zip(range(pre), r.integers(100, 1501, size=pre))))
+            c.commit()
+            return c
+
+        def shard(_):  # every process builds the same table (untimed), then checks the same batch against it
+            c = table()
+            t1 = time.perf_counter()
+            for m_ in sample:
+                is_duplicate_sync_message(c, 1, m_, [])
+            return len(sample), time.perf_counter() - t1
+        ncore = n_core_leg(shard, list(range(cores)), "messages/s",
+                           "the same %d messages in every process, each against its own copy of the %d-row table"
+                           % (batch, pre))
+        cpu = {"value": round(batch / dt, 1), "unit": "messages/s", "cores": 1, "kind": "port", "cpu_model": model,
                "sample": "%d messages through the reference's SELECT packet, undone ... WHERE community, member, "
                          "global_time + packet compare (dispersy.py:868-910) on an in-memory sqlite3 sync table of "
-                         "%d rows" % (batch, pre)}
+                         "%d rows" % (batch, pre), "n_core": ncore}
     return {"metric": "received messages duplicate-checked/sec", "batch": batch, "store_rows": N,
             "index_build_ms": round(build_ms, 2), "median_ms_per_batch": round(ms, 3),
             "messages_per_s": round(batch / (ms / 1e3), 1), "found_exact": exact, "found_new": new,
@@ -726,14 +749,36 @@ def ingest_bench(args, ctx, lib, store, step, pairs, N, batch=10_000, batches=10
         conn.commit()
         dt = time.perf_counter() - t0
         conn.close()
-        cpu = {"value": round(batch / dt, 1), "unit": "packets/s", "cores": 1, "kind": "port",
+        model, cores = cpu_info()
+
+        def shard(_):  # every process fills its own table (untimed), then INSERTs the same batch
+            c = sqlite3.connect(":memory:")
+            c.executescript(SYNC_SCHEMA)
+            r = np.random.Generator(np.random.PCG64(5))
+            pl = r.integers(100, 1501, size=pre)
+            c.executemany("INSERT INTO sync (community, member, global_time, meta_message, packet) VALUES (1, ?, ?, 1, ?)",
+                          ((i, int(g), r.bytes(int(l))) for i, (g, l) in enumerate(zip(r.integers(1, N + 1, size=pre), pl))))
+            c.commit()
+            t1 = time.perf_counter()
+            insert_packets(c, 1, msgs)
+            c.commit()
+            return len(msgs), time.perf_counter() - t1
+        ncore = n_core_leg(shard, list(range(cores)), "packets/s",
+                           "the same %d-packet batch in every process, each into its own %d-row table" % (batch, pre))
+        cpu = {"value": round(batch / dt, 1), "unit": "packets/s", "cores": 1, "kind": "port", "cpu_model": model,
                "sample": "one batch of %d packets INSERTed one statement each (dispersy.py:1523-1533) into an "
-                         "in-memory sqlite3 sync table with its index, pre-filled with %d rows" % (batch, pre)}
+                         "in-memory sqlite3 sync table with its index, pre-filled with %d rows" % (batch, pre),
+               "n_core": ncore}
     return {"metric": "received packets stored/sec", "batch": batch, "batches": batches, "cpu_baseline": cpu,
             "store_rows_after": rows, "median_ms_per_batch": round(ms, 3),
             "packets_per_s": round(batch / (ms / 1e3), 1),
             "first_append_ms": round(first_ms, 2),
             "index_bytes_per_append": 32 * rows, "packet_bytes_per_append": int(pkt_bytes),
+            "roofline": {"kernel": "k_ingest_merge_old/new (the whole append call: upload, rank, merge, lines)",
+                         "bound": "hbm", "unit": "GB/s", "peak": PEAK_HBM_GBS,
+                         "achieved": round((32 * rows + pkt_bytes) / (ms / 1e3) / 1e9, 1),
+                         "frac": round((32 * rows + pkt_bytes) / (ms / 1e3) / 1e9 / PEAK_HBM_GBS, 4),
+                         "traffic": None},
             "respond_after_ingest_pairs": int(pairs.value)}
 
 

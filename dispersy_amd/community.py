@@ -16,6 +16,7 @@ one call each, over the store's live index in HBM: dsy_claim_largest (the pivot 
 _select_and_fix) and dsy_claim_modulo (the residue class).
 """
 import ctypes
+import itertools
 import random as _random_module
 import time as _time
 from collections import OrderedDict, namedtuple
@@ -623,33 +624,32 @@ class SyncCommunity(object):
         R = len(requests)
         reqs = np.zeros(max(R, 1), dtype=_REQUEST_DTYPE)
         if R:
-            blooms = [q.bloom_filter for q in requests]
-            raws = [bf.bytes for bf in blooms]
+            # one pass over the Python objects, then whole columns
+            kinds = _native.HASH_KINDS
+            c = np.fromiter(itertools.chain.from_iterable(
+                (min(q.time_low, MAX_GT), min(q.time_high, MAX_GT), q.modulo, q.offset, bf._m_size, bf._k_functions,
+                 kinds[bf._hash_name], bf._chunk, len(bf._prefix)) for q in requests for bf in (q.bloom_filter,)),
+                dtype=np.uint64, count=9 * R).reshape(R, 9)
+            raws = [q.bloom_filter._raw for q in requests]
+            prefixes = [q.bloom_filter._prefix for q in requests]
+            for j, name in enumerate(("time_low", "time_high", "modulo", "offset", "m_bits", "k", "hash_kind",
+                                      "chunk_bytes", "prefix_len")):
+                reqs[name][:R] = c[:, j]
+            plen = c[:, 8]
             sizes = np.fromiter(((len(r) + 3) & ~3 for r in raws), dtype=np.uint64, count=R)
             reqs["filter_offset"][:R] = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
-            reqs["time_low"][:R] = [min(q.time_low, MAX_GT) for q in requests]
-            reqs["time_high"][:R] = [min(q.time_high, MAX_GT) for q in requests]
-            reqs["modulo"][:R] = [q.modulo for q in requests]
-            reqs["offset"][:R] = [q.offset for q in requests]
-            reqs["m_bits"][:R] = [bf.size for bf in blooms]
-            reqs["k"][:R] = [bf.functions for bf in blooms]
-            reqs["hash_kind"][:R] = [_native.HASH_KINDS[bf.hash_name] for bf in blooms]
-            reqs["chunk_bytes"][:R] = [bf.chunk_bytes for bf in blooms]
-            prefixes = [bf.prefix for bf in blooms]
-            plen = np.fromiter((len(p) for p in prefixes), dtype=np.uint32, count=R)
-            reqs["prefix_len"][:R] = plen
             if (plen == 1).all():
-                reqs["prefix"][:R, 0] = [p[0] for p in prefixes]
+                reqs["prefix"][:R, 0] = np.frombuffer(b"".join(prefixes), dtype=np.uint8)
             else:
                 for i, p in enumerate(prefixes):
                     reqs["prefix"][i, :len(p)] = np.frombuffer(p, dtype=np.uint8)
             first = len(raws[0])
-            if all(len(r) == first for r in raws):  # one filter size (the MTU claim): pad every row at once
-                rows = np.zeros((R, (first + 3) & ~3), dtype=np.uint8)
-                rows[:, :first] = np.frombuffer(b"".join(raws), dtype=np.uint8).reshape(R, first)
-                blob = rows.tobytes()
+            if all(len(r) == first for r in raws):
+                # one filter size (the MTU claim): the padding is the join's separator
+                pad = b"\x00" * ((-first) % 4)
+                blob = pad.join(raws) + pad
             else:
-                blob = b"".join(r + b"\x00" * ((-len(r)) % 4) for r in raws)
+                blob = b"".join(bytes(r) + b"\x00" * ((-len(r)) % 4) for r in raws)
         else:
             blob = b""
         return self._respond_requests(reqs, R, blob, include_inactive, byte_limit, random_seed)
@@ -694,7 +694,7 @@ class SyncCommunity(object):
         out_off = np.zeros(R + 1, dtype=np.uint64)
         cap = 1 << 16
         while True:
-            out = np.zeros(cap, dtype=np.uint64)
+            out = np.empty(cap, dtype=np.uint64)
             rc = ctx.lib.dsy_sync_respond(ctx.handle, st.handle, reqs.ctypes.data_as(ctypes.POINTER(_native.Request)),
                                           R, blob, len(blob), mt, len(metas),
                                           self.global_time, 1 if include_inactive else 0, int(byte_limit), seed,
@@ -704,7 +704,9 @@ class SyncCommunity(object):
                 continue
             _native.check(rc)
             break
-        return [out[int(out_off[i]):int(out_off[i + 1])].astype(np.int64) for i in range(R)]
+        rows = out[:int(out_off[R])].astype(np.int64)
+        offs = out_off.tolist()
+        return [rows[offs[i]:offs[i + 1]] for i in range(R)]
 
     def on_introduction_request_sync(self, messages, include_inactive=False):
         """The sync half of on_introduction_request (community.py:2531-2572) for a receive batch.

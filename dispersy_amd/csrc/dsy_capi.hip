@@ -60,6 +60,7 @@ struct dsy_ctx {
     std::map<std::string, DevBuf> ws;
     uint32_t max_grid = 2048;
     int bloom_diag = 0;  // DSY_BLOOM_DIAG at creation: single-filter ceiling diagnostics (k_bloom DIAG)
+    int pair_diag = 0;   // DSY_PAIR_DIAG at creation: responder ceiling diagnostics (k_pair_test DIAG)
     uint32_t timing = 0;  // bit i: bracket class i with events
     std::vector<PendingTimer> pending;
     std::vector<hipEvent_t> event_pool;
@@ -349,6 +350,7 @@ int dsy_ctx_create(int device, dsy_ctx** out) {
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
     c->max_grid = (uint32_t)std::max(cus, 1) * 8;
     if (const char* v = getenv("DSY_BLOOM_DIAG")) c->bloom_diag = atoi(v);
+    if (const char* v = getenv("DSY_PAIR_DIAG")) c->pair_diag = atoi(v);
     hipHostMalloc(&c->pinned, 4096, hipHostMallocDefault);
     *out = c;
     return DSY_OK;
@@ -1504,6 +1506,9 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
             d.chunk_bytes = q.chunk_bytes;
             d.prefix_len = q.prefix_len;
             d.prefix = d_pre + at;
+            d.prefix_word = 0;
+            for (uint32_t j = 0; j < std::min<uint32_t>(q.prefix_len, 4); ++j) d.prefix_word |= (uint32_t)q.prefix[j] << (8 * j);
+            d.pad[0] = d.pad[1] = d.pad[2] = 0;
             std::memcpy(h_pre + at, q.prefix, q.prefix_len);
             at += q.prefix_len;
             dq[r] = d;
@@ -1576,6 +1581,7 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     L.flags = (uint32_t*)(io + cnt_b);
     L.counters = (uint64_t*)io;
     L.stream = c->stream;
+    L.diag = c->pair_diag;
 
     // ---- per-claim output capacity: every emitted packet but the last costs >= min_len bytes of budget, so a
     // claim sends at most byte_limit / min_len + 2 packets.  When that bound is small the capacities and output

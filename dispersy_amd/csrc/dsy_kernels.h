@@ -123,6 +123,8 @@ struct DevRequest {
     uint64_t time_low, time_high, filter_offset, m_bits;
     uint32_t modulo, offset, k, hash_kind, chunk_bytes, prefix_len;
     const uint8_t* prefix;  // device pointer into the call's prefix buffer
+    uint32_t prefix_word;   // the first min(prefix_len, 4) prefix bytes, little-endian (the LDS-DMA paths' prefix)
+    uint32_t pad[3];
 };
 
 struct SegMeta {          // one syncable meta in serving order, resolved against the store
@@ -163,6 +165,7 @@ struct RespondLaunch {
     uint32_t* flags;          // device [16], zeroed by k_setup: [kFlagChunks] the window's longest claim in 64-pair
                               // chunks (k_fill atomicMax, read by k_pair_test, reset by k_compact)
     uint64_t* fill_clock;     // optional [n_act][4] s_memtime stamps of k_fill phases (DSY_FILL_PROFILE)
+    int diag;                 // k_pair_test DIAG (MD5 / SHA-1, 2-byte chunks): 0 product, 1 no loads, 2 loads only
     uint64_t* counters;       // device [kCntSpread][kCntN]: pairs hashed, compression blocks, packet bytes, pairs the reference
                               // would have hashed (it stops at the byte limit), lane-block slots of the hashing waves
     hipStream_t stream;

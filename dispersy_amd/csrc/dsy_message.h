@@ -387,9 +387,9 @@ __device__ __forceinline__ void hash_key_dma_reg(const KeyView& kv, H& st, uint8
 // message (prefix || packet) is the packet shifted by the prefix length r, which is wave-uniform (one claim per
 // wave): a uniform alignbyte funnel with a one-dword carry from the previous stage.  Single 8 KiB buffer per wave,
 // like hash_key_dma_reg<H, 2>.  Requires r <= 4 and kv.key 128-byte aligned; lines past the packet hold only
-// padding and are not loaded.
-template <class H>
-__device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uint8_t* lds_wave) {
+// padding and are not loaded.  preword: the r prefix bytes, little-endian (wave-uniform: read once per claim).  MODE as in hash_key_dma_reg (k_pair_test DIAG diagnostics only).
+template <class H, int MODE = 0>
+__device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uint8_t* lds_wave, uint32_t preword) {
     static_assert(H::block_bytes == 64, "LDS-DMA staging is for 64-byte blocks");
     using G = DmaGeometry<2, 1>;
     const uint32_t lane = threadIdx.x & 63;
@@ -402,8 +402,6 @@ __device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uin
     for (int d = 32; d >= 1; d >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, d, 64));
     const uint32_t nst = (nbmax + 1) / 2;
     const uint32_t tmin = wave_min_u32(total);
-    uint32_t preword = 0;
-    for (uint32_t j = 0; j < r; ++j) preword |= (uint32_t)kv.pre[j] << (8 * j);
     const uint64_t base = (uint64_t)(uintptr_t)kv.key;  // 128-byte aligned
     auto issue = [&](uint32_t s) {
 #pragma unroll
@@ -413,7 +411,7 @@ __device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uin
             const uint32_t pend = __shfl((int)len, p, 64);
             const uint32_t c = ((lane % G::kChunks) + ((uint32_t)p >> G::kShift)) % G::kChunks;
             const uint64_t b64 = ((uint64_t)bhi << 32) | blo;
-            if (s * 128 < pend)
+            if (MODE != 1 && s * 128 < pend)
                 __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)(b64 + s * 128 + 16 * c),
                                                  (__attribute__((address_space(3))) void*)(lds_wave + i * 1024), 16, 0, 0);
         }
@@ -457,7 +455,8 @@ __device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uin
                 }
                 const uint32_t o0 = b * 64;
                 finish_block<H>(x, o0, total, b + 1 == nb, o0 + 64 <= tmin);
-                st.compress(x);
+                if (MODE != 2) st.compress(x);
+                else st.h[0] ^= x[0] ^ x[5] ^ x[10] ^ x[15];
             }
         }
     }

@@ -607,7 +607,9 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
 }
 
 // -------------------------------------------------------------------------------------- k_pair_test
-template <class H, int CHUNK, bool DMA>
+// DIAG (DMA, 2-byte chunks; DSY_PAIR_DIAG): 0 the product kernel, 1 no packet loads (compute ceiling), 2 packet
+// loads without the compression (gather ceiling) -- diagnostics only, their answers are meaningless
+template <class H, int CHUNK, bool DMA, int DIAG = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_pair_test(RespondLaunch L, const uint32_t* __restrict__ req_list,
                                                    uint32_t n_list) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dma_lds[];
@@ -642,7 +644,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         }
         H st;
         if constexpr (DMA) {
-            hash_key_dma_lines<H>(kv, st, my_lds);  // the host routes prefixes > 4 bytes to DMA = false
+            hash_key_dma_lines<H, DIAG>(kv, st, my_lds, q.prefix_word);  // prefixes > 4 bytes go to DMA = false
         } else {
             hash_key<H>(kv, st);
         }
@@ -652,7 +654,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         const uint32_t nb = active ? n_blocks(kv.plen + kv.len, H::block_bytes, H::len_bytes) : 0u;
         if (active) {
             // misses are rare (the requester holds most of its range): one atomic bit per missing pair
-            if (!ok) atomicOr((unsigned long long*)&L.miss_mask[(uint64_t)a_slot * (W / 64) + t / 64], 1ull << (t % 64));
+            if (!ok && DIAG == 0)  // (the diagnostics' digests are garbage: their misses would be mostly atomics)
+                atomicOr((unsigned long long*)&L.miss_mask[(uint64_t)a_slot * (W / 64) + t / 64], 1ull << (t % 64));
             acc_blocks += nb;
             acc_bytes += kv.len;
         }
@@ -699,8 +702,12 @@ static hipError_t pair_test_family(const RespondLaunch& L, bool long_prefix, con
     if constexpr (dma) {
         if (!long_prefix) {
             const size_t lds = 4 * DmaGeometry<2, 1>::kWaveBytes;
-            hipLaunchKernelGGL((k_pair_test<H, CHUNK, true>), dim3((uint32_t)blocks), dim3(256), lds, L.stream, L, list,
-                               n_list);
+            auto kern = k_pair_test<H, CHUNK, true>;
+            if constexpr (CHUNK == 2) {
+                if (L.diag == 1) kern = k_pair_test<H, CHUNK, true, 1>;
+                if (L.diag == 2) kern = k_pair_test<H, CHUNK, true, 2>;
+            }
+            hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(256), lds, L.stream, L, list, n_list);
             return hipGetLastError();
         }
     }
