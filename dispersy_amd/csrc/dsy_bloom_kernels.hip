@@ -270,17 +270,17 @@ static hipError_t launch_op(const BloomLaunch& L, uint32_t grid) {
         if constexpr (H::block_bytes == 64 && CHUNK == 2) {
             if (L.diag == 1 || L.diag == 2) {
                 auto kern = L.diag == 1 ? k_bloom<H, CHUNK, OP, true, 1> : k_bloom<H, CHUNK, OP, true, 2>;
-                hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, L.stream, L.prm, L.blob, L.offsets, L.rows, L.rec,
-                                   L.tasks, L.n, L.filter, L.nwords, L.use_lds, L.present);
+                launch_timed(kern, dim3(grid), dim3(256), lds, L.stream, L.ev_start, L.ev_stop, L.prm, L.blob, L.offsets,
+                             L.rows, L.rec, L.tasks, L.n, L.filter, L.nwords, L.use_lds, L.present);
                 return hipGetLastError();
             }
         }
         if constexpr (H::block_bytes == 64)
-            hipLaunchKernelGGL((k_bloom<H, CHUNK, OP, true>), dim3(grid), dim3(256), lds, L.stream, L.prm, L.blob,
-                               L.offsets, L.rows, L.rec, L.tasks, L.n, L.filter, L.nwords, L.use_lds, L.present);
+            launch_timed(k_bloom<H, CHUNK, OP, true>, dim3(grid), dim3(256), lds, L.stream, L.ev_start, L.ev_stop, L.prm,
+                         L.blob, L.offsets, L.rows, L.rec, L.tasks, L.n, L.filter, L.nwords, L.use_lds, L.present);
     } else {
-        hipLaunchKernelGGL((k_bloom<H, CHUNK, OP, false>), dim3(grid), dim3(256), lds, L.stream, L.prm, L.blob,
-                           L.offsets, L.rows, L.rec, L.tasks, L.n, L.filter, L.nwords, L.use_lds, L.present);
+        launch_timed(k_bloom<H, CHUNK, OP, false>, dim3(grid), dim3(256), lds, L.stream, L.ev_start, L.ev_stop, L.prm,
+                     L.blob, L.offsets, L.rows, L.rec, L.tasks, L.n, L.filter, L.nwords, L.use_lds, L.present);
     }
     return hipGetLastError();
 }

@@ -165,6 +165,21 @@ void timer_end(dsy_ctx* c, PendingTimer* t) {
     c->pending.push_back(*t);
 }
 
+// the same timer for one kernel launched with launch_timed: its events are handed to the dispatch (*a, *b), not
+// recorded on the stream around it; timer_dispatched files them after the launch
+void timer_dispatch(dsy_ctx* c, PendingTimer* t, int cls, hipEvent_t* a, hipEvent_t* b) {
+    t->cls = cls;
+    t->a = t->b = nullptr;
+    *a = *b = nullptr;
+    if (!(c->timing & (1u << cls))) return;
+    *a = t->a = take_event(c);
+    *b = t->b = take_event(c);
+}
+
+void timer_dispatched(dsy_ctx* c, PendingTimer* t) {
+    if (t->a) c->pending.push_back(*t);
+}
+
 // fold completed timers; timers whose events have not completed yet stay pending
 void timers_collect(dsy_ctx* c) {
     size_t keep = 0;
@@ -303,9 +318,9 @@ int run_bloom(dsy_ctx* c, BloomOp op, const dsy_bloom_params* p, const uint8_t* 
         L.tasks = (const PairTask*)tasks;
     }
     PendingTimer t;
-    timer_begin(c, &t, kTimeBuild);
+    timer_dispatch(c, &t, kTimeBuild, &L.ev_start, &L.ev_stop);
     HIP_TRY(launch_bloom(L));
-    timer_end(c, &t);
+    timer_dispatched(c, &t);
     return DSY_OK;
 }
 
@@ -1678,11 +1693,12 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
         for (size_t f = 0; f < fam_active.size(); ++f) {
             if (!runs[f].second) continue;
             const int fid = fam_id[f];
-            timer_begin(c, &t, kTimePairTest);
+            timer_dispatch(c, &t, kTimePairTest, &L.ev_start, &L.ev_stop);
             const int kc = fid / 2;
             HIP_TRY(launch_pair_test_list(L, kc / 3, kc % 3 == 0 ? 2 : kc % 3 == 1 ? 4 : 8, fid % 2 == 1, d_slots + runs[f].first,
                                           (uint32_t)runs[f].second));
-            timer_end(c, &t);
+            timer_dispatched(c, &t);
+            L.ev_start = L.ev_stop = nullptr;
         }
         timer_begin(c, &t, kTimeCompact);
         HIP_TRY(launch_compact(L));

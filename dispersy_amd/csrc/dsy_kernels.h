@@ -1,6 +1,7 @@
 // dsy_kernels.h -- launch descriptors shared by the C-ABI (dsy_capi.hip) and the kernel translation units.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 #include "../../include/dsybloom.h"
@@ -54,7 +55,18 @@ struct BloomLaunch {
     uint32_t max_grid;
     hipStream_t stream;
     int diag;               // k_bloom DIAG: 0 = the product kernel, 1 / 2 = compute / gather ceiling diagnostics
+    hipEvent_t ev_start, ev_stop;  // when set: recorded by the hashing kernel's own dispatch (launch_timed)
 };
+
+// A kernel launch whose start/stop events, when given, are recorded by the dispatch itself
+// (hipExtLaunchKernelGGL: the timestamps of the kernel's AQL packet, no marker packets between kernels -- an event
+// record between two dispatches leaves a ~6 us gap on the queue)
+template <typename F, typename... Args>
+inline void launch_timed(F kern, dim3 grid, dim3 block, size_t lds, hipStream_t stream, hipEvent_t ev_start,
+                         hipEvent_t ev_stop, Args... args) {
+    if (ev_start) hipExtLaunchKernelGGL(kern, grid, block, (uint32_t)lds, stream, ev_start, ev_stop, 0, args...);
+    else hipLaunchKernelGGL(kern, grid, block, lds, stream, args...);
+}
 
 hipError_t launch_bloom(const BloomLaunch& L);
 hipError_t launch_or_reduce(const uint32_t* parts, uint32_t n_parts, uint64_t words, uint32_t* out, uint32_t max_grid,
@@ -166,6 +178,7 @@ struct RespondLaunch {
                               // chunks (k_fill atomicMax, read by k_pair_test, reset by k_compact)
     uint64_t* fill_clock;     // optional [n_act][4] s_memtime stamps of k_fill phases (DSY_FILL_PROFILE)
     int diag;                 // k_pair_test DIAG (MD5 / SHA-1, 2-byte chunks): 0 product, 1 no loads, 2 loads only
+    hipEvent_t ev_start, ev_stop;  // when set: recorded by k_pair_test's own dispatch (launch_timed)
     uint64_t* counters;       // device [kCntSpread][kCntN]: pairs hashed, compression blocks, packet bytes, pairs the reference
                               // would have hashed (it stops at the byte limit), lane-block slots of the hashing waves
     hipStream_t stream;

@@ -707,11 +707,12 @@ static hipError_t pair_test_family(const RespondLaunch& L, bool long_prefix, con
                 if (L.diag == 1) kern = k_pair_test<H, CHUNK, true, 1>;
                 if (L.diag == 2) kern = k_pair_test<H, CHUNK, true, 2>;
             }
-            hipLaunchKernelGGL(kern, dim3((uint32_t)blocks), dim3(256), lds, L.stream, L, list, n_list);
+            launch_timed(kern, dim3((uint32_t)blocks), dim3(256), lds, L.stream, L.ev_start, L.ev_stop, L, list, n_list);
             return hipGetLastError();
         }
     }
-    hipLaunchKernelGGL((k_pair_test<H, CHUNK, false>), dim3((uint32_t)blocks), dim3(256), 0, L.stream, L, list, n_list);
+    launch_timed(k_pair_test<H, CHUNK, false>, dim3((uint32_t)blocks), dim3(256), 0, L.stream, L.ev_start, L.ev_stop, L,
+                 list, n_list);
     return hipGetLastError();
 }
 
