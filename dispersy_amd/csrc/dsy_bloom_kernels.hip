@@ -106,25 +106,11 @@ __global__ void __launch_bounds__(256) k_len_scatter(LenSort s, const uint64_t* 
 }
 
 // ------------------------------------------------------------------------------------- hash + probe / set
-// OP 0: add (OR k bits per key into the filter), OP 1: test (present[key] = all k bits set).
-// The k probes of one key: OP 0 sets the bits (atomic OR), OP 1 returns 1 when all are set.
-template <class H, int CHUNK, int OP>
-__device__ __forceinline__ uint32_t probe_filter(uint32_t* fb, const H& st, uint32_t k, uint64_t m) {
-    if constexpr (OP == 1) return filter_has_all<H, CHUNK>(fb, st, k, m);
-#pragma unroll
-    for (int j = 0; j < ChunkLimit<H, CHUNK>::kmax; ++j) {
-        if (j < (int)k) {
-            const uint64_t pos = bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, j), m);
-            atomicOr(&fb[pos >> 5], 1u << (pos & 31));
-        }
-    }
-    return 1;
-}
-
 // DIAG (DMA path, 2-byte chunks only): 0 = the product kernel; 1 = no packet loads (the stage is hashed as left in
 // LDS: the compute ceiling); 2 = packet loads without the compression (the gather ceiling).  Diagnostics only, selected
 // by the ctx's DSY_BLOOM_DIAG environment knob (tools/hash_sweep.py); results are meaningless for DIAG != 0.
-template <class H, int CHUNK, int OP, bool DMA, int DIAG = 0>
+// OP 0: add (filter_set_all, OR_MODE as there), OP 1: test (present[key] = all k bits set).
+template <class H, int CHUNK, int OP, bool DMA, int DIAG = 0, int OR_MODE = 0>
 __global__ void __launch_bounds__(256) k_bloom(const DevParams* __restrict__ prm, const uint8_t* __restrict__ blob,
                                                const uint64_t* __restrict__ offsets, const uint64_t* __restrict__ rows,
                                                const RowRec* __restrict__ rec, const PairTask* __restrict__ tasks, uint64_t n,
@@ -165,13 +151,16 @@ __global__ void __launch_bounds__(256) k_bloom(const DevParams* __restrict__ prm
         H st;
         if constexpr (DMA) hash_key_dma_reg<H, kDmaS, DIAG>(kv, st, my_dma);
         else hash_key<H>(kv, st);
-        if (active) {
-            // two call sites, so each sees where its filter lives: ds_or / ds_read on the LDS copy, global atomics /
-            // loads on the HBM one (one pointer picked at run time would be a flat pointer: every probe a flat
-            // atomic or load behind its own vmcnt(0) wait -- 30 % of the SHA-1 add kernel)
-            const uint32_t ok = use_lds ? probe_filter<H, CHUNK, OP>(lds_filter, st, k, m)
-                                        : probe_filter<H, CHUNK, OP>(filter, st, k, m);
-            if (OP == 1) present[slot] = (uint8_t)ok;
+        // two call sites, so each sees where its filter lives: ds_or / ds_read on the LDS copy, global atomics /
+        // loads on the HBM one (one pointer picked at run time would be a flat pointer: every probe a flat atomic or
+        // load behind its own vmcnt(0) wait -- 30 % of the SHA-1 add kernel)
+        if constexpr (OP == 0) {
+            if (use_lds) filter_set_all<H, CHUNK, OR_MODE>(lds_filter, st, k, m, active);
+            else filter_set_all<H, CHUNK, OR_MODE>(filter, st, k, m, active);
+        } else if (active) {
+            const uint32_t ok = use_lds ? filter_has_all<H, CHUNK>(lds_filter, st, k, m)
+                                        : filter_has_all<H, CHUNK>(filter, st, k, m);
+            present[slot] = (uint8_t)ok;
         }
     }
     if (OP == 0 && use_lds) {
@@ -260,14 +249,14 @@ hipError_t launch_len_sort(const LenSort& s, const uint64_t* offsets, const uint
     return hipGetLastError();
 }
 
-template <class H, int CHUNK, int OP>
+template <class H, int CHUNK, int OP, int OR_MODE>
 static hipError_t launch_op(const BloomLaunch& L, uint32_t grid) {
     // LDS-DMA staging for MD5 / SHA-1 whenever the filter is small enough to leave room for it
     const bool dma = (H::kind == DSY_MD5 || H::kind == DSY_SHA1) && L.prm_prefix_len <= 4 &&
                      (!L.use_lds || L.nwords * 4 <= 16 * 1024);
     const size_t lds = (dma ? 4 * kDmaWaveBytes : 0) + (L.use_lds ? (size_t)L.nwords * 4 : 0);
     if (dma) {
-        if constexpr (H::block_bytes == 64 && CHUNK == 2) {
+        if constexpr (H::block_bytes == 64 && CHUNK == 2 && OR_MODE == 0) {
             if (L.diag == 1 || L.diag == 2) {
                 auto kern = L.diag == 1 ? k_bloom<H, CHUNK, OP, true, 1> : k_bloom<H, CHUNK, OP, true, 2>;
                 launch_timed(kern, dim3(grid), dim3(256), lds, L.stream, L.ev_start, L.ev_stop, L.prm, L.blob, L.offsets,
@@ -276,11 +265,13 @@ static hipError_t launch_op(const BloomLaunch& L, uint32_t grid) {
             }
         }
         if constexpr (H::block_bytes == 64)
-            launch_timed(k_bloom<H, CHUNK, OP, true>, dim3(grid), dim3(256), lds, L.stream, L.ev_start, L.ev_stop, L.prm,
-                         L.blob, L.offsets, L.rows, L.rec, L.tasks, L.n, L.filter, L.nwords, L.use_lds, L.present);
+            launch_timed(k_bloom<H, CHUNK, OP, true, 0, OR_MODE>, dim3(grid), dim3(256), lds, L.stream, L.ev_start,
+                         L.ev_stop, L.prm, L.blob, L.offsets, L.rows, L.rec, L.tasks, L.n, L.filter, L.nwords, L.use_lds,
+                         L.present);
     } else {
-        launch_timed(k_bloom<H, CHUNK, OP, false>, dim3(grid), dim3(256), lds, L.stream, L.ev_start, L.ev_stop, L.prm,
-                     L.blob, L.offsets, L.rows, L.rec, L.tasks, L.n, L.filter, L.nwords, L.use_lds, L.present);
+        launch_timed(k_bloom<H, CHUNK, OP, false, 0, OR_MODE>, dim3(grid), dim3(256), lds, L.stream, L.ev_start,
+                     L.ev_stop, L.prm, L.blob, L.offsets, L.rows, L.rec, L.tasks, L.n, L.filter, L.nwords, L.use_lds,
+                     L.present);
     }
     return hipGetLastError();
 }
@@ -291,8 +282,13 @@ static hipError_t launch_family(const BloomLaunch& L) {
     const uint64_t want = (L.n + block - 1) / block;
     const uint32_t grid = (uint32_t)(want < L.max_grid ? (want ? want : 1) : L.max_grid);
     switch (L.op) {
-        case BloomOp::Add: return launch_op<H, CHUNK, 0>(L, grid);
-        case BloomOp::Test: return launch_op<H, CHUNK, 1>(L, grid);
+        case BloomOp::Add:
+            switch (L.or_mode) {
+                case 0: return launch_op<H, CHUNK, 0, 0>(L, grid);
+                case 2: return launch_op<H, CHUNK, 0, 2>(L, grid);
+                default: return launch_op<H, CHUNK, 0, 1>(L, grid);
+            }
+        case BloomOp::Test: return launch_op<H, CHUNK, 1, 0>(L, grid);
         case BloomOp::Indices:
             hipLaunchKernelGGL((k_bloom_indices<H, CHUNK>), dim3(grid), dim3(block), 0, L.stream, L.prm, L.blob,
                                L.offsets, L.n, L.indices);

@@ -61,6 +61,7 @@ struct dsy_ctx {
     uint32_t max_grid = 2048;
     int bloom_diag = 0;  // DSY_BLOOM_DIAG at creation: single-filter ceiling diagnostics (k_bloom DIAG)
     int pair_diag = 0;   // DSY_PAIR_DIAG at creation: responder ceiling diagnostics (k_pair_test DIAG)
+    int or_mode = 1;     // DSY_OR_MODE at creation: filter-build atomics (filter_set_all OR_MODE, dsy_message.h)
     uint32_t timing = 0;  // bit i: bracket class i with events
     std::vector<PendingTimer> pending;
     std::vector<hipEvent_t> event_pool;
@@ -305,6 +306,7 @@ int run_bloom(dsy_ctx* c, BloomOp op, const dsy_bloom_params* p, const uint8_t* 
     L.max_grid = c->max_grid;
     L.stream = c->stream;
     L.diag = c->bloom_diag;
+    L.or_mode = c->or_mode;
     // Large batches hash in length-bucketed order (a wave's 64 lanes then run the same number of blocks); the
     // sort costs ~40 B of traffic per key next to the key bytes themselves.
     if (op != BloomOp::Indices && n >= kLenSortMin) {
@@ -366,6 +368,7 @@ int dsy_ctx_create(int device, dsy_ctx** out) {
     c->max_grid = (uint32_t)std::max(cus, 1) * 8;
     if (const char* v = getenv("DSY_BLOOM_DIAG")) c->bloom_diag = atoi(v);
     if (const char* v = getenv("DSY_PAIR_DIAG")) c->pair_diag = atoi(v);
+    if (const char* v = getenv("DSY_OR_MODE")) c->or_mode = atoi(v);
     hipHostMalloc(&c->pinned, 4096, hipHostMallocDefault);
     *out = c;
     return DSY_OK;
@@ -1795,6 +1798,7 @@ static SimLaunch sim_launch(dsy_ctx* c, const dsy_sim_config* cfg) {
     SimLaunch L{};
     L.cfg = *cfg;
     L.stream = c->stream;
+    L.or_mode = c->or_mode;
     return L;
 }
 

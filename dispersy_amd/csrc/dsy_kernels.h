@@ -55,6 +55,7 @@ struct BloomLaunch {
     uint32_t max_grid;
     hipStream_t stream;
     int diag;               // k_bloom DIAG: 0 = the product kernel, 1 / 2 = compute / gather ceiling diagnostics
+    int or_mode;            // filter build: filter_set_all OR_MODE (dsy_message.h)
     hipEvent_t ev_start, ev_stop;  // when set: recorded by the hashing kernel's own dispatch (launch_timed)
 };
 
@@ -297,6 +298,7 @@ struct SimLaunch {
     unsigned long long* tested;
     unsigned long long* stats;
     unsigned long long* work;  // [kSimTestedSlots][4]: build blocks, build lane-block slots, respond blocks, respond slots
+    int or_mode;               // claim filter build: filter_set_all OR_MODE (dsy_message.h)
     hipStream_t stream;
 };
 

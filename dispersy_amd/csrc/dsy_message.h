@@ -516,4 +516,61 @@ __device__ __forceinline__ uint32_t filter_has_all(W* fb, const H& st, uint32_t 
     return ok & 1u;
 }
 
+// Filter build of one key per lane (bloomfilter.py:172-178: filter |= 1 << pos for its k positions).  Called by the
+// whole wave (`active`: the lane holds a key), so the wave-level modes can ballot and shuffle.
+//   OR_MODE 0  one atomic OR per lane per probe.
+//   OR_MODE 1  the k words are read first (one batch, as filter_has_all); a probe's OR is issued only by the lanes
+//              whose bit is still clear, and skipped by the wave when none is (a saturating filter -- 100 k keys
+//              into a 10 Kbit MTU filter -- needs almost no atomics after its first few thousand keys).
+//   OR_MODE 2  OR_MODE 1, and when at most kOrLeaders lanes still need a probe, the lanes that need the same word
+//              are merged into one OR by a leader (wave-aggregated atomicOr: a wave OR-reduction per distinct word).
+static constexpr int kOrLeaders = 4;
+template <class H, int CHUNK, int OR_MODE, class W>
+__device__ __forceinline__ void filter_set_all(W* fb, const H& st, uint32_t k, uint64_t m, bool active) {
+    constexpr int kmax = ChunkLimit<H, CHUNK>::kmax;
+    if constexpr (OR_MODE == 0) {
+#pragma unroll
+        for (int j = 0; j < kmax; ++j) {
+            if (active && j < (int)k) {
+                const uint64_t pos = bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, j), m);
+                atomicOr(&fb[pos >> 5], 1u << (pos & 31));
+            }
+        }
+        return;
+    }
+    uint32_t w[kmax], idx[kmax], bit[kmax];
+#pragma unroll
+    for (int j = 0; j < kmax; ++j) {
+        const uint64_t pos = active ? bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, j), m) : 0;
+        idx[j] = (uint32_t)(pos >> 5);
+        bit[j] = 1u << (pos & 31);
+        w[j] = fb[idx[j]];
+    }
+#pragma unroll
+    for (int j = 0; j < kmax; ++j) asm volatile("" : "+v"(w[j])::"memory");
+#pragma unroll
+    for (int j = 0; j < kmax; ++j) {
+        const bool need = active && j < (int)k && !(w[j] & bit[j]);
+        if constexpr (OR_MODE == 2) {
+            uint64_t pend = __ballot(need);
+            if (!pend) continue;
+            if (__popcll(pend) <= kOrLeaders) {
+                const uint32_t lane = threadIdx.x & 63;
+                while (pend) {
+                    const int leader = __builtin_ctzll(pend);
+                    const uint32_t wi = (uint32_t)__shfl((int)idx[j], leader, 64);
+                    const bool same = need && idx[j] == wi;
+                    uint32_t v = same ? bit[j] : 0u;
+#pragma unroll
+                    for (int d = 32; d >= 1; d >>= 1) v |= (uint32_t)__shfl_xor((int)v, d, 64);
+                    if (lane == (uint32_t)leader) atomicOr(&fb[wi], v);
+                    pend &= ~__ballot(same);
+                }
+                continue;
+            }
+        }
+        if (need) atomicOr(&fb[idx[j]], bit[j]);
+    }
+}
+
 }  // namespace dsy

@@ -158,9 +158,8 @@ __host__ __device__ constexpr uint32_t sim_build_wave_lds(uint32_t nwords) {
 
 // one wave per local requester: list its packets, put the claimed ones in block-count order (a counting sort in
 // LDS: the filter is an OR, so the hashing order is free, and equal-length lanes finish together), hash them into
-// an LDS-resident filter (ds_or_b32; lanes that hit the same word in one instruction are merged by the LDS atomic
-// unit), write the claim record
-template <class H, int CHUNK>
+// an LDS-resident filter (filter_set_all, OR_MODE as there), write the claim record
+template <class H, int CHUNK, int OR_MODE>
 __global__ void __launch_bounds__(256) k_sim_build_claims(dsy_sim_config c, uint32_t round, const uint8_t* __restrict__ ublob,
                                                           const uint64_t* __restrict__ uoff, const uint32_t* __restrict__ bits,
                                                           uint8_t* __restrict__ out, const uint32_t* __restrict__ slots,
@@ -217,19 +216,13 @@ __global__ void __launch_bounds__(256) k_sim_build_claims(dsy_sim_config c, uint
     for (uint32_t i0 = 0; i0 < n; i0 += 64) {
         const uint32_t i = i0 + lane;
         wave_work(i < n ? n_blocks(1 + (uint32_t)(uoff[sorted[i] + 1] - uoff[sorted[i]]), blk, lenb) : 0u, wblocks, wslots);
+        H st;
         if (i < n) {
             const uint32_t id = sorted[i];
             KeyView kv{ublob + uoff[id], (uint32_t)(uoff[id + 1] - uoff[id]), pre, 1};
-            H st;
             hash_key<H>(kv, st);
-#pragma unroll
-            for (int j = 0; j < ChunkLimit<H, CHUNK>::kmax; ++j) {
-                if (j < (int)c.k) {
-                    const uint64_t pos = bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, j), c.m_bits);
-                    atomicOr(&filt[pos >> 5], 1u << (pos & 31));
-                }
-            }
         }
+        filter_set_all<H, CHUNK, OR_MODE>(filt, st, c.k, c.m_bits, i < n);
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
@@ -375,8 +368,10 @@ static hipError_t sim_family(int op, const SimLaunch& L) {
     if (op == 0) {
         if (!local) return hipSuccess;
         const size_t lds = 4 * (size_t)sim_build_wave_lds((uint32_t)((L.cfg.m_bits + 31) / 32));
-        hipLaunchKernelGGL((k_sim_build_claims<H, CHUNK>), dim3((uint32_t)((local + 3) / 4)), dim3(256), lds, L.stream, L.cfg,
-                           L.round, L.ublob, L.uoff, L.bits, L.out, L.slots, L.work);
+        auto kern = L.or_mode == 0 ? k_sim_build_claims<H, CHUNK, 0>
+                                   : L.or_mode == 2 ? k_sim_build_claims<H, CHUNK, 2> : k_sim_build_claims<H, CHUNK, 1>;
+        hipLaunchKernelGGL(kern, dim3((uint32_t)((local + 3) / 4)), dim3(256), lds, L.stream, L.cfg, L.round, L.ublob,
+                           L.uoff, L.bits, L.out, L.slots, L.work);
     } else {
         if (!L.n_in) return hipSuccess;
         hipLaunchKernelGGL((k_sim_respond<H, CHUNK>), dim3((uint32_t)((L.n_in + 3) / 4)), dim3(256), 0, L.stream, L.cfg,

@@ -210,3 +210,24 @@ def test_largest_filter_2_24_against_oracle():
     expect = [all(bits[p] for p in ref.indices(k)) for k in probes]
     assert got.astype(bool).tolist() == expect
     assert got[:1000].all() and sum(expect[1000:]) < 10
+
+
+@pytest.mark.parametrize("or_mode", [0, 1, 2])
+@pytest.mark.parametrize("m,f,prefix,n", [(10160, 0.01, b"\x00\x01\x02\x03", 40_000), (10160, 0.01, b"\x2a", 300),
+                                          (4096, 0.001, b"x", 40_000), (1 << 20, 0.01, b"\x07", 5_000),
+                                          (64, 0.5, b"", 3_000)])
+def test_filter_build_or_modes(monkeypatch, or_mode, m, f, prefix, n):
+    """Every filter-build mode (DSY_OR_MODE: per-lane atomics, skip-if-set, wave-aggregated leaders) gives the oracle's
+    bytes: saturating MTU and SHA-1 filters (length-sorted, LDS-DMA), a sparse one, an HBM-resident 2^20 filter, and
+    a 64-bit filter where most lanes of a wave hit the same word."""
+    monkeypatch.setenv("DSY_OR_MODE", str(or_mode))
+    ctx = _native.Context(0)
+    try:
+        blob, off = random_packets(m + n + or_mode, n, 60, 1500)
+        bf = BloomFilter(m, f, prefix)
+        got = ctx.bloom_add(bf.params, blob, off, b"\x00" * (len(bf.bytes) + (-len(bf.bytes)) % 4))
+        ref = OracleBloom.from_m_f(m, f, prefix)
+        ref.add_keys(blob[int(off[i]):int(off[i + 1])] for i in range(n))
+        assert got[:len(bf.bytes)] == ref.to_bytes()
+    finally:
+        ctx.close()
