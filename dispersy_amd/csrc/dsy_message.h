@@ -195,6 +195,79 @@ struct DmaGeometry {
     static constexpr int kWaveBytes = NB * kStageBytes;
 };
 
+// The DMA pieces one lane moves for its wave's 64 keys.  In wave instruction i of a stage the lane copies 16 bytes
+// of key p_i = kKeysPerInst * i + lane / kChunks (chunk c_i of that key's stage window, rotated as above).  The
+// keys' addresses and lengths are fixed for the whole hash, so each lane gathers its kInsts (address, live stages)
+// pairs once per key -- kInsts x 3 shuffles -- instead of once per stage: per stage an instruction is then a
+// compare, a 64-bit add and the load, with no LDS round trip (ds_bpermute) and no register pressure from hoisted
+// per-stage address math between the loads (the per-stage form spilled to scratch in k_pair_test, and every
+// scratch reload waited on vmcnt(0) -- on the stage's own DMA -- in the middle of issuing it).
+template <int S>
+struct DmaLanes {
+    using G = DmaGeometry<S, 1>;
+    uint64_t addr[G::kInsts];  // key p_i's stage-0 piece address
+    uint32_t live[G::kInsts];  // stages of key p_i that hold message bytes
+    // base: the lane's stage-0 window start (stage s covers [base + s*S*64, +S*64)); bytes: message bytes from base
+    __device__ __forceinline__ void init(uint64_t base, uint32_t bytes) {
+        const uint32_t lane = threadIdx.x & 63;
+        const uint32_t nst = (bytes + S * 64 - 1) / (S * 64);
+#pragma unroll
+        for (int i = 0; i < G::kInsts; ++i) {
+            const int p = G::kKeysPerInst * i + (int)(lane / G::kChunks);
+            const uint32_t blo = __shfl((int)(uint32_t)base, p, 64), bhi = __shfl((int)(uint32_t)(base >> 32), p, 64);
+            live[i] = (uint32_t)__shfl((int)nst, p, 64);
+            const uint32_t c = ((lane % G::kChunks) + ((uint32_t)p >> G::kShift)) % G::kChunks;
+            addr[i] = (((uint64_t)bhi << 32) | blo) + 16 * c;
+        }
+    }
+    // stage s of every key into the wave's LDS buffer (skip: no loads -- the DIAG compute-ceiling builds)
+    template <bool SKIP = false>
+    __device__ __forceinline__ void issue(uint32_t s, uint8_t* lds_wave) const {
+        if constexpr (SKIP) return;
+#pragma unroll
+        for (int i = 0; i < G::kInsts; ++i)
+            if (s < live[i])
+                __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)(addr[i] + (uint64_t)s * (S * 64)),
+                                                 (__attribute__((address_space(3))) void*)(lds_wave + i * 1024), 16, 0, 0);
+    }
+};
+
+// DmaLanes for line-aligned keys (hash_key_dma_lines): each piece is named by its 128-byte line index relative to a
+// wave-uniform base (u32: 512 GB of lines) and the live-stage counts of two keys share a register, so the per-key
+// list costs 12 VGPRs instead of 24 -- the responder kernel sits at its 128-VGPR cap.
+struct DmaLinePieces {
+    using G = DmaGeometry<2, 1>;
+    uint32_t line[G::kInsts];      // key p_i's first line, in lines from the base
+    uint32_t live2[G::kInsts / 2]; // live stages (lines) of keys p_2j (low half) and p_2j+1 (high half)
+    __device__ __forceinline__ void init(const uint8_t* base, const uint8_t* key, uint32_t len) {
+        const uint32_t lane = threadIdx.x & 63;
+        const uint32_t my_line = (uint32_t)((uint64_t)(key - base) >> 7);
+        const uint32_t my_live = (len + 127) >> 7;  // <= 512 for a 65535-byte packet
+#pragma unroll
+        for (int i = 0; i < G::kInsts; ++i) {
+            const int p = G::kKeysPerInst * i + (int)(lane / G::kChunks);
+            line[i] = (uint32_t)__shfl((int)my_line, p, 64);
+            const uint32_t lv = (uint32_t)__shfl((int)my_live, p, 64);
+            if (i & 1) live2[i / 2] |= lv << 16;
+            else live2[i / 2] = lv;
+        }
+    }
+    template <bool SKIP = false>
+    __device__ __forceinline__ void issue(uint32_t s, const uint8_t* base, uint8_t* lds_wave) const {
+        if constexpr (SKIP) return;
+        const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+        for (int i = 0; i < G::kInsts; ++i) {
+            const uint32_t lv = (i & 1) ? live2[i / 2] >> 16 : live2[i / 2] & 0xffffu;
+            const int p = G::kKeysPerInst * i + (int)(lane / G::kChunks);
+            const uint32_t c = ((lane % G::kChunks) + ((uint32_t)p >> G::kShift)) % G::kChunks;
+            if (s < lv)
+                __builtin_amdgcn_global_load_lds((const void*)(base + ((uint64_t)(line[i] + s) << 7) + 16 * c),
+                                                 (__attribute__((address_space(3))) void*)(lds_wave + i * 1024), 16, 0, 0);
+        }
+    }
+};
+
 // Flags: kDmaSkipDead -- (NB == 2 only, where every wait is vmcnt(0)) lanes whose key has ended issue no load;
 // kDmaPrio -- raise the wave's issue priority while it issues a stage's loads.
 enum { kDmaSkipDead = 1, kDmaPrio = 2 };
@@ -332,22 +405,10 @@ __device__ __forceinline__ void hash_key_dma_reg(const KeyView& kv, H& st, uint8
     const uint32_t tmin = wave_min_u32(total);
     uint32_t preword = 0;
     for (uint32_t j = 0; j < r; ++j) preword |= (uint32_t)kv.pre[j] << (8 * j);
-    const uint64_t base = (uint64_t)(uintptr_t)kv.key - r;
-    auto issue = [&](uint32_t s) {
-#pragma unroll
-        for (int i = 0; i < G::kInsts; ++i) {
-            const int p = G::kKeysPerInst * i + (int)(lane / G::kChunks);
-            const uint32_t blo = __shfl((int)(uint32_t)base, p, 64), bhi = __shfl((int)(uint32_t)(base >> 32), p, 64);
-            const uint32_t pend = __shfl((int)total, p, 64);
-            const uint32_t c = ((lane % G::kChunks) + ((uint32_t)p >> G::kShift)) % G::kChunks;
-            const uint64_t b64 = ((uint64_t)bhi << 32) | blo;
-            if (MODE != 1 && s * (S * 64) < pend)
-                __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)(b64 + s * (S * 64) + 16 * c),
-                                                 (__attribute__((address_space(3))) void*)(lds_wave + i * 1024), 16, 0, 0);
-        }
-    };
+    DmaLanes<S> dl;
+    dl.init((uint64_t)(uintptr_t)kv.key - r, total);
     st.init();
-    if (nst) issue(0);
+    if (nst) dl.template issue<MODE == 1>(0, lds_wave);
     for (uint32_t s = 0; s < nst; ++s) {
         __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): stage s has landed
         __builtin_amdgcn_wave_barrier();
@@ -365,7 +426,7 @@ __device__ __forceinline__ void hash_key_dma_reg(const KeyView& kv, H& st, uint8
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the buffer is free again
         __builtin_amdgcn_wave_barrier();
-        if (s + 1 < nst) issue(s + 1);
+        if (s + 1 < nst) dl.template issue<MODE == 1>(s + 1, lds_wave);
 #pragma unroll
         for (int bb = 0; bb < S; ++bb) {
             const uint32_t b = S * s + bb;
@@ -386,10 +447,12 @@ __device__ __forceinline__ void hash_key_dma_reg(const KeyView& kv, H& st, uint8
 // no line is fetched twice (tools/hashbench: 70 vs 57 Gblk/s MD5 over the same packets, 4.3 vs 3.5 TB/s).  The
 // message (prefix || packet) is the packet shifted by the prefix length r, which is wave-uniform (one claim per
 // wave): a uniform alignbyte funnel with a one-dword carry from the previous stage.  Single 8 KiB buffer per wave,
-// like hash_key_dma_reg<H, 2>.  Requires r <= 4 and kv.key 128-byte aligned; lines past the packet hold only
+// like hash_key_dma_reg<H, 2>.  Requires r <= 4 and kv.key 128-byte aligned, at most 2^32 lines past `lines` (the
+// copy's base, wave-uniform); lines past the packet hold only
 // padding and are not loaded.  preword: the r prefix bytes, little-endian (wave-uniform: read once per claim).  MODE as in hash_key_dma_reg (k_pair_test DIAG diagnostics only).
 template <class H, int MODE = 0>
-__device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uint8_t* lds_wave, uint32_t preword) {
+__device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uint8_t* lds_wave, uint32_t preword,
+                                                   const uint8_t* lines) {
     static_assert(H::block_bytes == 64, "LDS-DMA staging is for 64-byte blocks");
     using G = DmaGeometry<2, 1>;
     const uint32_t lane = threadIdx.x & 63;
@@ -402,25 +465,13 @@ __device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uin
     for (int d = 32; d >= 1; d >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, d, 64));
     const uint32_t nst = (nbmax + 1) / 2;
     const uint32_t tmin = wave_min_u32(total);
-    const uint64_t base = (uint64_t)(uintptr_t)kv.key;  // 128-byte aligned
-    auto issue = [&](uint32_t s) {
-#pragma unroll
-        for (int i = 0; i < G::kInsts; ++i) {
-            const int p = G::kKeysPerInst * i + (int)(lane / G::kChunks);
-            const uint32_t blo = __shfl((int)(uint32_t)base, p, 64), bhi = __shfl((int)(uint32_t)(base >> 32), p, 64);
-            const uint32_t pend = __shfl((int)len, p, 64);
-            const uint32_t c = ((lane % G::kChunks) + ((uint32_t)p >> G::kShift)) % G::kChunks;
-            const uint64_t b64 = ((uint64_t)bhi << 32) | blo;
-            if (MODE != 1 && s * 128 < pend)
-                __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)(b64 + s * 128 + 16 * c),
-                                                 (__attribute__((address_space(3))) void*)(lds_wave + i * 1024), 16, 0, 0);
-        }
-    };
+    DmaLinePieces dl;
+    dl.init(lines, kv.key, len);  // 128-byte aligned: stage s is line s of the packet
     st.init();
     // carry: the dword before the stage's first one; its top r bytes are the message bytes before the stage
     uint32_t carry = r ? preword << (8 * (4 - r)) : 0u;
     const uint32_t sh = (4 - r) & 3;  // alignbyte shift for r in 1..3
-    if (nst) issue(0);
+    if (nst) dl.template issue<MODE == 1>(0, lines, lds_wave);
     for (uint32_t s = 0; s < nst; ++s) {
         __builtin_amdgcn_s_waitcnt(0x0f70);
         __builtin_amdgcn_wave_barrier();
@@ -435,7 +486,7 @@ __device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uin
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
-        if (s + 1 < nst) issue(s + 1);
+        if (s + 1 < nst) dl.template issue<MODE == 1>(s + 1, lines, lds_wave);
         carry = d[32];
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb) {

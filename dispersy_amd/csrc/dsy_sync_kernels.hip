@@ -644,7 +644,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         }
         H st;
         if constexpr (DMA) {
-            hash_key_dma_lines<H, DIAG>(kv, st, my_lds, q.prefix_word);  // prefixes > 4 bytes go to DMA = false
+            hash_key_dma_lines<H, DIAG>(kv, st, my_lds, q.prefix_word, L.st.lines);  // prefixes > 4 bytes go to DMA = false
         } else {
             hash_key<H>(kv, st);
         }
