@@ -1493,7 +1493,9 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     bool fresh = false;
     if ((rc = ws_get(c, "ticket", 64, &d_ticket, &fresh))) return rc;
     if (fresh) HIP_TRY(hipMemsetAsync(d_ticket, 0, 64, c->stream));
-    if ((rc = ws_get(c, "resp_io", io_b, &d_io))) return rc;
+    bool io_fresh = false;
+    if ((rc = ws_get(c, "resp_io", io_b, &d_io, &io_fresh))) return rc;
+    if (io_fresh) HIP_TRY(hipMemsetAsync(d_io, 0, io_b, c->stream));  // flags start (and stay, k_compact) at zero
     if ((rc = ws_get(c, "plans", std::max<size_t>((size_t)R * J, 1) * sizeof(Plan), &d_plans))) return rc;
     if ((rc = ws_get(c, "state", std::max<size_t>(R, 1) * sizeof(ReqState), &d_state))) return rc;
     if ((rc = ws_get(c, "pairs", pool * 8, &d_pairs))) return rc;
@@ -1611,9 +1613,14 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     const uint64_t per_claim = byte_limit <= 0 ? 1 : (s->min_len > 0 ? (uint64_t)byte_limit / s->min_len + 2 : ~0ull);
     const bool dev_caps = per_claim != ~0ull && per_claim <= (1ull << 26) / std::max<uint32_t>(R, 1);
     PendingTimer t;
-    timer_begin(c, &t, kTimeSelect);
-    HIP_TRY(launch_setup(L, h_in, d_in, in_b, d_io, head_b, dev_caps ? per_claim : 0));
-    timer_end(c, &t);
+    // one meta and device-side capacities (the common case): the setup runs inside the first window's fill
+    // (k_fill_first); otherwise k_setup plans every (claim, meta) first
+    const bool fused_first = J == 1 && dev_caps && R > 0;
+    if (!fused_first) {
+        timer_begin(c, &t, kTimeSelect);
+        HIP_TRY(launch_setup(L, h_in, d_in, in_b, d_io, head_b, dev_caps ? per_claim : 0));
+        timer_end(c, &t);
+    }
     if (dev_caps) {
         cap_total = per_claim * R;
         if ((rc = ws_get(c, "out", std::max<uint64_t>(cap_total, 1) * 8, &d_out))) return rc;
@@ -1640,7 +1647,7 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     void *d_packed_v, *d_packed_off_v;
     if ((rc = ws_get(c, "packed", std::max<uint64_t>(cap_total, 1) * 8, &d_packed_v))) return rc;
     if ((rc = ws_get(c, "packed_off", ((size_t)R + 1) * 8, &d_packed_off_v))) return rc;
-    bool first = true, ran = false;
+    bool first = true, ran = false, first_fill = true;
     for (;;) {
         std::vector<std::pair<size_t, size_t>> runs;  // per family: (first slot, slots)
         size_t n_act = 0;
@@ -1671,25 +1678,34 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
             L.fill_clock = (uint64_t*)d_fc;
         }
         timer_begin(c, &t, kTimeSelect);
-        HIP_TRY(launch_fill(L));
+        if (first_fill && fused_first)
+            HIP_TRY(launch_fill_first(L, h_in, d_in, in_b, d_io, cnt_b, per_claim,
+                                      fam_active.size() == 1 ? nullptr : h_act0));
+        else
+            HIP_TRY(launch_fill(L));
+        first_fill = false;
         timer_end(c, &t);
         if (fill_profile) {  // per-window stderr line: k_fill phase durations over the workgroups (s_memtime ticks)
             std::vector<uint64_t> fc(n_act * 4);
             HIP_TRY(hipMemcpyAsync(fc.data(), d_fc, n_act * 32, hipMemcpyDeviceToHost, c->stream));
             HIP_TRY(hipStreamSynchronize(c->stream));
-            uint64_t t0 = ~0ull, t2 = 0, sel = 0, srt = 0, mx_sel = 0, mx_srt = 0, n = 0;
+            uint64_t t0 = ~0ull, t2 = 0, sel = 0, srt = 0, stp = 0, mx_sel = 0, mx_srt = 0, mx_stp = 0, n = 0;
             for (size_t a = 0; a < n_act; ++a) {
                 if (!fc[a * 4]) continue;
-                t0 = std::min(t0, fc[a * 4]);
+                t0 = std::min(t0, fc[a * 4 + 3]);
                 t2 = std::max(t2, fc[a * 4 + 2]);
+                stp += fc[a * 4] - fc[a * 4 + 3];
                 sel += fc[a * 4 + 1] - fc[a * 4];
                 srt += fc[a * 4 + 2] - fc[a * 4 + 1];
+                mx_stp = std::max(mx_stp, fc[a * 4] - fc[a * 4 + 3]);
                 mx_sel = std::max(mx_sel, fc[a * 4 + 1] - fc[a * 4]);
                 mx_srt = std::max(mx_srt, fc[a * 4 + 2] - fc[a * 4 + 1]);
                 ++n;
             }
-            if (n) fprintf(stderr, "fill_profile n=%llu span=%llu select avg=%llu max=%llu sort avg=%llu max=%llu\n",
-                           (unsigned long long)n, (unsigned long long)(t2 - t0), (unsigned long long)(sel / n),
+            // shader-clock ticks; setup = k_fill_first's host reads + plan (0 for k_fill)
+            if (n) fprintf(stderr, "fill_profile n=%llu span=%llu setup avg=%llu max=%llu select avg=%llu max=%llu "
+                           "sort avg=%llu max=%llu\n", (unsigned long long)n, (unsigned long long)(t2 - t0),
+                           (unsigned long long)(stp / n), (unsigned long long)mx_stp, (unsigned long long)(sel / n),
                            (unsigned long long)mx_sel, (unsigned long long)(srt / n), (unsigned long long)mx_srt);
             L.fill_clock = nullptr;
         }

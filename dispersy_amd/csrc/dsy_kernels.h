@@ -191,6 +191,10 @@ hipError_t launch_setup(const RespondLaunch& L, const void* h_src, void* d_dst, 
                         size_t zero_bytes, uint64_t per_claim_cap);
 static constexpr uint32_t kPackFusedMax = 8192;  // claims packed by one launch (k_pack_fused)
 hipError_t launch_fill(const RespondLaunch& L);
+// first window of a one-meta call with device-side capacities: k_setup fused into k_fill (every claim's plan, state and
+// window in one launch); h_act: the first active list in pinned host memory, or nullptr when window slot a is claim a
+hipError_t launch_fill_first(const RespondLaunch& L, const void* h_src, void* d_dst, size_t in_bytes, void* d_counters,
+                             size_t counter_bytes, uint64_t per_claim_cap, const uint32_t* h_act);
 // hash + test the window's pairs of the listed window slots, all of one (hash kind, chunk) family
 // long_prefix: the listed claims' prefixes are longer than 4 bytes (hashed without the LDS-DMA staging)
 hipError_t launch_pair_test_list(const RespondLaunch& L, int kind, uint32_t chunk, bool long_prefix,

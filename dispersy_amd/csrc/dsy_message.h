@@ -509,6 +509,9 @@ __device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uin
                 if (MODE != 2) st.compress(x);
                 else st.h[0] ^= x[0] ^ x[5] ^ x[10] ^ x[15];
             }
+            // keep block 1's message words from being formed while block 0 compresses (register pressure: the
+            // responder kernel's occupancy is set by its VGPR count)
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
 }
@@ -576,15 +579,17 @@ __device__ __forceinline__ uint32_t filter_has_all(W* fb, const H& st, uint32_t 
 //   OR_MODE 2  OR_MODE 1, and when at most kOrLeaders lanes still need a probe, the lanes that need the same word
 //              are merged into one OR by a leader (wave-aggregated atomicOr: a wave OR-reduction per distinct word).
 static constexpr int kOrLeaders = 4;
+// wbase: the lane's filter starts wbase words past fb (lanes of one wave may fill different filters; fb is uniform)
 template <class H, int CHUNK, int OR_MODE, class W>
-__device__ __forceinline__ void filter_set_all(W* fb, const H& st, uint32_t k, uint64_t m, bool active) {
+__device__ __forceinline__ void filter_set_all(W* fb, const H& st, uint32_t k, uint64_t m, bool active,
+                                               uint32_t wbase = 0) {
     constexpr int kmax = ChunkLimit<H, CHUNK>::kmax;
     if constexpr (OR_MODE == 0) {
 #pragma unroll
         for (int j = 0; j < kmax; ++j) {
             if (active && j < (int)k) {
                 const uint64_t pos = bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, j), m);
-                atomicOr(&fb[pos >> 5], 1u << (pos & 31));
+                atomicOr(&fb[wbase + (uint32_t)(pos >> 5)], 1u << (pos & 31));
             }
         }
         return;
@@ -593,7 +598,7 @@ __device__ __forceinline__ void filter_set_all(W* fb, const H& st, uint32_t k, u
 #pragma unroll
     for (int j = 0; j < kmax; ++j) {
         const uint64_t pos = active ? bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, j), m) : 0;
-        idx[j] = (uint32_t)(pos >> 5);
+        idx[j] = wbase + (uint32_t)(pos >> 5);
         bit[j] = 1u << (pos & 31);
         w[j] = fb[idx[j]];
     }

@@ -155,10 +155,17 @@ __device__ __forceinline__ void work_flush(unsigned long long* work, int which, 
 __host__ __device__ constexpr uint32_t sim_build_wave_lds(uint32_t nwords) {
     return (4 * kSimListCap + 256 + 16 + nwords * 4 + 15) / 16 * 16;
 }
+// LDS shared by the workgroup's four requesters: the pooled tails (key id, owner wave) in block-count order, a
+// 64-bin histogram and the pool's size
+static constexpr uint32_t kSimPoolLds = 256 * 2 + 256 + 64 * 4 + 16;
+__host__ __device__ constexpr uint32_t sim_build_lds(uint32_t nwords) { return 4 * sim_build_wave_lds(nwords) + kSimPoolLds; }
 
 // one wave per local requester: list its packets, put the claimed ones in block-count order (a counting sort in
 // LDS: the filter is an OR, so the hashing order is free, and equal-length lanes finish together), hash them into
-// an LDS-resident filter (filter_set_all, OR_MODE as there), write the claim record
+// an LDS-resident filter (filter_set_all, OR_MODE as there), write the claim record.  A wave hashes only its full
+// 64-key chunks; the tails (< 64 keys each, the requester's shortest) of the workgroup's four requesters are pooled,
+// sorted by block count, and hashed together in ceil(pool / 64) chunks, each key into its owner's filter -- ~150-key
+// stores otherwise leave a third of the lanes of every third chunk idle.
 template <class H, int CHUNK, int OR_MODE>
 __global__ void __launch_bounds__(256) k_sim_build_claims(dsy_sim_config c, uint32_t round, const uint8_t* __restrict__ ublob,
                                                           const uint64_t* __restrict__ uoff, const uint32_t* __restrict__ bits,
@@ -167,18 +174,28 @@ __global__ void __launch_bounds__(256) k_sim_build_claims(dsy_sim_config c, uint
     extern __shared__ __attribute__((aligned(16))) uint8_t sim_lds[];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t lp = (uint64_t)blockIdx.x * 4 + wv;
-    if (lp >= c.peer_end - c.peer_begin) return;  // wave-uniform
+    const bool live = lp < c.peer_end - c.peer_begin;  // wave-uniform; idle waves still meet the barriers
     const uint32_t nwords = (uint32_t)((c.m_bits + 31) / 32);
-    uint8_t* mine = sim_lds + wv * sim_build_wave_lds(nwords);
+    const uint32_t wave_b = sim_build_wave_lds(nwords);
+    uint8_t* mine = sim_lds + wv * wave_b;
     uint16_t* list = (uint16_t*)mine;
     uint16_t* sorted = list + kSimListCap;
     uint32_t* hist = (uint32_t*)(sorted + kSimListCap);
     uint8_t* pre = (uint8_t*)(hist + 64);
     uint32_t* filt = (uint32_t*)(pre + 16);
+    uint8_t* pool_base = sim_lds + 4 * wave_b;
+    uint16_t* pool_id = (uint16_t*)pool_base;            // [256] pooled tails, then (sorted) their hashing order
+    uint8_t* pool_own = pool_base + 512;                 // [256]
+    uint32_t* pool_hist = (uint32_t*)(pool_base + 768);  // [64]
+    uint32_t* pool_n = pool_hist + 64;
     const uint64_t p = c.peer_begin + lp;
+    const uint32_t blk = H::block_bytes, lenb = H::len_bytes;
+    auto bin_of = [&](uint32_t id) { return 63u - min(n_blocks(1 + (uint32_t)(uoff[id + 1] - uoff[id]), blk, lenb), 63u); };
     for (uint32_t i = lane; i < nwords; i += 64) filt[i] = 0;
     hist[lane] = 0;
-    uint32_t n = wave_list_ids(bits + lp * c.words, c.words, list, kSimListCap);
+    if (threadIdx.x < 64) pool_hist[threadIdx.x] = 0;
+    if (threadIdx.x == 0) *pool_n = 0;
+    uint32_t n = live ? wave_list_ids(bits + lp * c.words, c.words, list, kSimListCap) : 0u;
     // _select_and_fix(..., 0, capacity, True): the first capacity packets; over-full drops the (capacity+1)-th
     // global time (global times are distinct here) and the range ends at the last kept one
     uint64_t time_high = 0x7fffffffffffffffull;
@@ -186,10 +203,8 @@ __global__ void __launch_bounds__(256) k_sim_build_claims(dsy_sim_config c, uint
         n = c.capacity;
         time_high = (uint64_t)list[n - 1] + 1;
     }
-    const uint32_t prefix = sim_prefix(c, round, p);
+    const uint32_t prefix = live ? sim_prefix(c, round, p) : 0u;
     if (lane == 0) pre[0] = (uint8_t)prefix;
-    const uint32_t blk = H::block_bytes, lenb = H::len_bytes;
-    auto bin_of = [&](uint32_t id) { return 63u - min(n_blocks(1 + (uint32_t)(uoff[id + 1] - uoff[id]), blk, lenb), 63u); };
     __builtin_amdgcn_wave_barrier();
     for (uint32_t i = lane; i < n; i += 64) atomicAdd(&hist[bin_of(list[i])], 1u);
     __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -213,20 +228,73 @@ __global__ void __launch_bounds__(256) k_sim_build_claims(dsy_sim_config c, uint
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
     uint64_t wblocks = 0, wslots = 0;
-    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
-        const uint32_t i = i0 + lane;
-        wave_work(i < n ? n_blocks(1 + (uint32_t)(uoff[sorted[i] + 1] - uoff[sorted[i]]), blk, lenb) : 0u, wblocks, wslots);
+    const uint32_t n_full = n & ~63u;  // sorted longest first: the tail is the requester's shortest keys
+    for (uint32_t i0 = 0; i0 < n_full; i0 += 64) {
+        const uint32_t id = sorted[i0 + lane];
+        const uint32_t len = (uint32_t)(uoff[id + 1] - uoff[id]);
+        wave_work(n_blocks(1 + len, blk, lenb), wblocks, wslots);
+        KeyView kv{ublob + uoff[id], len, pre, 1};
         H st;
-        if (i < n) {
-            const uint32_t id = sorted[i];
-            KeyView kv{ublob + uoff[id], (uint32_t)(uoff[id + 1] - uoff[id]), pre, 1};
+        hash_key<H>(kv, st);
+        filter_set_all<H, CHUNK, OR_MODE>(filt, st, c.k, c.m_bits, true);
+    }
+    // pool the tail: rank by block count over the workgroup's tails (counting sort over 64 bins)
+    const uint32_t tail = n - n_full;
+    uint32_t my_at = 0;
+    if (lane == 0 && tail) my_at = atomicAdd(pool_n, tail);
+    my_at = (uint32_t)__shfl((int)my_at, 0, 64);
+    if (lane < tail) {
+        pool_id[my_at + lane] = sorted[n_full + lane];
+        pool_own[my_at + lane] = (uint8_t)wv;
+    }
+    __syncthreads();
+    const uint32_t pn = *pool_n;
+    uint32_t pid = 0, pown = 0, pbin = 0;
+    if (threadIdx.x < pn) {
+        pid = pool_id[threadIdx.x];
+        pown = pool_own[threadIdx.x];
+        pbin = bin_of(pid);
+        atomicAdd(&pool_hist[pbin], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const uint32_t h = pool_hist[threadIdx.x];
+        uint32_t incl = h;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(incl, d, 64);
+            if ((int)lane >= d) incl += o;
+        }
+        pool_hist[threadIdx.x] = incl - h;
+    }
+    __syncthreads();
+    if (threadIdx.x < pn) {
+        const uint32_t at = atomicAdd(&pool_hist[pbin], 1u);
+        pool_id[at] = (uint16_t)pid;      // every thread has read its entry (barrier above): safe to overwrite
+        pool_own[at] = (uint8_t)pown;
+    }
+    __syncthreads();
+    if (wv * 64 < pn) {  // wave wv hashes pooled chunk wv
+        const uint32_t i = wv * 64 + lane;
+        const bool act = i < pn;
+        const uint32_t id = act ? pool_id[i] : 0u;
+        const uint32_t own = act ? pool_own[i] : 0u;
+        uint8_t* own_lds = sim_lds + own * wave_b;
+        const uint32_t len = act ? (uint32_t)(uoff[id + 1] - uoff[id]) : 0u;
+        wave_work(act ? n_blocks(1 + len, blk, lenb) : 0u, wblocks, wslots);
+        H st;
+        if (act) {
+            KeyView kv{ublob + uoff[id], len, own_lds + 4 * kSimListCap + 256, 1};
             hash_key<H>(kv, st);
         }
-        filter_set_all<H, CHUNK, OR_MODE>(filt, st, c.k, c.m_bits, i < n);
+        // one LDS base for the wave, each lane's filter as a word offset from it (OR_MODE 2 merges by word index)
+        filter_set_all<H, CHUNK, OR_MODE>((uint32_t*)sim_lds, st, c.k, c.m_bits, act,
+                                          (own * wave_b + 4 * kSimListCap + 256 + 16) / 4);
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
+    __syncthreads();
     work_flush(work, 0, wblocks, wslots);
+    if (!live) return;
     const uint64_t q = sim_partner(c, round, p);
     uint8_t* rec = out + (uint64_t)slots[lp] * c.claim_bytes;
     if (lane == 0) {
@@ -367,7 +435,7 @@ static hipError_t sim_family(int op, const SimLaunch& L) {
     const uint64_t local = L.cfg.peer_end - L.cfg.peer_begin;
     if (op == 0) {
         if (!local) return hipSuccess;
-        const size_t lds = 4 * (size_t)sim_build_wave_lds((uint32_t)((L.cfg.m_bits + 31) / 32));
+        const size_t lds = sim_build_lds((uint32_t)((L.cfg.m_bits + 31) / 32));
         auto kern = L.or_mode == 0 ? k_sim_build_claims<H, CHUNK, 0>
                                    : L.or_mode == 2 ? k_sim_build_claims<H, CHUNK, 2> : k_sim_build_claims<H, CHUNK, 1>;
         hipLaunchKernelGGL(kern, dim3((uint32_t)((local + 3) / 4)), dim3(256), lds, L.stream, L.cfg, L.round, L.ublob,

@@ -90,7 +90,7 @@ __device__ __forceinline__ uint64_t permute(uint64_t x, uint64_t n, uint32_t bit
 }
 
 __device__ __forceinline__ uint64_t plan_one(const RespondLaunch& L, const DevRequest& q, const SegMeta& mt,
-                                             uint32_t idx, uint32_t r, uint32_t j) {
+                                             uint32_t idx, uint32_t r, uint32_t j, Plan* copy = nullptr) {
     uint64_t lo = q.time_low, hi = q.time_high;
     if (!L.include_inactive && mt.has_pruning) {
         // time_low' = min(max(time_low, global_time - inactive + 1), 2^63-1)   (community.py:2806)
@@ -136,6 +136,7 @@ __device__ __forceinline__ uint64_t plan_one(const RespondLaunch& L, const DevRe
         p.perm_key = (uint64_t)mix32(L.seed ^ ((uint64_t)r << 32) ^ j) << 32 | mix32(L.seed * 31 + r * 131 + j);
     }
     L.plans[idx] = p;
+    if (copy) *copy = p;
     return span;
 }
 
@@ -298,33 +299,35 @@ __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* l
     return before + incl - v;
 }
 
-__global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
+// The next window of claim r (window slot a_slot) from its cursor (meta j, candidate c, rows s of c already sent):
+// selection in send order, then the block-count sort into task records; thread 0 stores the new cursor in *S.
+// plan_at(j): the claim's plan for meta j.
+template <class PlanAt>
+__device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_slot, uint32_t r, const DevRequest& q,
+                                           ReqState* S, uint32_t j, uint64_t c, uint64_t s, PlanAt plan_at,
+                                           uint64_t clk_start, uint64_t clk0) {
     __shared__ uint64_t scan[kFillWaves + 2];
     __shared__ uint32_t first_cross;
-    const uint32_t a_slot = blockIdx.x;
-    const uint64_t clk0 = L.fill_clock ? __builtin_amdgcn_s_memtime() : 0;
-    const uint32_t r = L.act[a_slot];
-    ReqState* S = &L.state[r];
-    if (S->done) {
-        if (threadIdx.x == 0) S->n_window = 0;
-        return;
-    }
-    const DevRequest& q = L.reqs[r];
     const uint64_t W = L.window;
     // this window's missing-pair bits of the claim start clear (k_pair_test sets them)
     for (uint64_t w = threadIdx.x; w < W / 64; w += kFillThreads) L.miss_mask[(uint64_t)a_slot * (W / 64) + w] = 0;
     uint64_t* out = L.pair_row + (uint64_t)a_slot * W;
     uint64_t* out_off = L.pair_off + (uint64_t)a_slot * W;
     uint32_t* out_len = L.pair_len + (uint64_t)a_slot * W;
-    uint32_t j = S->meta;
-    uint64_t c = S->cand, s = S->sub, filled = 0;
+    uint64_t filled = 0;
     const uint64_t mod = q.modulo, off = q.offset;
+    // the sort's registers (below); a window that is one dense run of <= kFillThreads * kSortReg rows fills them
+    // during the selection itself (pair t = thread t % 256, register t / 256), so the sort reads nothing back
+    constexpr int kSortReg = 8;
+    uint32_t reg_off[kSortReg];  // line index: a pair's packet starts on a 128-byte line of the line copy
+    uint32_t reg_len[kSortReg];
+    uint64_t regs_rows = 0;  // pairs t < regs_rows are in the registers already (their pair_off is not written)
     // each thread takes kCand consecutive candidates, so one round of independent lookups covers
     // kFillThreads * kCand candidates (the fill is latency-bound: fewer, wider rounds)
-    constexpr int kCand = 4;
+    constexpr int kCand = 2;
     constexpr uint64_t kBatch = (uint64_t)kFillThreads * kCand;
     while (j < L.J && filled < W) {
-        const Plan p = L.plans[(uint64_t)r * L.J + j];
+        const Plan p = plan_at(j);
         if (c >= p.ncand) { ++j; c = 0; s = 0; continue; }
         if (p.dense && p.dir != DSY_RANDOM && (p.mode == 1 || mod <= 1)) {
             // One row per global time, consecutive: candidate -> row is arithmetic, no lookup and no scan.
@@ -343,7 +346,8 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
             const uint64_t take = avail < W - filled ? avail : W - filled;
             const RowRec* __restrict__ rec = L.st.rec;
             // kDenseU rows per thread per round, every load of the round issued before the first is consumed
-            constexpr int kDenseU = 8;
+            constexpr int kDenseU = kSortReg;
+            const bool to_regs = filled == 0 && take <= (uint64_t)kFillThreads * kDenseU;
             for (uint64_t i0 = 0; i0 < take; i0 += (uint64_t)kFillThreads * kDenseU) {
                 uint64_t row[kDenseU];
                 RowRec rr[kDenseU];
@@ -365,11 +369,16 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
                     const uint64_t i = i0 + threadIdx.x + (uint64_t)kFillThreads * u;
                     if (i < take) {
                         out[filled + i] = row[u];
-                        out_off[filled + i] = rr[u].off;
+                        if (!to_regs) out_off[filled + i] = rr[u].off;  // read back only by the sort
                         out_len[filled + i] = rr[u].len;
+                    }
+                    if (to_regs) {
+                        reg_off[u] = (uint32_t)(rr[u].off >> 7);
+                        reg_len[u] = rr[u].len;
                     }
                 }
             }
+            if (to_regs) regs_rows = take;
             filled += take;
             c = cs + take;
             if (c >= it1) c = p.ncand;  // the remaining candidates have no row
@@ -535,17 +544,24 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
     };
     for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads) hist[i] = 0;
     // small windows (the common case): every pair's (offset, length) loaded once, in one round, into registers
-    constexpr int kSortReg = 8;
     const bool in_regs = filled <= (uint64_t)kFillThreads * kSortReg;
-    uint64_t reg_off[kSortReg];
-    uint32_t reg_len[kSortReg];
     __syncthreads();  // the selection's placements (other threads' writes) are complete
-    if (in_regs) {
+    if (!in_regs && regs_rows) {
+        // the window outgrew the registers: their pairs' offsets go to pair_off like every other pair's
 #pragma unroll
         for (int u = 0; u < kSortReg; ++u) {
             const uint64_t t = threadIdx.x + (uint64_t)kFillThreads * u;
-            reg_off[u] = t < filled ? out_off[t] : 0;
-            reg_len[u] = t < filled ? out_len[t] : 0;
+            if (t < regs_rows) out_off[t] = (uint64_t)reg_off[u] << 7;
+        }
+    }
+    if (in_regs && regs_rows < filled) {
+#pragma unroll
+        for (int u = 0; u < kSortReg; ++u) {
+            const uint64_t t = threadIdx.x + (uint64_t)kFillThreads * u;
+            if (t >= regs_rows) {
+                reg_off[u] = t < filled ? (uint32_t)(out_off[t] >> 7) : 0u;
+                reg_len[u] = t < filled ? out_len[t] : 0;
+            }
         }
     }
     __syncthreads();
@@ -582,7 +598,7 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
             const uint64_t t = threadIdx.x + (uint64_t)kFillThreads * u;
             if (t < filled) {
                 PairTask tk;
-                tk.off = reg_off[u];
+                tk.off = (uint64_t)reg_off[u] << 7;
                 tk.len = reg_len[u];
                 tk.slot = (uint32_t)t;
                 task[atomicAdd(&hist[bin_of(tk.len)], 1u)] = tk;
@@ -602,13 +618,81 @@ __global__ void __launch_bounds__(kFillThreads) k_fill(RespondLaunch L) {
         fc[0] = clk0;
         fc[1] = clk1;
         fc[2] = __builtin_amdgcn_s_memtime();
-        fc[3] = filled;
+        fc[3] = clk_start;  // k_fill_first: before the claim's host reads and plan (k_fill: == clk0)
     }
+}
+
+__global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) k_fill(RespondLaunch L) {
+    const uint32_t a_slot = blockIdx.x;
+    const uint64_t clk0 = L.fill_clock ? __builtin_amdgcn_s_memtime() : 0;
+    const uint32_t r = L.act[a_slot];
+    ReqState* S = &L.state[r];
+    if (S->done) {
+        if (threadIdx.x == 0) S->n_window = 0;
+        return;
+    }
+    const Plan* plans = L.plans + (uint64_t)r * L.J;
+    fill_claim(L, a_slot, r, L.reqs[r], S, S->meta, S->cand, S->sub, [&](uint32_t j) { return plans[j]; }, clk0, clk0);
+}
+
+// First window of a call whose claims all serve one meta with device-side output capacities (respond_core's common
+// case): k_setup's work fused into k_fill -- one launch and one dependent chain per claim instead of two kernels.
+// Every workgroup copies its share of the staged upload (pinned host memory -> the device copy later kernels read);
+// workgroup a_slot reads its own claim and meta straight from the host copy, plans the claim (one lane), initialises
+// its state and fills its first window.  The status counters are zeroed by workgroup 0 (flags[kFlagChunks], which
+// the workgroups raise, is zero between calls: k_compact resets it).  identity_act: window slot a serves claim a.
+__global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) k_fill_first(RespondLaunch L, const uint4* __restrict__ src,
+                                                             uint4* __restrict__ dst, uint32_t in_words,
+                                                             uint4* __restrict__ counters, uint32_t counter_words,
+                                                             uint64_t per_claim_cap, const uint32_t* __restrict__ h_act) {
+    __shared__ DevRequest sq;
+    __shared__ Plan sp;
+    __shared__ ReqState sst;
+    const uint32_t a_slot = blockIdx.x;
+    const uint64_t clk0 = L.fill_clock ? __builtin_amdgcn_s_memtime() : 0;
+    const uint32_t tid = blockIdx.x * kFillThreads + threadIdx.x, nthr = gridDim.x * kFillThreads;
+    // the host reads of this thread are all issued before the first is consumed (each is a PCIe round trip)
+    constexpr uint32_t kQw = sizeof(DevRequest) / 16, kMw = sizeof(SegMeta) / 16;
+    const uint32_t r = h_act ? h_act[a_slot] : a_slot;
+    uint4 w = make_uint4(0, 0, 0, 0);
+    if (threadIdx.x < kQw) w = src[(size_t)r * kQw + threadIdx.x];
+    else if (threadIdx.x < kQw + kMw) w = src[(size_t)L.R * kQw + (threadIdx.x - kQw)];
+    uint4 cw = make_uint4(0, 0, 0, 0);
+    if (tid < in_words) cw = src[tid];
+    if (tid < in_words) dst[tid] = cw;
+    for (uint32_t i = tid + nthr; i < in_words; i += nthr) dst[i] = src[i];
+    if (blockIdx.x == 0)
+        for (uint32_t i = threadIdx.x; i < counter_words; i += kFillThreads) counters[i] = make_uint4(0, 0, 0, 0);
+    if (threadIdx.x < kQw) ((uint4*)&sq)[threadIdx.x] = w;
+    else if (threadIdx.x < kQw + kMw) ((uint4*)&sp)[threadIdx.x - kQw] = w;  // the SegMeta, parked in sp
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        SegMeta mt;
+        __builtin_memcpy(&mt, &sp, sizeof mt);
+        const uint64_t span = plan_one(L, sq, mt, r, r, 0, &sp);  // and in L.plans[r] for later windows
+        L.upper[r] = span;
+        ReqState st{};
+        st.cap = min(span, per_claim_cap);
+        st.out_base = (uint64_t)r * per_claim_cap;
+        st.done = span == 0;
+        sst = st;
+    }
+    __syncthreads();
+    ReqState* S = &L.state[r];
+    if (sst.done) {
+        if (threadIdx.x == 0) S[0] = sst;  // n_window = 0
+        return;
+    }
+    if (threadIdx.x == 0) S[0] = sst;  // the cursor fields are rewritten by fill_claim's thread 0 below
+    fill_claim(L, a_slot, r, sq, S, 0u, 0ull, 0ull, [&](uint32_t) { return sp; }, clk0,
+               L.fill_clock ? __builtin_amdgcn_s_memtime() : 0);
 }
 
 // -------------------------------------------------------------------------------------- k_pair_test
 // DIAG (DMA, 2-byte chunks; DSY_PAIR_DIAG): 0 the product kernel, 1 no packet loads (compute ceiling), 2 packet
 // loads without the compression (gather ceiling) -- diagnostics only, their answers are meaningless
+// Registers: 128 VGPRs (4 waves per SIMD, as the 8 KiB-per-wave LDS allows 5).  Forcing 5 waves (96 VGPRs) spills
+// per task and measured 234 -> 338 us per headline launch.
 template <class H, int CHUNK, bool DMA, int DIAG = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_pair_test(RespondLaunch L, const uint32_t* __restrict__ req_list,
                                                    uint32_t n_list) {
@@ -999,6 +1083,15 @@ hipError_t launch_setup(const RespondLaunch& L, const void* h_src, void* d_dst, 
 hipError_t launch_fill(const RespondLaunch& L) {
     if (!L.n_act) return hipSuccess;
     hipLaunchKernelGGL(k_fill, dim3(L.n_act), dim3(kFillThreads), 0, L.stream, L);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill_first(const RespondLaunch& L, const void* h_src, void* d_dst, size_t in_bytes, void* d_counters,
+                             size_t counter_bytes, uint64_t per_claim_cap, const uint32_t* h_act) {
+    if (!L.n_act) return hipSuccess;
+    hipLaunchKernelGGL(k_fill_first, dim3(L.n_act), dim3(kFillThreads), 0, L.stream, L, (const uint4*)h_src,
+                       (uint4*)d_dst, (uint32_t)(in_bytes / 16), (uint4*)d_counters, (uint32_t)(counter_bytes / 16),
+                       per_claim_cap, h_act);
     return hipGetLastError();
 }
 
