@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -1448,10 +1449,18 @@ static const uint64_t kWindow = 4096;
 static const uint64_t kMaxWindow = 1 << 18;
 static const uint64_t kMinSlots = 4096;
 
+// DSY_HOST_PROFILE: one stderr line per call with the host-side phases of respond_core (microseconds)
+static double host_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, uint32_t R, const uint8_t* d_filters,
                         uint64_t filters_len, const dsy_meta* metas, uint32_t J, uint64_t responder_gt,
                         int include_inactive, int64_t byte_limit, uint64_t seed, uint64_t** d_packed,
                         uint64_t** d_packed_off, uint64_t* total_pairs) {
+    static const bool host_profile = getenv("DSY_HOST_PROFILE") != nullptr;
+    double hp[6] = {host_profile ? host_us() : 0.0};
+    double hp_wait = 0.0;
     // ---- validate claims (payload.py:89-101, conversion.py:772-789) and their filters; group them by hash family
     // (kind x chunk width: one pair-test launch per family)
     // family id = (kind * 3 + chunk class) * 2 + long prefix (> 4 bytes: the byte-wise hashing path)
@@ -1564,6 +1573,7 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
             for (uint32_t r : fa) h_act0[a++] = r;
     }
     uint8_t* io = (uint8_t*)d_io;
+    if (host_profile) hp[1] = host_us();  // claims validated and staged
 
     RespondLaunch L{};
     L.st.blob = s->d_blob;
@@ -1725,7 +1735,10 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
         // speculatively pack the output now (it is redone if another window follows): the GPU packs while the
         // host wakes up and reads the status
         HIP_TRY(launch_pack(L, (uint64_t*)d_packed_v, (uint64_t*)d_packed_off_v, nullptr));
+        const double w0 = host_profile ? host_us() : 0.0;
+        if (host_profile && !hp[2]) hp[2] = w0;  // first window enqueued
         HIP_TRY(hipStreamSynchronize(c->stream));
+        if (host_profile) hp_wait += host_us() - w0;
         // capacity overflow can only come from a wrong min_len bound; report it loudly
         if (((const volatile uint64_t*)h_io)[kCntN]) return fail(DSY_ECAPACITY, "internal: a claim overflowed its output capacity");
         const volatile uint8_t* done = h_io + kHostHead;
@@ -1748,6 +1761,11 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     *total_pairs = h_tot[kCntPairs];
     *d_packed = (uint64_t*)d_packed_v;
     *d_packed_off = (uint64_t*)d_packed_off_v;
+    if (host_profile) {
+        hp[3] = host_us();
+        fprintf(stderr, "host_profile R=%u stage=%.1f enqueue=%.1f wait=%.1f total=%.1f\n", R, hp[1] - hp[0],
+                hp[2] ? hp[2] - hp[1] : 0.0, hp_wait, hp[3] - hp[0]);
+    }
     return DSY_OK;
 }
 

@@ -167,7 +167,7 @@ __host__ __device__ constexpr uint32_t sim_build_lds(uint32_t nwords) { return 4
 // sorted by block count, and hashed together in ceil(pool / 64) chunks, each key into its owner's filter -- ~150-key
 // stores otherwise leave a third of the lanes of every third chunk idle.
 template <class H, int CHUNK, int OR_MODE>
-__global__ void __launch_bounds__(256) k_sim_build_claims(dsy_sim_config c, uint32_t round, const uint8_t* __restrict__ ublob,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H::kind == DSY_SHA256 ? 3 : 4, 8))) k_sim_build_claims(dsy_sim_config c, uint32_t round, const uint8_t* __restrict__ ublob,
                                                           const uint64_t* __restrict__ uoff, const uint32_t* __restrict__ bits,
                                                           uint8_t* __restrict__ out, const uint32_t* __restrict__ slots,
                                                           unsigned long long* __restrict__ work) {
@@ -229,13 +229,20 @@ __global__ void __launch_bounds__(256) k_sim_build_claims(dsy_sim_config c, uint
     __builtin_amdgcn_wave_barrier();
     uint64_t wblocks = 0, wslots = 0;
     const uint32_t n_full = n & ~63u;  // sorted longest first: the tail is the requester's shortest keys
+    // MD5 / SHA-1 stage the packets through LDS with DMA (hash_key_dma_reg, one 64-byte block per key per stage:
+    // 4 KiB, the wave's id list, dead once sorted): 8 keys x 64 contiguous bytes per wave instruction instead of 64
+    // scattered 16-byte loads.  The universe blob keeps DSY_BLOB_GUARD readable bytes on both sides (sim.py).
+    constexpr bool kDma = H::kind == DSY_MD5 || H::kind == DSY_SHA1;
+    uint8_t* dma_buf = (uint8_t*)list;
+    static_assert(DmaGeometry<1, 1>::kWaveBytes == 2 * kSimListCap, "the DMA stage reuses the id list");
     for (uint32_t i0 = 0; i0 < n_full; i0 += 64) {
         const uint32_t id = sorted[i0 + lane];
         const uint32_t len = (uint32_t)(uoff[id + 1] - uoff[id]);
         wave_work(n_blocks(1 + len, blk, lenb), wblocks, wslots);
         KeyView kv{ublob + uoff[id], len, pre, 1};
         H st;
-        hash_key<H>(kv, st);
+        if constexpr (kDma) hash_key_dma_reg<H, 1>(kv, st, dma_buf);
+        else hash_key<H>(kv, st);
         filter_set_all<H, CHUNK, OR_MODE>(filt, st, c.k, c.m_bits, true);
     }
     // pool the tail: rank by block count over the workgroup's tails (counting sort over 64 bins)
@@ -283,10 +290,10 @@ __global__ void __launch_bounds__(256) k_sim_build_claims(dsy_sim_config c, uint
         const uint32_t len = act ? (uint32_t)(uoff[id + 1] - uoff[id]) : 0u;
         wave_work(act ? n_blocks(1 + len, blk, lenb) : 0u, wblocks, wslots);
         H st;
-        if (act) {
-            KeyView kv{ublob + uoff[id], len, own_lds + 4 * kSimListCap + 256, 1};
-            hash_key<H>(kv, st);
-        }
+        // idle lanes: an empty key at the universe's start (its prefix byte is read from the owner's LDS slot 0)
+        KeyView kv{ublob + (act ? uoff[id] : uoff[0]) , len, own_lds + 4 * kSimListCap + 256, 1};
+        if constexpr (kDma) hash_key_dma_reg<H, 1>(kv, st, dma_buf);
+        else if (act) hash_key<H>(kv, st);
         // one LDS base for the wave, each lane's filter as a word offset from it (OR_MODE 2 merges by word index)
         filter_set_all<H, CHUNK, OR_MODE>((uint32_t*)sim_lds, st, c.k, c.m_bits, act,
                                           (own * wave_b + 4 * kSimListCap + 256 + 16) / 4);
@@ -323,28 +330,38 @@ __global__ void k_sim_resp_counts(dsy_sim_config c, const uint8_t* __restrict__ 
 // one wave per incoming claim: the responder's packets in global-time order, 64 at a time; hash + probe; send the
 // missing ones until the byte budget is spent (the crossing packet is sent), then stop -- lazily, as the
 // reference's generator chain does
+// LDS of one responder wave in k_sim_respond: the responder's id list, the claim's filter (sized by m at launch), the
+// prefix byte, the response ids and (MD5 / SHA-1) a 4 KiB LDS-DMA stage
+__host__ __device__ constexpr uint32_t sim_respond_wave_lds(uint32_t nwords, bool dma) {
+    return (2 * kSimListCap + nwords * 4 + 16 + 2 * kSimRespMax + 15) / 16 * 16 + (dma ? 4096u : 0u);
+}
+
 template <class H, int CHUNK>
-__global__ void __launch_bounds__(256) k_sim_respond(dsy_sim_config c, const uint8_t* __restrict__ ublob,
-                                                     const uint64_t* __restrict__ uoff, const uint32_t* __restrict__ bits,
-                                                     const uint8_t* __restrict__ claims, uint64_t n_claims,
-                                                     uint8_t* __restrict__ out, const uint32_t* __restrict__ slots,
-                                                     unsigned long long* __restrict__ tested,
-                                                     unsigned long long* __restrict__ work) {
-    __shared__ uint16_t lists[4][kSimListCap];
-    __shared__ uint32_t filt[4][kSimFilterWordsMax];
-    __shared__ uint8_t pre[4][4];
-    __shared__ uint16_t outl[4][kSimRespMax];
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H::kind == DSY_SHA256 ? 3 : 4, 8)))
+k_sim_respond(dsy_sim_config c, const uint8_t* __restrict__ ublob, const uint64_t* __restrict__ uoff,
+              const uint32_t* __restrict__ bits, const uint8_t* __restrict__ claims, uint64_t n_claims,
+              uint8_t* __restrict__ out, const uint32_t* __restrict__ slots, unsigned long long* __restrict__ tested,
+              unsigned long long* __restrict__ work) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t sim_lds[];
+    // MD5 / SHA-1 stage the packets through LDS with DMA (hash_key_dma_reg, one block per stage), as the claim build
+    constexpr bool kDma = H::kind == DSY_MD5 || H::kind == DSY_SHA1;
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t ci = (uint64_t)blockIdx.x * 4 + wv;
-    if (ci >= n_claims) return;
+    if (ci >= n_claims) return;  // wave-uniform, no workgroup barrier below
+    const uint32_t nwords = (uint32_t)((c.m_bits + 31) / 32);
+    uint8_t* mine = sim_lds + wv * sim_respond_wave_lds(nwords, kDma);
+    uint8_t* dma_buf = mine;  // 4 KiB, first (16-byte aligned)
+    uint16_t* list = (uint16_t*)(mine + (kDma ? 4096 : 0));
+    uint32_t* filt = (uint32_t*)(list + kSimListCap);
+    uint8_t* pre = (uint8_t*)(filt + nwords);
+    uint16_t* outl = (uint16_t*)(pre + 16);
     const uint8_t* rec = claims + ci * c.claim_bytes;
     const dsy_sim_claim_header h = *(const dsy_sim_claim_header*)rec;
-    const uint32_t nwords = (uint32_t)((c.m_bits + 31) / 32);
     const uint32_t* fw = (const uint32_t*)(rec + sizeof(dsy_sim_claim_header));
-    for (uint32_t i = lane; i < nwords; i += 64) filt[wv][i] = fw[i];
-    if (lane == 0) pre[wv][0] = (uint8_t)h.prefix;
+    for (uint32_t i = lane; i < nwords; i += 64) filt[i] = fw[i];
+    if (lane == 0) pre[0] = (uint8_t)h.prefix;
     const uint64_t lq = h.responder - c.peer_begin;
-    const uint32_t n = min(wave_list_ids(bits + lq * c.words, c.words, lists[wv], kSimListCap), kSimListCap);
+    const uint32_t n = min(wave_list_ids(bits + lq * c.words, c.words, list, kSimListCap), kSimListCap);
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
     uint32_t sent = 0;
@@ -353,18 +370,20 @@ __global__ void __launch_bounds__(256) k_sim_respond(dsy_sim_config c, const uin
     uint64_t wblocks = 0, wslots = 0;
     for (uint32_t i0 = 0; i0 < n; i0 += 64) {
         const uint32_t i = i0 + lane;
-        const uint32_t id = i < n ? lists[wv][i] : 0u;
+        const uint32_t id = i < n ? list[i] : 0u;
         // range [1, time_high]: global_time = id + 1
         const bool sel = i < n && (uint64_t)id + 1 <= h.time_high;
         wave_work(sel ? n_blocks(1 + (uint32_t)(uoff[id + 1] - uoff[id]), H::block_bytes, H::len_bytes) : 0u, wblocks,
                   wslots);
         bool miss = false;
         int64_t len = 0;
+        // unselected lanes hash an empty key at the universe's start (DMA: every lane takes part)
+        KeyView kv{ublob + uoff[sel ? id : 0u], sel ? (uint32_t)(uoff[id + 1] - uoff[id]) : 0u, pre, 1};
+        H st;
+        if constexpr (kDma) hash_key_dma_reg<H, 1>(kv, st, dma_buf);
+        else if (sel) hash_key<H>(kv, st);
         if (sel) {
-            KeyView kv{ublob + uoff[id], (uint32_t)(uoff[id + 1] - uoff[id]), pre[wv], 1};
-            H st;
-            hash_key<H>(kv, st);
-            const uint32_t ok = filter_has_all<H, CHUNK>(filt[wv], st, c.k, c.m_bits);
+            const uint32_t ok = filter_has_all<H, CHUNK>(filt, st, c.k, c.m_bits);
             miss = !ok;
             len = miss ? (int64_t)kv.len : 0;
         }
@@ -381,7 +400,7 @@ __global__ void __launch_bounds__(256) k_sim_respond(dsy_sim_config c, const uin
         const bool inc = miss && ((sent + rank == 0) || (spent + incl - len < c.byte_limit));
         const uint64_t imask = __ballot(inc);
         const uint32_t nin = __popcll(imask);
-        if (inc && sent + rank < kSimRespMax) outl[wv][sent + rank] = (uint16_t)id;
+        if (inc && sent + rank < kSimRespMax) outl[sent + rank] = (uint16_t)id;
         if (nin) spent += __shfl(incl, 63 - __builtin_clzll(imask), 64);
         sent += nin;
         if (sent > 0 && spent >= c.byte_limit) break;
@@ -399,7 +418,7 @@ __global__ void __launch_bounds__(256) k_sim_respond(dsy_sim_config c, const uin
         atomicAdd(&tested[blockIdx.x & (kSimTestedSlots - 1)], (unsigned long long)ntested);  // spread
     }
     uint16_t* ids = (uint16_t*)(o + sizeof(dsy_sim_resp_header));
-    if (lane < cnt) ids[lane] = outl[wv][lane];
+    if (lane < cnt) ids[lane] = outl[lane];
 }
 
 // ------------------------------------------------------------------------------------------- merge
@@ -442,7 +461,9 @@ static hipError_t sim_family(int op, const SimLaunch& L) {
                            L.uoff, L.bits, L.out, L.slots, L.work);
     } else {
         if (!L.n_in) return hipSuccess;
-        hipLaunchKernelGGL((k_sim_respond<H, CHUNK>), dim3((uint32_t)((L.n_in + 3) / 4)), dim3(256), 0, L.stream, L.cfg,
+        constexpr bool dma = H::kind == DSY_MD5 || H::kind == DSY_SHA1;
+        const size_t lds = 4 * (size_t)sim_respond_wave_lds((uint32_t)((L.cfg.m_bits + 31) / 32), dma);
+        hipLaunchKernelGGL((k_sim_respond<H, CHUNK>), dim3((uint32_t)((L.n_in + 3) / 4)), dim3(256), lds, L.stream, L.cfg,
                            L.ublob, L.uoff, L.bits, L.in, L.n_in, L.out, L.slots, L.tested, L.work);
     }
     return hipGetLastError();

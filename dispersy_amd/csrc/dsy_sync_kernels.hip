@@ -693,6 +693,8 @@ __global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_waves_per_
 // loads without the compression (gather ceiling) -- diagnostics only, their answers are meaningless
 // Registers: 128 VGPRs (4 waves per SIMD, as the 8 KiB-per-wave LDS allows 5).  Forcing 5 waves (96 VGPRs) spills
 // per task and measured 234 -> 338 us per headline launch.
+// Measured and dropped: half-line staging (two 4 KiB buffers, one block's words live, 95 VGPRs, 5 waves per SIMD)
+// ran the headline launch in the same 234 us (compute ceiling 175 us, gather ceiling 191 us vs 176 for full lines).
 template <class H, int CHUNK, bool DMA, int DIAG = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_pair_test(RespondLaunch L, const uint32_t* __restrict__ req_list,
                                                    uint32_t n_list) {
@@ -728,7 +730,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         }
         H st;
         if constexpr (DMA) {
-            hash_key_dma_lines<H, DIAG>(kv, st, my_lds, q.prefix_word, L.st.lines);  // prefixes > 4 bytes go to DMA = false
+            // prefixes > 4 bytes go to DMA = false
+            hash_key_dma_lines<H, DIAG>(kv, st, my_lds, q.prefix_word, L.st.lines);
         } else {
             hash_key<H>(kv, st);
         }

@@ -25,7 +25,7 @@ def main():
     for r in rows(d + "/**/*memory_copy_trace.csv"):
         ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "copy " + r.get("Direction", "?")))
     ev.sort()
-    starts = [i for i, e in enumerate(ev) if e[2].startswith("dsy::k_setup")]
+    starts = [i for i, e in enumerate(ev) if e[2].startswith("dsy::k_setup") or e[2].startswith("dsy::k_fill_first")]
     if len(starts) < first + nsteps + 1:
         first = max(0, len(starts) - nsteps - 1)
     for s in range(first, first + nsteps):
