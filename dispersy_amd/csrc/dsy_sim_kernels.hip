@@ -335,7 +335,20 @@ __global__ void k_sim_resp_counts(dsy_sim_config c, const uint8_t* __restrict__ 
 __host__ __device__ constexpr uint32_t sim_respond_wave_lds(uint32_t nwords, bool dma) {
     return (2 * kSimListCap + nwords * 4 + 16 + 2 * kSimRespMax + 15) / 16 * 16 + (dma ? 4096u : 0u);
 }
+// shared by the workgroup's four claims: one round's pooled candidates (id, owner, position) in block-count order,
+// their miss flags per owner, a 64-bin histogram, per-wave counts and the active flags
+static constexpr uint32_t kSimRespPoolLds = 256 * 2 + 256 + 256 + 4 * 64 + 64 * 4 + 4 * 4 + 16;
+__host__ __device__ constexpr uint32_t sim_respond_lds(uint32_t nwords, bool dma) {
+    return 4 * sim_respond_wave_lds(nwords, dma) + kSimRespPoolLds;
+}
 
+// One wave per incoming claim answers it: the responder's packets in global-time order, 64 candidates per round,
+// hash + probe, then the missing ones are sent until the byte budget is spent (the crossing packet is sent) and the
+// claim stops -- lazily, as the reference's generator chain does.  The workgroup's four claims hash together: each
+// round pools every active claim's next <= 64 candidates (<= 256), sorts them by block count, and the four waves hash
+// the pool in chunks of 64 equal-length lanes (the filter and prefix of each lane's own claim); then each claim's
+// wave applies the budget rule to its candidates in order.  Without the pool a chunk runs as long as its longest
+// random-length packet (lane utilisation 0.56).
 template <class H, int CHUNK>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H::kind == DSY_SHA256 ? 3 : 4, 8)))
 k_sim_respond(dsy_sim_config c, const uint8_t* __restrict__ ublob, const uint64_t* __restrict__ uoff,
@@ -347,65 +360,123 @@ k_sim_respond(dsy_sim_config c, const uint8_t* __restrict__ ublob, const uint64_
     constexpr bool kDma = H::kind == DSY_MD5 || H::kind == DSY_SHA1;
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t ci = (uint64_t)blockIdx.x * 4 + wv;
-    if (ci >= n_claims) return;  // wave-uniform, no workgroup barrier below
+    const bool live = ci < n_claims;  // wave-uniform; idle waves still meet the barriers
     const uint32_t nwords = (uint32_t)((c.m_bits + 31) / 32);
-    uint8_t* mine = sim_lds + wv * sim_respond_wave_lds(nwords, kDma);
-    uint8_t* dma_buf = mine;  // 4 KiB, first (16-byte aligned)
-    uint16_t* list = (uint16_t*)(mine + (kDma ? 4096 : 0));
-    uint32_t* filt = (uint32_t*)(list + kSimListCap);
+    const uint32_t wave_b = sim_respond_wave_lds(nwords, kDma);
+    auto list_of = [&](uint32_t w) { return (uint16_t*)(sim_lds + w * wave_b + (kDma ? 4096 : 0)); };
+    auto filt_of = [&](uint32_t w) { return (uint32_t*)(list_of(w) + kSimListCap); };
+    uint8_t* dma_buf = sim_lds + wv * wave_b;  // 4 KiB, first (16-byte aligned)
+    uint16_t* list = list_of(wv);
+    uint32_t* filt = filt_of(wv);
     uint8_t* pre = (uint8_t*)(filt + nwords);
     uint16_t* outl = (uint16_t*)(pre + 16);
-    const uint8_t* rec = claims + ci * c.claim_bytes;
-    const dsy_sim_claim_header h = *(const dsy_sim_claim_header*)rec;
-    const uint32_t* fw = (const uint32_t*)(rec + sizeof(dsy_sim_claim_header));
-    for (uint32_t i = lane; i < nwords; i += 64) filt[i] = fw[i];
-    if (lane == 0) pre[0] = (uint8_t)h.prefix;
-    const uint64_t lq = h.responder - c.peer_begin;
-    const uint32_t n = min(wave_list_ids(bits + lq * c.words, c.words, list, kSimListCap), kSimListCap);
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
+    uint8_t* pool = sim_lds + 4 * wave_b;
+    uint16_t* pool_id = (uint16_t*)pool;         // [256]
+    uint8_t* pool_own = pool + 512;              // [256] owner wave
+    uint8_t* pool_pos = pool + 768;              // [256] position in the owner's chunk
+    uint8_t* flags = pool + 1024;                // [4][64] miss flags of the round
+    uint32_t* phist = (uint32_t*)(pool + 1280);  // [64]
+    uint32_t* pcnt = phist + 64;                 // [4] candidates per wave this round
+    dsy_sim_claim_header h{};
+    uint32_t n_sel = 0;
+    if (live) {
+        const uint8_t* rec = claims + ci * c.claim_bytes;
+        h = *(const dsy_sim_claim_header*)rec;
+        const uint32_t* fw = (const uint32_t*)(rec + sizeof(dsy_sim_claim_header));
+        for (uint32_t i = lane; i < nwords; i += 64) filt[i] = fw[i];
+        if (lane == 0) pre[0] = (uint8_t)h.prefix;
+        const uint32_t n = min(wave_list_ids(bits + (h.responder - c.peer_begin) * c.words, c.words, list, kSimListCap),
+                               kSimListCap);
+        // range [1, time_high]: global_time = id + 1, ids ascending, so the candidates are a prefix of the list
+        for (uint32_t i0 = 0; i0 < n; i0 += 64)
+            n_sel += (uint32_t)__popcll(__ballot(i0 + lane < n && (uint64_t)list[i0 + lane] + 1 <= h.time_high));
+    }
     uint32_t sent = 0;
     int64_t spent = 0;
     uint32_t ntested = 0;
+    bool done = !live;
     uint64_t wblocks = 0, wslots = 0;
-    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
-        const uint32_t i = i0 + lane;
-        const uint32_t id = i < n ? list[i] : 0u;
-        // range [1, time_high]: global_time = id + 1
-        const bool sel = i < n && (uint64_t)id + 1 <= h.time_high;
-        wave_work(sel ? n_blocks(1 + (uint32_t)(uoff[id + 1] - uoff[id]), H::block_bytes, H::len_bytes) : 0u, wblocks,
-                  wslots);
-        bool miss = false;
-        int64_t len = 0;
-        // unselected lanes hash an empty key at the universe's start (DMA: every lane takes part)
-        KeyView kv{ublob + uoff[sel ? id : 0u], sel ? (uint32_t)(uoff[id + 1] - uoff[id]) : 0u, pre, 1};
-        H st;
-        if constexpr (kDma) hash_key_dma_reg<H, 1>(kv, st, dma_buf);
-        else if (sel) hash_key<H>(kv, st);
-        if (sel) {
-            const uint32_t ok = filter_has_all<H, CHUNK>(filt, st, c.k, c.m_bits);
-            miss = !ok;
-            len = miss ? (int64_t)kv.len : 0;
+    const uint32_t blk = H::block_bytes, lenb = H::len_bytes;
+    auto bin_of = [&](uint32_t id) { return 63u - min(n_blocks(1 + (uint32_t)(uoff[id + 1] - uoff[id]), blk, lenb), 63u); };
+    for (uint32_t k = 0;; ++k) {
+        const uint32_t base = 64 * k;
+        const uint32_t cnt = (!done && base < n_sel) ? min(64u, n_sel - base) : 0u;
+        if (lane == 0) pcnt[wv] = cnt;
+        if (threadIdx.x < 64) phist[threadIdx.x] = 0;
+        __syncthreads();
+        const uint32_t c0 = pcnt[0], c1 = pcnt[1], c2 = pcnt[2], c3 = pcnt[3];
+        const uint32_t pn = c0 + c1 + c2 + c3;
+        if (!pn) break;  // workgroup-uniform
+        const uint32_t at = wv == 0 ? 0 : wv == 1 ? c0 : wv == 2 ? c0 + c1 : c0 + c1 + c2;
+        // pool this wave's candidates, then rank them by block count over the workgroup
+        uint32_t my_id = 0, my_bin = 0;
+        if (lane < cnt) {
+            my_id = list[base + lane];
+            my_bin = bin_of(my_id);
+            atomicAdd(&phist[my_bin], 1u);
         }
-        ntested += __popcll(__ballot(sel));
-        int64_t incl = len;
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            const uint32_t hv = phist[threadIdx.x];
+            uint32_t incl = hv;
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int64_t o = __shfl_up(incl, d, 64);
-            if ((int)lane >= d) incl += o;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t o = __shfl_up(incl, d, 64);
+                if ((int)lane >= d) incl += o;
+            }
+            phist[threadIdx.x] = incl - hv;
         }
-        const uint64_t mmask = __ballot(miss);
-        const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-        const uint32_t rank = __popcll(mmask & lt);
-        const bool inc = miss && ((sent + rank == 0) || (spent + incl - len < c.byte_limit));
-        const uint64_t imask = __ballot(inc);
-        const uint32_t nin = __popcll(imask);
-        if (inc && sent + rank < kSimRespMax) outl[sent + rank] = (uint16_t)id;
-        if (nin) spent += __shfl(incl, 63 - __builtin_clzll(imask), 64);
-        sent += nin;
-        if (sent > 0 && spent >= c.byte_limit) break;
+        __syncthreads();
+        if (lane < cnt) {
+            const uint32_t slot = atomicAdd(&phist[my_bin], 1u);
+            pool_id[slot] = (uint16_t)my_id;
+            pool_own[slot] = (uint8_t)wv;
+            pool_pos[slot] = (uint8_t)lane;
+        }
+        (void)at;
+        __syncthreads();
+        if (wv * 64 < pn) {  // wave wv hashes pooled chunk wv (workgroup-uniform per wave)
+            const uint32_t i = wv * 64 + lane;
+            const bool act = i < pn;
+            const uint32_t id = act ? pool_id[i] : 0u;
+            const uint32_t own = act ? pool_own[i] : 0u;
+            const uint32_t len = act ? (uint32_t)(uoff[id + 1] - uoff[id]) : 0u;
+            wave_work(act ? n_blocks(1 + len, blk, lenb) : 0u, wblocks, wslots);
+            const uint32_t* own_filt = filt_of(own);
+            KeyView kv{ublob + uoff[id], len, (const uint8_t*)(own_filt + nwords), 1};
+            H st;
+            if constexpr (kDma) hash_key_dma_reg<H, 1>(kv, st, dma_buf);
+            else if (act) hash_key<H>(kv, st);
+            if (act) flags[own * 64 + pool_pos[i]] = (uint8_t)!filter_has_all<H, CHUNK>(own_filt, st, c.k, c.m_bits);
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __syncthreads();
+        if (cnt) {  // this claim's budget rule over its candidates, in order
+            const uint32_t id = lane < cnt ? list[base + lane] : 0u;
+            const bool miss = lane < cnt && flags[wv * 64 + lane];
+            const int64_t len = miss ? (int64_t)(uoff[id + 1] - uoff[id]) : 0;
+            ntested += cnt;
+            int64_t incl = len;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int64_t o = __shfl_up(incl, d, 64);
+                if ((int)lane >= d) incl += o;
+            }
+            const uint64_t mmask = __ballot(miss);
+            const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+            const uint32_t rank = __popcll(mmask & lt);
+            const bool inc = miss && ((sent + rank == 0) || (spent + incl - len < c.byte_limit));
+            const uint64_t imask = __ballot(inc);
+            const uint32_t nin = __popcll(imask);
+            if (inc && sent + rank < kSimRespMax) outl[sent + rank] = (uint16_t)id;
+            if (nin) spent += __shfl(incl, 63 - __builtin_clzll(imask), 64);
+            sent += nin;
+            if (sent > 0 && spent >= c.byte_limit) done = true;
+        }
+        __syncthreads();  // the pool and the flags are rewritten next round
     }
     work_flush(work, 2, wblocks, wslots);
+    if (!live) return;
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
     uint8_t* o = out + (uint64_t)slots[ci] * c.resp_bytes;
@@ -462,7 +533,7 @@ static hipError_t sim_family(int op, const SimLaunch& L) {
     } else {
         if (!L.n_in) return hipSuccess;
         constexpr bool dma = H::kind == DSY_MD5 || H::kind == DSY_SHA1;
-        const size_t lds = 4 * (size_t)sim_respond_wave_lds((uint32_t)((L.cfg.m_bits + 31) / 32), dma);
+        const size_t lds = sim_respond_lds((uint32_t)((L.cfg.m_bits + 31) / 32), dma);
         hipLaunchKernelGGL((k_sim_respond<H, CHUNK>), dim3((uint32_t)((L.n_in + 3) / 4)), dim3(256), lds, L.stream, L.cfg,
                            L.ublob, L.uoff, L.bits, L.in, L.n_in, L.out, L.slots, L.tested, L.work);
     }
