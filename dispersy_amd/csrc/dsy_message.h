@@ -233,35 +233,36 @@ struct DmaLanes {
 };
 
 // DmaLanes for line-aligned keys (hash_key_dma_lines): each piece is named by its 128-byte line index relative to a
-// wave-uniform base (u32: 512 GB of lines) and the live-stage counts of two keys share a register, so the per-key
-// list costs 12 VGPRs instead of 24 -- the responder kernel sits at its 128-VGPR cap.
+// wave-uniform base (u32: 512 GB of lines) and the lengths of two keys share a register, so the per-key list costs
+// 12 VGPRs instead of 24 -- the responder kernel sits at its 128-VGPR cap.
 struct DmaLinePieces {
     using G = DmaGeometry<2, 1>;
     uint32_t line[G::kInsts];      // key p_i's first line, in lines from the base
-    uint32_t live2[G::kInsts / 2]; // live stages (lines) of keys p_2j (low half) and p_2j+1 (high half)
+    uint32_t len2[G::kInsts / 2];  // packet lengths of keys p_2j (low half) and p_2j+1 (high half), <= 65535 bytes
     __device__ __forceinline__ void init(const uint8_t* base, const uint8_t* key, uint32_t len) {
         const uint32_t lane = threadIdx.x & 63;
         const uint32_t my_line = (uint32_t)((uint64_t)(key - base) >> 7);
-        const uint32_t my_live = (len + 127) >> 7;  // <= 512 for a 65535-byte packet
 #pragma unroll
         for (int i = 0; i < G::kInsts; ++i) {
             const int p = G::kKeysPerInst * i + (int)(lane / G::kChunks);
             line[i] = (uint32_t)__shfl((int)my_line, p, 64);
-            const uint32_t lv = (uint32_t)__shfl((int)my_live, p, 64);
-            if (i & 1) live2[i / 2] |= lv << 16;
-            else live2[i / 2] = lv;
+            const uint32_t lv = (uint32_t)__shfl((int)len, p, 64);
+            if (i & 1) len2[i / 2] |= lv << 16;
+            else len2[i / 2] = lv;
         }
     }
+    // a 16-byte piece is loaded only when it holds packet bytes: the last line of a packet moves only the chunks
+    // its bytes reach (the rest of that line is padding)
     template <bool SKIP = false>
     __device__ __forceinline__ void issue(uint32_t s, const uint8_t* base, uint8_t* lds_wave) const {
         if constexpr (SKIP) return;
         const uint32_t lane = threadIdx.x & 63;
 #pragma unroll
         for (int i = 0; i < G::kInsts; ++i) {
-            const uint32_t lv = (i & 1) ? live2[i / 2] >> 16 : live2[i / 2] & 0xffffu;
+            const uint32_t lv = (i & 1) ? len2[i / 2] >> 16 : len2[i / 2] & 0xffffu;
             const int p = G::kKeysPerInst * i + (int)(lane / G::kChunks);
             const uint32_t c = ((lane % G::kChunks) + ((uint32_t)p >> G::kShift)) % G::kChunks;
-            if (s < lv)
+            if (s * 128 + 16 * c < lv)
                 __builtin_amdgcn_global_load_lds((const void*)(base + ((uint64_t)(line[i] + s) << 7) + 16 * c),
                                                  (__attribute__((address_space(3))) void*)(lds_wave + i * 1024), 16, 0, 0);
         }

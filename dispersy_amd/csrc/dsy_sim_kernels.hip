@@ -150,27 +150,29 @@ __device__ __forceinline__ void work_flush(unsigned long long* work, int which, 
     }
 }
 
-// LDS of one requester wave in k_sim_build_claims: id list, the same ids sorted by block count, a 64-bin
-// histogram, the prefix byte and the filter (sized by m at launch)
+// LDS of one requester wave in k_sim_build_claims: its id list (4 KiB, reused as the LDS-DMA stage once the ids are
+// pooled), the prefix byte and the filter (sized by m at launch)
 __host__ __device__ constexpr uint32_t sim_build_wave_lds(uint32_t nwords) {
-    return (4 * kSimListCap + 256 + 16 + nwords * 4 + 15) / 16 * 16;
+    return (2 * kSimListCap + 16 + nwords * 4 + 15) / 16 * 16;
 }
-// LDS shared by the workgroup's four requesters: the pooled tails (key id, owner wave) in block-count order, a
-// 64-bin histogram and the pool's size
-static constexpr uint32_t kSimPoolLds = 256 * 2 + 256 + 64 * 4 + 16;
-__host__ __device__ constexpr uint32_t sim_build_lds(uint32_t nwords) { return 4 * sim_build_wave_lds(nwords) + kSimPoolLds; }
+// shared by the workgroup's four requesters: their claimed ids pooled in block-count order (id | owner << 16, at most
+// 4 x capacity), a 64-bin histogram and the per-wave counts
+__host__ __device__ constexpr uint32_t sim_build_lds(uint32_t nwords, uint32_t capacity) {
+    return 4 * sim_build_wave_lds(nwords) + 4 * 4 * capacity + 64 * 4 + 16;
+}
 
-// one wave per local requester: list its packets, put the claimed ones in block-count order (a counting sort in
-// LDS: the filter is an OR, so the hashing order is free, and equal-length lanes finish together), hash them into
-// an LDS-resident filter (filter_set_all, OR_MODE as there), write the claim record.  A wave hashes only its full
-// 64-key chunks; the tails (< 64 keys each, the requester's shortest) of the workgroup's four requesters are pooled,
-// sorted by block count, and hashed together in ceil(pool / 64) chunks, each key into its owner's filter -- ~150-key
-// stores otherwise leave a third of the lanes of every third chunk idle.
+// One workgroup per four local requesters, each the reference's claim: _dispersy_claim_sync_bloom_filter_largest's
+// "fewer than capacity packets" branch (community.py:808-821) over its packets in global-time order.  Every wave
+// lists its requester's packets; the workgroup pools the four claims' keys (the filter is an OR, so the hashing
+// order is free), sorts them by compression-block count, and the waves hash the pool in chunks of 64 near-equal
+// lanes, round-robin, each key into its owner's LDS filter (filter_set_all, OR_MODE as there; a lane's filter is a
+// word offset from one LDS base).  Sorting ~4 x 150 keys instead of each requester's ~150 keeps a chunk's lanes
+// within a few blocks of each other.  Then every wave writes its claim record.
 template <class H, int CHUNK, int OR_MODE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H::kind == DSY_SHA256 ? 3 : 4, 8))) k_sim_build_claims(dsy_sim_config c, uint32_t round, const uint8_t* __restrict__ ublob,
-                                                          const uint64_t* __restrict__ uoff, const uint32_t* __restrict__ bits,
-                                                          uint8_t* __restrict__ out, const uint32_t* __restrict__ slots,
-                                                          unsigned long long* __restrict__ work) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H::kind == DSY_SHA256 ? 3 : 4, 8)))
+k_sim_build_claims(dsy_sim_config c, uint32_t round, const uint8_t* __restrict__ ublob, const uint64_t* __restrict__ uoff,
+                   const uint32_t* __restrict__ bits, uint8_t* __restrict__ out, const uint32_t* __restrict__ slots,
+                   unsigned long long* __restrict__ work) {
     extern __shared__ __attribute__((aligned(16))) uint8_t sim_lds[];
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t lp = (uint64_t)blockIdx.x * 4 + wv;
@@ -178,23 +180,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H::kin
     const uint32_t nwords = (uint32_t)((c.m_bits + 31) / 32);
     const uint32_t wave_b = sim_build_wave_lds(nwords);
     uint8_t* mine = sim_lds + wv * wave_b;
-    uint16_t* list = (uint16_t*)mine;
-    uint16_t* sorted = list + kSimListCap;
-    uint32_t* hist = (uint32_t*)(sorted + kSimListCap);
-    uint8_t* pre = (uint8_t*)(hist + 64);
+    uint16_t* list = (uint16_t*)mine;  // later: this wave's LDS-DMA stage (4 KiB)
+    uint8_t* pre = mine + 2 * kSimListCap;
     uint32_t* filt = (uint32_t*)(pre + 16);
-    uint8_t* pool_base = sim_lds + 4 * wave_b;
-    uint16_t* pool_id = (uint16_t*)pool_base;            // [256] pooled tails, then (sorted) their hashing order
-    uint8_t* pool_own = pool_base + 512;                 // [256]
-    uint32_t* pool_hist = (uint32_t*)(pool_base + 768);  // [64]
-    uint32_t* pool_n = pool_hist + 64;
+    uint32_t* pool = (uint32_t*)(sim_lds + 4 * wave_b);  // [4 * capacity]
+    uint32_t* phist = pool + 4 * c.capacity;            // [64]
+    uint32_t* pcnt = phist + 64;                        // [4]
     const uint64_t p = c.peer_begin + lp;
     const uint32_t blk = H::block_bytes, lenb = H::len_bytes;
     auto bin_of = [&](uint32_t id) { return 63u - min(n_blocks(1 + (uint32_t)(uoff[id + 1] - uoff[id]), blk, lenb), 63u); };
     for (uint32_t i = lane; i < nwords; i += 64) filt[i] = 0;
-    hist[lane] = 0;
-    if (threadIdx.x < 64) pool_hist[threadIdx.x] = 0;
-    if (threadIdx.x == 0) *pool_n = 0;
+    if (threadIdx.x < 64) phist[threadIdx.x] = 0;
     uint32_t n = live ? wave_list_ids(bits + lp * c.words, c.words, list, kSimListCap) : 0u;
     // _select_and_fix(..., 0, capacity, True): the first capacity packets; over-full drops the (capacity+1)-th
     // global time (global times are distinct here) and the range ends at the last kept one
@@ -204,99 +200,52 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H::kin
         time_high = (uint64_t)list[n - 1] + 1;
     }
     const uint32_t prefix = live ? sim_prefix(c, round, p) : 0u;
-    if (lane == 0) pre[0] = (uint8_t)prefix;
-    __builtin_amdgcn_wave_barrier();
-    for (uint32_t i = lane; i < n; i += 64) atomicAdd(&hist[bin_of(list[i])], 1u);
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-    {
-        const uint32_t h = hist[lane];
-        uint32_t incl = h;
+    if (lane == 0) {
+        pre[0] = (uint8_t)prefix;
+        pcnt[wv] = n;
+    }
+    __syncthreads();
+    const uint32_t c0 = pcnt[0], c1 = pcnt[1], c2 = pcnt[2];
+    const uint32_t pn = c0 + c1 + c2 + pcnt[3];
+    for (uint32_t i = lane; i < n; i += 64) atomicAdd(&phist[bin_of(list[i])], 1u);
+    __syncthreads();
+    if (threadIdx.x < 64) {  // exclusive scan of the bins (longest first)
+        const uint32_t hv = phist[threadIdx.x];
+        uint32_t incl = hv;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
             const uint32_t o = __shfl_up(incl, d, 64);
             if ((int)lane >= d) incl += o;
         }
-        hist[lane] = incl - h;
+        phist[threadIdx.x] = incl - hv;
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
+    __syncthreads();
     for (uint32_t i = lane; i < n; i += 64) {
         const uint32_t id = list[i];
-        sorted[atomicAdd(&hist[bin_of(id)], 1u)] = (uint16_t)id;
+        pool[atomicAdd(&phist[bin_of(id)], 1u)] = id | (wv << 16);
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-    uint64_t wblocks = 0, wslots = 0;
-    const uint32_t n_full = n & ~63u;  // sorted longest first: the tail is the requester's shortest keys
-    // MD5 / SHA-1 stage the packets through LDS with DMA (hash_key_dma_reg, one 64-byte block per key per stage:
-    // 4 KiB, the wave's id list, dead once sorted): 8 keys x 64 contiguous bytes per wave instruction instead of 64
-    // scattered 16-byte loads.  The universe blob keeps DSY_BLOB_GUARD readable bytes on both sides (sim.py).
+    __syncthreads();  // every list has been read: the waves' LDS-DMA stages may overwrite them
+    // MD5 / SHA-1 stage the packets through LDS with DMA (hash_key_dma_reg, one 64-byte block per key per stage):
+    // 8 keys x 64 contiguous bytes per wave instruction instead of 64 scattered 16-byte loads.  The universe blob keeps
+    // DSY_BLOB_GUARD readable bytes on both sides (sim.py); idle lanes hash an empty key at its start.
     constexpr bool kDma = H::kind == DSY_MD5 || H::kind == DSY_SHA1;
-    uint8_t* dma_buf = (uint8_t*)list;
     static_assert(DmaGeometry<1, 1>::kWaveBytes == 2 * kSimListCap, "the DMA stage reuses the id list");
-    for (uint32_t i0 = 0; i0 < n_full; i0 += 64) {
-        const uint32_t id = sorted[i0 + lane];
-        const uint32_t len = (uint32_t)(uoff[id + 1] - uoff[id]);
-        wave_work(n_blocks(1 + len, blk, lenb), wblocks, wslots);
-        KeyView kv{ublob + uoff[id], len, pre, 1};
-        H st;
-        if constexpr (kDma) hash_key_dma_reg<H, 1>(kv, st, dma_buf);
-        else hash_key<H>(kv, st);
-        filter_set_all<H, CHUNK, OR_MODE>(filt, st, c.k, c.m_bits, true);
-    }
-    // pool the tail: rank by block count over the workgroup's tails (counting sort over 64 bins)
-    const uint32_t tail = n - n_full;
-    uint32_t my_at = 0;
-    if (lane == 0 && tail) my_at = atomicAdd(pool_n, tail);
-    my_at = (uint32_t)__shfl((int)my_at, 0, 64);
-    if (lane < tail) {
-        pool_id[my_at + lane] = sorted[n_full + lane];
-        pool_own[my_at + lane] = (uint8_t)wv;
-    }
-    __syncthreads();
-    const uint32_t pn = *pool_n;
-    uint32_t pid = 0, pown = 0, pbin = 0;
-    if (threadIdx.x < pn) {
-        pid = pool_id[threadIdx.x];
-        pown = pool_own[threadIdx.x];
-        pbin = bin_of(pid);
-        atomicAdd(&pool_hist[pbin], 1u);
-    }
-    __syncthreads();
-    if (threadIdx.x < 64) {
-        const uint32_t h = pool_hist[threadIdx.x];
-        uint32_t incl = h;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t o = __shfl_up(incl, d, 64);
-            if ((int)lane >= d) incl += o;
-        }
-        pool_hist[threadIdx.x] = incl - h;
-    }
-    __syncthreads();
-    if (threadIdx.x < pn) {
-        const uint32_t at = atomicAdd(&pool_hist[pbin], 1u);
-        pool_id[at] = (uint16_t)pid;      // every thread has read its entry (barrier above): safe to overwrite
-        pool_own[at] = (uint8_t)pown;
-    }
-    __syncthreads();
-    if (wv * 64 < pn) {  // wave wv hashes pooled chunk wv
-        const uint32_t i = wv * 64 + lane;
+    uint8_t* dma_buf = (uint8_t*)list;
+    uint64_t wblocks = 0, wslots = 0;
+    for (uint32_t j = wv; 64 * j < pn; j += 4) {
+        const uint32_t i = 64 * j + lane;
         const bool act = i < pn;
-        const uint32_t id = act ? pool_id[i] : 0u;
-        const uint32_t own = act ? pool_own[i] : 0u;
-        uint8_t* own_lds = sim_lds + own * wave_b;
+        const uint32_t e = act ? pool[i] : 0u;
+        const uint32_t id = e & 0xffffu, own = e >> 16;
         const uint32_t len = act ? (uint32_t)(uoff[id + 1] - uoff[id]) : 0u;
         wave_work(act ? n_blocks(1 + len, blk, lenb) : 0u, wblocks, wslots);
+        uint8_t* own_lds = sim_lds + own * wave_b;
+        KeyView kv{ublob + uoff[id], len, own_lds + 2 * kSimListCap, 1};
         H st;
-        // idle lanes: an empty key at the universe's start (its prefix byte is read from the owner's LDS slot 0)
-        KeyView kv{ublob + (act ? uoff[id] : uoff[0]) , len, own_lds + 4 * kSimListCap + 256, 1};
         if constexpr (kDma) hash_key_dma_reg<H, 1>(kv, st, dma_buf);
         else if (act) hash_key<H>(kv, st);
-        // one LDS base for the wave, each lane's filter as a word offset from it (OR_MODE 2 merges by word index)
         filter_set_all<H, CHUNK, OR_MODE>((uint32_t*)sim_lds, st, c.k, c.m_bits, act,
-                                          (own * wave_b + 4 * kSimListCap + 256 + 16) / 4);
+                                          (own * wave_b + 2 * kSimListCap + 16) / 4);
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __syncthreads();
@@ -525,7 +474,7 @@ static hipError_t sim_family(int op, const SimLaunch& L) {
     const uint64_t local = L.cfg.peer_end - L.cfg.peer_begin;
     if (op == 0) {
         if (!local) return hipSuccess;
-        const size_t lds = sim_build_lds((uint32_t)((L.cfg.m_bits + 31) / 32));
+        const size_t lds = sim_build_lds((uint32_t)((L.cfg.m_bits + 31) / 32), L.cfg.capacity);
         auto kern = L.or_mode == 0 ? k_sim_build_claims<H, CHUNK, 0>
                                    : L.or_mode == 2 ? k_sim_build_claims<H, CHUNK, 2> : k_sim_build_claims<H, CHUNK, 1>;
         hipLaunchKernelGGL(kern, dim3((uint32_t)((local + 3) / 4)), dim3(256), lds, L.stream, L.cfg, L.round, L.ublob,
