@@ -100,3 +100,47 @@ def test_respond_vs_oracle(skew, window):
 
 
 _ORACLE = {}
+
+
+@pytest.mark.parametrize("window", [0, 256])
+@pytest.mark.parametrize("meta_name", ["a", "d", "p"])
+@pytest.mark.parametrize("skew", [False, "dense"])
+def test_one_meta_mixed_families_vs_oracle(skew, meta_name, window):
+    """One served meta with device-side capacities: the first window's setup runs inside the fill (k_fill_first),
+    here with MD5, SHA-1 and 'L'-chunk claims in one call (the first active list is then family-ordered, not the
+    identity), prefixes of 0-5 bytes, and capped windows so later windows resume from k_fill_first's cursor."""
+    seed = 7 if skew is False else 8
+    rows, conn = build(seed, 40_000, 150_000 if skew is False else 5_000, skew)
+    store = SyncStore.from_rows(rows)
+    gt_now = 150_100 if skew is False else 30_100
+    chosen = [m for m in METAS if m[0] == meta_name]
+    served = [MetaMessage(n, i, SyncDistribution(d, p, GlobalTimePruning(*pr) if pr else None)) for n, i, d, p, pr in chosen]
+    served_oracle = [dict(name=n, id=i, direction=d, priority=p, pruning=pr) for n, i, d, p, pr in chosen]
+    com = SyncCommunity(store, served, global_time=gt_now)
+    rng = np.random.Generator(np.random.PCG64(31 + seed))
+    packets = {r[0]: r[4] for r in rows}
+    shapes = [(4096, 0.001), (10160, 0.01), (1 << 15, 0.01)]
+    reqs, oracle_blooms = [], []
+    for q in range(64):
+        modulo = int(rng.choice([1, 1, 7, 331]))
+        offset = int(rng.integers(0, modulo))
+        lo = int(rng.integers(1, gt_now // 2))
+        hi = int(rng.integers(lo, gt_now + 10))
+        m, f = shapes[q % len(shapes)]
+        prefix = bytes(rng.integers(0, 256, size=int(q % 6), dtype=np.uint8))
+        bf, ob = BloomFilter(m, f, prefix), OracleBloom.from_m_f(m, f, prefix)
+        known = [packets[r[0]] for r in rows if rng.random() < 0.9]
+        bf.add_keys(known)
+        ob.add_keys(known)
+        reqs.append(ClaimRequest(lo, hi, modulo, offset, bf))
+        oracle_blooms.append(ob)
+    store.ctx.set_window(window)
+    try:
+        results = [(limit, com.respond(reqs, byte_limit=limit)) for limit in (5120, 1)]
+    finally:
+        store.ctx.set_window(0)
+    for limit, got in results:
+        for q, ob, g in zip(reqs, oracle_blooms, got):
+            want = sync_ref.respond_lists(conn, served_oracle, (q.time_low, q.time_high, q.offset, q.modulo), ob,
+                                          gt_now, limit, False)
+            assert store.rowid[g].tolist() == want, (meta_name, q.time_low, q.time_high, q.modulo, q.offset, limit)
