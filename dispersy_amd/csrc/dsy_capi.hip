@@ -59,6 +59,7 @@ struct dsy_ctx {
     hipStream_t stream = nullptr;
     std::mutex mu;
     std::map<std::string, DevBuf> ws;
+    std::unordered_map<const char*, DevBuf*> ws_by_name;  // ws_get's cache, keyed by the literal's address
     uint32_t max_grid = 2048;
     int bloom_diag = 0;  // DSY_BLOOM_DIAG at creation: single-filter ceiling diagnostics (k_bloom DIAG)
     int pair_diag = 0;   // DSY_PAIR_DIAG at creation: responder ceiling diagnostics (k_pair_test DIAG)
@@ -107,7 +108,10 @@ namespace {
 
 // grow-only named workspace buffer
 int ws_get(dsy_ctx* c, const char* name, size_t bytes, void** out, bool* fresh = nullptr) {
-    DevBuf& b = c->ws[name];
+    // names are string literals: their address finds the buffer without building a std::string per call
+    DevBuf*& slot = c->ws_by_name[name];
+    if (!slot) slot = &c->ws[name];  // std::map nodes do not move
+    DevBuf& b = *slot;
     if (fresh) *fresh = b.bytes < bytes;
     if (b.bytes < bytes) {
         if (b.ptr) hipFree(b.ptr);
@@ -1466,20 +1470,31 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     // family id = (kind * 3 + chunk class) * 2 + long prefix (> 4 bytes: the byte-wise hashing path)
     constexpr int kFamilies = 5 * 3 * 2;
     std::vector<uint32_t> fam_members[kFamilies];
+    uint64_t memo_m = 0;  // check_family of the previous claim's (m, k): a batch's claims share one filter shape
+    uint32_t memo_k = 0, memo_chunk = 0;
+    int32_t memo_kind = -1;
     for (uint32_t r = 0; r < R; ++r) {
         const dsy_request& q = reqs[r];
         if (q.modulo == 0 || q.offset >= q.modulo)
             return fail(DSY_EINVAL, "claim %u: need 0 <= offset < modulo (offset=%u modulo=%u)", r, q.offset, q.modulo);
         int32_t kind;
         uint32_t chunk;
-        int rc = check_family(q.m_bits, q.k, &kind, &chunk);
-        if (rc) return rc;
+        if (memo_kind >= 0 && q.m_bits == memo_m && q.k == memo_k) {
+            kind = memo_kind;
+            chunk = memo_chunk;
+        } else {
+            int rc = check_family(q.m_bits, q.k, &kind, &chunk);
+            if (rc) return rc;
+            memo_m = q.m_bits, memo_k = q.k, memo_kind = kind, memo_chunk = chunk;
+        }
         if (kind != q.hash_kind || chunk != q.chunk_bytes) return fail(DSY_EINVAL, "claim %u: hash family mismatch", r);
         if (q.prefix_len > 255) return fail(DSY_EINVAL, "claim %u: prefix too long", r);
         if (q.filter_offset % 4) return fail(DSY_EINVAL, "claim %u: filter_offset must be a multiple of 4", r);
         if (filters_len && q.filter_offset + filter_words(q.m_bits) * 4 > filters_len)
             return fail(DSY_EINVAL, "claim %u: filter beyond the filters buffer", r);
-        fam_members[(kind * 3 + (chunk == 2 ? 0 : chunk == 4 ? 1 : 2)) * 2 + (q.prefix_len > 4)].push_back(r);
+        std::vector<uint32_t>& fm = fam_members[(kind * 3 + (chunk == 2 ? 0 : chunk == 4 ? 1 : 2)) * 2 + (q.prefix_len > 4)];
+        if (fm.empty()) fm.reserve(R);
+        fm.push_back(r);
     }
     const uint64_t pool = kWindow * std::max<uint64_t>(R, kMinSlots);
     // ---- device layout: one upload region [claims | metas | window slots 0..R-1 | first active list] and one
