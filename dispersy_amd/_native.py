@@ -116,20 +116,21 @@ _lib_lock = threading.Lock()
 
 
 def load_library():
-    """Load libdsybloom.so.  torch is imported first (when present) so the library binds to the same HIP runtime
+    """Load libdsybloom.so (DSY_LIB_PATH: another build of it, for same-box A/B runs of a kernel change).  torch is imported first (when present) so the library binds to the same HIP runtime
     (libamdhip64.so.7) torch uses and device pointers are shared between them."""
     global _lib
     with _lib_lock:
         if _lib is not None:
             return _lib
-        if not os.path.isfile(LIB_PATH):
+        path = os.environ.get("DSY_LIB_PATH") or LIB_PATH
+        if not os.path.isfile(path):
             raise NativeUnavailable("%s is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
-                                    % LIB_PATH)
+                                    % path)
         try:
             import torch  # noqa: F401  (shares one HIP runtime with the library)
         except ImportError:
             pass
-        lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)
             fn.restype = res

@@ -606,16 +606,17 @@ static int store_finish(dsy_ctx* c, dsy_store* s, const uint64_t* h_gt_or_null, 
     return DSY_OK;
 }
 
-// The responder's line copy: row i's packet at rec[i].off, a multiple of 128, so every LDS-DMA piece of the
-// hashing kernel is one whole line (dsy_message.h hash_key_dma_lines).  Costs < 128 bytes per row.
+// The responder's line copy: row i's packet at rec[i].off, kLineBias bytes past a multiple of 128, so every LDS-DMA
+// piece of the hashing kernel is one whole line and a 1-byte-prefixed message is line-aligned (dsy_message.h
+// hash_key_dma_lines).  Costs <= 128 bytes per row.
 static int store_build_lines(dsy_ctx* c, dsy_store* s, const uint64_t* h_off) {
     const uint64_t n = s->n;
     std::vector<RowRec> rec(std::max<uint64_t>(n, 1));
     uint64_t at = DSY_BLOB_GUARD;
     for (uint64_t i = 0; i < n; ++i) {
         const uint64_t len = h_off[i + 1] - h_off[i];
-        rec[i] = RowRec{at, (uint32_t)len, 0u};
-        at += (len + 127) & ~127ull;
+        rec[i] = RowRec{at + kLineBias, (uint32_t)len, 0u};
+        at += (len + kLineBias + 127) & ~127ull;
     }
     const uint64_t bytes = at + DSY_BLOB_GUARD;
     void *pl, *pr;
@@ -855,8 +856,8 @@ int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blo
     uint64_t at = s->lines_used;
     for (uint64_t j = 0; j < a; ++j) {
         const uint64_t len = offsets[j + 1] - offsets[j];
-        nrec[j] = RowRec{at, (uint32_t)len, 0u};
-        at += (len + 127) & ~127ull;
+        nrec[j] = RowRec{at + kLineBias, (uint32_t)len, 0u};
+        at += (len + kLineBias + 127) & ~127ull;
     }
     if ((rc = lines_reserve(c, s, at))) return rc;
     if (n0 + a > s->rec_cap) {
@@ -1163,8 +1164,8 @@ int dsy_store_replace(dsy_ctx* c, dsy_store* s, const uint64_t* rows, const uint
     uint64_t at = s->lines_used, minlen = s->min_len;
     for (uint64_t i = 0; i < k; ++i) {
         const uint64_t len = offsets[i + 1] - offsets[i];
-        nrec[i] = RowRec{at, (uint32_t)len, 0u};
-        at += (len + 127) & ~127ull;
+        nrec[i] = RowRec{at + kLineBias, (uint32_t)len, 0u};
+        at += (len + kLineBias + 127) & ~127ull;
         minlen = std::min(minlen, len);
     }
     for (uint64_t i = 0; i <= k; ++i) noff[i] = offsets[i] - base0;
@@ -1492,7 +1493,9 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
         if (q.filter_offset % 4) return fail(DSY_EINVAL, "claim %u: filter_offset must be a multiple of 4", r);
         if (filters_len && q.filter_offset + filter_words(q.m_bits) * 4 > filters_len)
             return fail(DSY_EINVAL, "claim %u: filter beyond the filters buffer", r);
-        std::vector<uint32_t>& fm = fam_members[(kind * 3 + (chunk == 2 ? 0 : chunk == 4 ? 1 : 2)) * 2 + (q.prefix_len > 4)];
+        // prefixes of 1-4 bytes take the line-staged hashing; longer ones and the empty prefix the byte-wise path
+        std::vector<uint32_t>& fm =
+            fam_members[(kind * 3 + (chunk == 2 ? 0 : chunk == 4 ? 1 : 2)) * 2 + (q.prefix_len > 4 || q.prefix_len == 0)];
         if (fm.empty()) fm.reserve(R);
         fm.push_back(r);
     }

@@ -28,7 +28,8 @@ struct __attribute__((aligned(16))) PairTask {
     uint32_t slot;
 };
 
-// A store row's packet in the line copy: starts on a 128-byte line of StoreView::lines.
+// A store row's packet in the line copy: starts kLineBias (dsy_message.h) bytes into a 128-byte line of
+// StoreView::lines.
 struct RowRec {
     uint64_t off;
     uint32_t len;

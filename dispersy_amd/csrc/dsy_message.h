@@ -232,21 +232,28 @@ struct DmaLanes {
     }
 };
 
+// The store's line copy puts every packet kLineBias bytes into a 128-byte line.  With one byte of slack in front of
+// every packet, the message prefix || packet of a 1-byte prefix (every claim the reference builds, community.py:773,
+// :911) starts exactly on the line, and the responder's blocks need no byte shift.
+static constexpr uint64_t kLineBias = 1;
+
 // DmaLanes for line-aligned keys (hash_key_dma_lines): each piece is named by its 128-byte line index relative to a
 // wave-uniform base (u32: 512 GB of lines) and the lengths of two keys share a register, so the per-key list costs
 // 12 VGPRs instead of 24 -- the responder kernel sits at its 128-VGPR cap.
 struct DmaLinePieces {
     using G = DmaGeometry<2, 1>;
     uint32_t line[G::kInsts];      // key p_i's first line, in lines from the base
-    uint32_t len2[G::kInsts / 2];  // packet lengths of keys p_2j (low half) and p_2j+1 (high half), <= 65535 bytes
+    uint32_t len2[G::kInsts / 2];  // end of keys p_2j (low half) / p_2j+1 (high half) in their first line, < 65536
+    // key = base + line * 128 + kLineBias; a piece is live when it holds a byte of [line start, key + len)
     __device__ __forceinline__ void init(const uint8_t* base, const uint8_t* key, uint32_t len) {
         const uint32_t lane = threadIdx.x & 63;
         const uint32_t my_line = (uint32_t)((uint64_t)(key - base) >> 7);
+        const uint32_t my_end = len + (uint32_t)kLineBias;
 #pragma unroll
         for (int i = 0; i < G::kInsts; ++i) {
             const int p = G::kKeysPerInst * i + (int)(lane / G::kChunks);
             line[i] = (uint32_t)__shfl((int)my_line, p, 64);
-            const uint32_t lv = (uint32_t)__shfl((int)len, p, 64);
+            const uint32_t lv = (uint32_t)__shfl((int)my_end, p, 64);
             if (i & 1) len2[i / 2] |= lv << 16;
             else len2[i / 2] = lv;
         }
@@ -443,21 +450,25 @@ __device__ __forceinline__ void hash_key_dma_reg(const KeyView& kv, H& st, uint8
     }
 }
 
-// Line-aligned packets (the store's line copy, dsy_capi.hip store_build_lines): every packet starts on a 128-byte
-// line, so stage s of a key is exactly the line [A + 128 s, A + 128 s + 128) -- every DMA piece is one whole line,
-// no line is fetched twice (tools/hashbench: 70 vs 57 Gblk/s MD5 over the same packets, 4.3 vs 3.5 TB/s).  The
-// message (prefix || packet) is the packet shifted by the prefix length r, which is wave-uniform (one claim per
-// wave): a uniform alignbyte funnel with a one-dword carry from the previous stage.  Single 8 KiB buffer per wave,
-// like hash_key_dma_reg<H, 2>.  Requires r <= 4 and kv.key 128-byte aligned, at most 2^32 lines past `lines` (the
-// copy's base, wave-uniform); lines past the packet hold only
-// padding and are not loaded.  preword: the r prefix bytes, little-endian (wave-uniform: read once per claim).  MODE as in hash_key_dma_reg (k_pair_test DIAG diagnostics only).
+// Line-staged packets (the store's line copy, dsy_capi.hip store_build_lines): every packet starts kLineBias = 1 byte
+// into a 128-byte line, so stage s of a key is exactly line s of it -- every DMA piece is one whole line, no line is
+// fetched twice (tools/hashbench: 70 vs 57 Gblk/s MD5 over the same packets, 4.3 vs 3.5 TB/s) -- and the message
+// prefix || packet of a 1-byte prefix starts on the line: its blocks are the line's words as loaded, with the slack
+// byte in front of the packet replaced by the prefix byte.  A prefix of r bytes shifts the message by r - 1 bytes
+// (wave-uniform: one claim per wave): a uniform alignbyte funnel with a one-dword carry from the previous stage.
+// Single 8 KiB buffer per wave, like hash_key_dma_reg<H, 2>.  Requires 1 <= r <= 4 (the responder routes other
+// prefixes to the byte-wise path), kv.key = lines + 128 * line + kLineBias, at most 2^32 lines past `lines` (the
+// copy's base, wave-uniform); line bytes past the packet are not loaded (their words are masked by finish_block).
+// preword: the r prefix bytes, little-endian (wave-uniform: read once per claim).  MODE as in hash_key_dma_reg
+// (k_pair_test DIAG diagnostics only).
 template <class H, int MODE = 0>
 __device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uint8_t* lds_wave, uint32_t preword,
                                                    const uint8_t* lines) {
     static_assert(H::block_bytes == 64, "LDS-DMA staging is for 64-byte blocks");
+    static_assert(kLineBias == 1, "the shift below assumes one byte of slack before every packet");
     using G = DmaGeometry<2, 1>;
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t r = kv.plen;  // wave-uniform, <= 4
+    const uint32_t r = kv.plen;  // wave-uniform, 1..4
     const uint32_t len = kv.len;
     const uint32_t total = r + len;
     const uint32_t nb = n_blocks(total, 64, H::len_bytes);
@@ -467,11 +478,15 @@ __device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uin
     const uint32_t nst = (nbmax + 1) / 2;
     const uint32_t tmin = wave_min_u32(total);
     DmaLinePieces dl;
-    dl.init(lines, kv.key, len);  // 128-byte aligned: stage s is line s of the packet
+    dl.init(lines, kv.key, len);  // stage s is line s of the packet
     st.init();
-    // carry: the dword before the stage's first one; its top r bytes are the message bytes before the stage
-    uint32_t carry = r ? preword << (8 * (4 - r)) : 0u;
-    const uint32_t sh = (4 - r) & 3;  // alignbyte shift for r in 1..3
+    // message byte j is line byte j - rr (rr = r - 1): the carry is the dword before the stage's first one, its top
+    // rr bytes the message bytes before the stage (at stage 0 the first rr prefix bytes); the slack byte, line byte 0
+    // of stage 0, becomes the last prefix byte
+    const uint32_t rr = r - 1;
+    uint32_t carry = rr ? (preword & low_bytes_mask(rr)) << (8 * (4 - rr)) : 0u;
+    const uint32_t slack = (preword >> (8 * rr)) & 0xffu;
+    const uint32_t sh = (4 - rr) & 3;  // alignbyte shift for rr in 1..3
     if (nst) dl.template issue<MODE == 1>(0, lines, lds_wave);
     for (uint32_t s = 0; s < nst; ++s) {
         __builtin_amdgcn_s_waitcnt(0x0f70);
@@ -485,6 +500,7 @@ __device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uin
                                             16 * (G::kChunks * (lane % G::kKeysPerInst) + slot));
             d[1 + 4 * q] = v.x; d[2 + 4 * q] = v.y; d[3 + 4 * q] = v.z; d[4 + 4 * q] = v.w;
         }
+        if (s == 0) d[1] = (d[1] & ~0xffu) | slack;
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
         if (s + 1 < nst) dl.template issue<MODE == 1>(s + 1, lines, lds_wave);
@@ -494,13 +510,10 @@ __device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uin
             const uint32_t b = 2 * s + bb;
             if (b < nb) {
                 uint32_t x[16];
-                // message word i of block b = packet bytes [64 bb + 4 i - r, +4): d[1 + 16 bb + i] shifted by r
-                if (r == 0) {
+                // message word i of block b = line bytes [64 bb + 4 i - rr, +4): d[1 + 16 bb + i] shifted by rr
+                if (rr == 0) {  // the 1-byte prefix of every reference claim: the line's words as loaded
 #pragma unroll
                     for (int i = 0; i < 16; ++i) x[i] = d[1 + 16 * bb + i];
-                } else if (r == 4) {
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) x[i] = d[16 * bb + i];
                 } else {
 #pragma unroll
                     for (int i = 0; i < 16; ++i) x[i] = __builtin_amdgcn_alignbyte(d[1 + 16 * bb + i], d[16 * bb + i], sh);

@@ -319,7 +319,7 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
     // the sort's registers (below); a window that is one dense run of <= kFillThreads * kSortReg rows fills them
     // during the selection itself (pair t = thread t % 256, register t / 256), so the sort reads nothing back
     constexpr int kSortReg = 8;
-    uint32_t reg_off[kSortReg];  // line index: a pair's packet starts on a 128-byte line of the line copy
+    uint32_t reg_off[kSortReg];  // line index: a pair's packet starts kLineBias bytes into a 128-byte line
     uint32_t reg_len[kSortReg];
     uint64_t regs_rows = 0;  // pairs t < regs_rows are in the registers already (their pair_off is not written)
     // each thread takes kCand consecutive candidates, so one round of independent lookups covers
@@ -373,7 +373,7 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
                         out_len[filled + i] = rr[u].len;
                     }
                     if (to_regs) {
-                        reg_off[u] = (uint32_t)(rr[u].off >> 7);
+                        reg_off[u] = (uint32_t)(rr[u].off >> 7);  // line index (off = line * 128 + kLineBias)
                         reg_len[u] = rr[u].len;
                     }
                 }
@@ -551,7 +551,7 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
 #pragma unroll
         for (int u = 0; u < kSortReg; ++u) {
             const uint64_t t = threadIdx.x + (uint64_t)kFillThreads * u;
-            if (t < regs_rows) out_off[t] = (uint64_t)reg_off[u] << 7;
+            if (t < regs_rows) out_off[t] = ((uint64_t)reg_off[u] << 7) + kLineBias;
         }
     }
     if (in_regs && regs_rows < filled) {
@@ -598,7 +598,7 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
             const uint64_t t = threadIdx.x + (uint64_t)kFillThreads * u;
             if (t < filled) {
                 PairTask tk;
-                tk.off = (uint64_t)reg_off[u] << 7;
+                tk.off = ((uint64_t)reg_off[u] << 7) + kLineBias;
                 tk.len = reg_len[u];
                 tk.slot = (uint32_t)t;
                 task[atomicAdd(&hist[bin_of(tk.len)], 1u)] = tk;
@@ -730,7 +730,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         }
         H st;
         if constexpr (DMA) {
-            // prefixes > 4 bytes go to DMA = false
+            // prefixes of 0 or > 4 bytes go to DMA = false
             hash_key_dma_lines<H, DIAG>(kv, st, my_lds, q.prefix_word, L.st.lines);
         } else {
             hash_key<H>(kv, st);

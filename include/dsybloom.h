@@ -160,8 +160,9 @@ int dsy_store_upload(dsy_ctx* ctx, const uint8_t* blob, uint64_t blob_len, const
                      const uint64_t* global_time, const uint32_t* meta, const uint8_t* undone, dsy_store** out);
 /* Same, over device buffers the caller keeps alive (the index arrays are not copied).  d_blob needs
  * DSY_BLOB_GUARD readable bytes before offsets[0] and past offsets[n].
- * Both forms also build the responder's line copy of the packets on the device: every packet starts on a
- * 128-byte line (< 128 bytes of padding per row), so the hashing kernel's loads are whole cache lines. */
+ * Both forms also build the responder's line copy of the packets on the device: every packet starts one byte
+ * into a 128-byte line (<= 128 bytes of padding per row), so the hashing kernel's loads are whole cache lines and a
+ * message with a 1-byte prefix starts on a line. */
 int dsy_store_attach(dsy_ctx* ctx, const uint8_t* d_blob, uint64_t blob_len, const uint64_t* d_offsets, uint64_t n,
                      const uint64_t* d_global_time, const uint32_t* d_meta, const uint8_t* d_undone, dsy_store** out);
 int dsy_store_free(dsy_store* store);
