@@ -179,7 +179,9 @@ class EpidemicSim(object):
         poffs = np.concatenate([[0], np.cumsum(pcounts)[:-1]])
         resps, tested = self.e.respond(claims_in, n_in, poffs, int(pcounts.sum()))
         self.tested += tested
-        back = self._alltoall_counts(pcounts)
+        # every claim gets exactly one response record, so the responses rank d returns are the claims sent to d:
+        # no count exchange is needed on the way back
+        back = counts
         resps_in = self._alltoall_records(resps, pcounts, back, c.resp_bytes)
         self.e.merge(resps_in, int(back.sum()))
 
