@@ -8,9 +8,10 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/ab || exit 1
 BASE=${BASE:-$PWD/dispersy_amd/libdsybloom_base.so}
 ROUNDS=${ROUNDS:-2}
+EXTRA=${EXTRA:-sha1}  # bench.py --extra legs beside the headline
 for i in $(seq 1 "$ROUNDS"); do
-  DSY_LIB_PATH=$BASE timeout -k 10 150 python bench.py --steps 30 --extra sha1 --cpu-claims 0 \
+  DSY_LIB_PATH=$BASE timeout -k 10 200 python bench.py --steps 30 --extra "$EXTRA" --cpu-claims 0 \
       > gpurun_out/ab/base$i.json 2> gpurun_out/ab/base$i.err &&
-  timeout -k 10 150 python bench.py --steps 30 --extra sha1 --cpu-claims 0 \
+  timeout -k 10 200 python bench.py --steps 30 --extra "$EXTRA" --cpu-claims 0 \
       > gpurun_out/ab/new$i.json 2> gpurun_out/ab/new$i.err || exit 1
 done
