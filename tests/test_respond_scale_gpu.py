@@ -144,3 +144,54 @@ def test_one_meta_mixed_families_vs_oracle(skew, meta_name, window):
             want = sync_ref.respond_lists(conn, served_oracle, (q.time_low, q.time_high, q.offset, q.modulo), ob,
                                           gt_now, limit, False)
             assert store.rowid[g].tolist() == want, (meta_name, q.time_low, q.time_high, q.modulo, q.offset, limit)
+
+
+def test_one_meta_many_claims_with_empty_ranges():
+    """5000 claims in one call (more than the 4096-claim minimum window pool, so the pool is sized by the batch) on
+    one served meta: the fused first window with claims whose range selects nothing (beyond the store, inverted, a
+    modulo no row satisfies) mixed among ordinary ones, every answer checked against the sqlite oracle."""
+    rows, conn = build(41, 8_000, 20_000, False)
+    store = SyncStore.from_rows(rows)
+    gt_now = 20_100
+    chosen = [m for m in METAS if m[0] == "a"]
+    served = [MetaMessage(n, i, SyncDistribution(d, p, None)) for n, i, d, p, _ in chosen]
+    served_oracle = [dict(name=n, id=i, direction=d, priority=p, pruning=None) for n, i, d, p, _ in chosen]
+    com = SyncCommunity(store, served, global_time=gt_now)
+    rng = np.random.Generator(np.random.PCG64(77))
+    packets = {r[0]: r[4] for r in rows}
+    shapes = [(10160, 0.01), (4096, 0.001)]
+    filters = []
+    for m, f in shapes:
+        for prefix in (b"\x01", b"\x02\x03"):
+            bf, ob = BloomFilter(m, f, prefix), OracleBloom.from_m_f(m, f, prefix)
+            known = [packets[r[0]] for r in rows if rng.random() < 0.97]
+            bf.add_keys(known)
+            ob.add_keys(known)
+            filters.append((bf, ob))
+    reqs, obs = [], []
+    for q in range(5000):
+        bf, ob = filters[q % len(filters)]
+        kind = q % 10
+        if kind == 0:    # beyond every stored global time
+            lo, hi, modulo, offset = gt_now + 5, gt_now + 500, 1, 0
+        elif kind == 1:  # inverted
+            lo, hi, modulo, offset = 900, 100, 1, 0
+        elif kind == 2:  # a one-global-time range that the modulo excludes
+            g = int(rng.integers(1, gt_now))
+            lo, hi, modulo, offset = g, g, 7, (7 - g % 7 + 1) % 7
+        else:
+            modulo = int(rng.choice([1, 1, 5, 113]))
+            offset = int(rng.integers(0, modulo))
+            lo = int(rng.integers(1, gt_now // 2))
+            hi = int(rng.integers(lo, gt_now + 10))
+        reqs.append(ClaimRequest(lo, hi, modulo, offset, bf))
+        obs.append(ob)
+    got = com.respond(reqs, byte_limit=5120)
+    for i, (q, ob, g) in enumerate(zip(reqs, obs, got)):
+        if i % 10 >= 3 and i % 5:
+            continue  # every empty-range claim, one ordinary claim in five (the oracle costs ~10 ms per claim)
+        want = sync_ref.respond_lists(conn, served_oracle, (q.time_low, q.time_high, q.offset, q.modulo), ob, gt_now,
+                                      5120, False)
+        assert store.rowid[g].tolist() == want, (i, q.time_low, q.time_high, q.modulo, q.offset)
+        if i % 10 < 3:
+            assert len(g) == 0
