@@ -63,6 +63,7 @@ struct dsy_ctx {
     uint32_t max_grid = 2048;
     int bloom_diag = 0;  // DSY_BLOOM_DIAG at creation: single-filter ceiling diagnostics (k_bloom DIAG)
     int pair_diag = 0;   // DSY_PAIR_DIAG at creation: responder ceiling diagnostics (k_pair_test DIAG)
+    uint32_t pair_grid = 0;  // DSY_PAIR_GRID at creation: k_pair_test grid cap (0: max_grid, 8 workgroups per CU)
     int or_mode = 1;     // DSY_OR_MODE at creation: filter-build atomics (filter_set_all OR_MODE, dsy_message.h)
     uint32_t timing = 0;  // bit i: bracket class i with events
     std::vector<PendingTimer> pending;
@@ -374,6 +375,7 @@ int dsy_ctx_create(int device, dsy_ctx** out) {
     if (const char* v = getenv("DSY_BLOOM_DIAG")) c->bloom_diag = atoi(v);
     if (const char* v = getenv("DSY_PAIR_DIAG")) c->pair_diag = atoi(v);
     if (const char* v = getenv("DSY_OR_MODE")) c->or_mode = atoi(v);
+    if (const char* v = getenv("DSY_PAIR_GRID")) c->pair_grid = (uint32_t)atoi(v);
     hipHostMalloc(&c->pinned, 4096, hipHostMallocDefault);
     *out = c;
     return DSY_OK;
@@ -1630,6 +1632,7 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     L.counters = (uint64_t*)io;
     L.stream = c->stream;
     L.diag = c->pair_diag;
+    L.grid_cap = c->pair_grid ? c->pair_grid : c->max_grid;
 
     // ---- per-claim output capacity: every emitted packet but the last costs >= min_len bytes of budget, so a
     // claim sends at most byte_limit / min_len + 2 packets.  When that bound is small the capacities and output

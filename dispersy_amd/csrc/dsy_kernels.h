@@ -180,6 +180,7 @@ struct RespondLaunch {
                               // chunks (k_fill atomicMax, read by k_pair_test, reset by k_compact)
     uint64_t* fill_clock;     // optional [n_act][4] s_memtime stamps of k_fill phases (DSY_FILL_PROFILE)
     int diag;                 // k_pair_test DIAG (MD5 / SHA-1, 2-byte chunks): 0 product, 1 no loads, 2 loads only
+    uint32_t grid_cap;        // k_pair_test workgroups at most (0: 2048)
     hipEvent_t ev_start, ev_stop;  // when set: recorded by k_pair_test's own dispatch (launch_timed)
     uint64_t* counters;       // device [kCntSpread][kCntN]: pairs hashed, compression blocks, packet bytes, pairs the reference
                               // would have hashed (it stops at the byte limit), lane-block slots of the hashing waves

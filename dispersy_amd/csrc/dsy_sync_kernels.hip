@@ -780,7 +780,11 @@ template <class H, int CHUNK>
 static hipError_t pair_test_family(const RespondLaunch& L, bool long_prefix, const uint32_t* list, uint32_t n_list) {
     const uint64_t waves = (uint64_t)n_list * (L.window / 64);
     uint64_t blocks = (waves + 3) / 4;
-    if (blocks > 256 * 16) blocks = 256 * 16;
+    // 8 workgroups per CU (respond_core: the ctx's max_grid, DSY_PAIR_GRID overrides): the grid-stride then deals
+    // each wave 2-3 wave-tasks round-robin; same-box A/B on the headline, 4096 / 2048 / 1280 / 1024 workgroups:
+    // 227-229 / 224-226 / 230-233 / 230-234 us
+    const uint64_t cap = L.grid_cap ? L.grid_cap : 2048;
+    if (blocks > cap) blocks = cap;
     if (blocks == 0) return hipSuccess;
     // MD5 and SHA-1 stage their 64-byte blocks through LDS with DMA (8 keys x 128 contiguous bytes per wave
     // instruction, single LDS buffer, next stage in flight while the current one is compressed from registers:
