@@ -63,6 +63,7 @@ struct dsy_ctx {
     uint32_t max_grid = 2048;
     int bloom_diag = 0;  // DSY_BLOOM_DIAG at creation: single-filter ceiling diagnostics (k_bloom DIAG)
     int pair_diag = 0;   // DSY_PAIR_DIAG at creation: responder ceiling diagnostics (k_pair_test DIAG)
+    uint32_t bloom_grid = 0; // DSY_BLOOM_GRID at creation: k_bloom grid cap (0: max_grid)
     uint32_t pair_grid = 0;  // DSY_PAIR_GRID at creation: k_pair_test grid cap (0: max_grid, 8 workgroups per CU)
     int or_mode = 1;     // DSY_OR_MODE at creation: filter-build atomics (filter_set_all OR_MODE, dsy_message.h)
     uint32_t timing = 0;  // bit i: bracket class i with events
@@ -309,7 +310,7 @@ int run_bloom(dsy_ctx* c, BloomOp op, const dsy_bloom_params* p, const uint8_t* 
     L.use_lds = (uint64_t)L.nwords * 4 <= 64 * 1024;
     L.present = d_present;
     L.indices = d_idx;
-    L.max_grid = c->max_grid;
+    L.max_grid = c->bloom_grid ? c->bloom_grid : c->max_grid;
     L.stream = c->stream;
     L.diag = c->bloom_diag;
     L.or_mode = c->or_mode;
@@ -376,6 +377,7 @@ int dsy_ctx_create(int device, dsy_ctx** out) {
     if (const char* v = getenv("DSY_PAIR_DIAG")) c->pair_diag = atoi(v);
     if (const char* v = getenv("DSY_OR_MODE")) c->or_mode = atoi(v);
     if (const char* v = getenv("DSY_PAIR_GRID")) c->pair_grid = (uint32_t)atoi(v);
+    if (const char* v = getenv("DSY_BLOOM_GRID")) c->bloom_grid = (uint32_t)atoi(v);
     hipHostMalloc(&c->pinned, 4096, hipHostMallocDefault);
     *out = c;
     return DSY_OK;
