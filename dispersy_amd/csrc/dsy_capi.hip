@@ -63,7 +63,7 @@ struct dsy_ctx {
     uint32_t max_grid = 2048;
     int bloom_diag = 0;  // DSY_BLOOM_DIAG at creation: single-filter ceiling diagnostics (k_bloom DIAG)
     int pair_diag = 0;   // DSY_PAIR_DIAG at creation: responder ceiling diagnostics (k_pair_test DIAG)
-    uint32_t bloom_grid = 0; // DSY_BLOOM_GRID at creation: k_bloom grid cap (0: max_grid)
+    uint32_t bloom_grid = 0; // DSY_BLOOM_GRID at creation: k_bloom grid cap (0: 2 x max_grid)
     uint32_t pair_grid = 0;  // DSY_PAIR_GRID at creation: k_pair_test grid cap (0: max_grid, 8 workgroups per CU)
     int or_mode = 1;     // DSY_OR_MODE at creation: filter-build atomics (filter_set_all OR_MODE, dsy_message.h)
     uint32_t timing = 0;  // bit i: bracket class i with events
@@ -310,7 +310,10 @@ int run_bloom(dsy_ctx* c, BloomOp op, const dsy_bloom_params* p, const uint8_t* 
     L.use_lds = (uint64_t)L.nwords * 4 <= 64 * 1024;
     L.present = d_present;
     L.indices = d_idx;
-    L.max_grid = c->bloom_grid ? c->bloom_grid : c->max_grid;
+    // 16 workgroups per CU for the hashing kernels (same-box A/B over 10 M keys, grid 1024 / 1536 / 2048 / 4096 /
+    // 8192 / 16384: MD5 test 2.39-2.42 / 2.38-2.42 / 2.38-2.40 / 2.34-2.37 / 2.36-2.38 / 2.40 ms, SHA-1 within 1 % of
+    // 4096 from 4096 up; profiles/ab_bloom_grid_r2.json)
+    L.max_grid = c->bloom_grid ? c->bloom_grid : 2 * c->max_grid;
     L.stream = c->stream;
     L.diag = c->bloom_diag;
     L.or_mode = c->or_mode;
