@@ -36,7 +36,8 @@ OPS_PER_BLOCK = {"md5": 500, "sha1": 961, "sha256": 2168, "sha384": 5504, "sha51
 # ------------------------------------------------------------------------------------------- CPU legs
 def cpu_info():
     """(CPU model, cores this process may use).  On the GPU box the affinity mask shows the whole machine; the
-    box's share is OMP_NUM_THREADS (16 per GPU), so that caps the worker count."""
+    box's share is OMP_NUM_THREADS (16 per GPU), so that caps the worker count (N = the cores the
+    job may use)."""
     model = None
     try:
         with open("/proc/cpuinfo") as f:
@@ -48,37 +49,116 @@ def cpu_info():
         pass
     avail = len(os.sched_getaffinity(0))
     share = int(os.environ.get("OMP_NUM_THREADS") or avail)
-    # forked workers inherit the parent's open device files: stay below the box's 16-process GPU guard
-    return model, max(1, min(avail, share, 15))
+    return model, max(1, min(avail, share))
 
 
-_PAR = {}
+# ------------------------------------------------------------------- the CPU worker pool (forked before any GPU use)
+class Shared(object):
+    """A read-only numpy array in a file under /dev/shm: it pickles as the file's path, so a pool task attaches to
+    it (np.memmap) instead of receiving a copy.  The creating process unlinks the files at exit (Shared.cleanup)."""
+    _mine = []
+
+    def __init__(self, arr):
+        import tempfile
+        base = "/dev/shm" if os.access("/dev/shm", os.W_OK) else None
+        fd, self.path = tempfile.mkstemp(prefix="dsy_bench_", suffix=".bin", dir=base)
+        arr = np.ascontiguousarray(arr)
+        with os.fdopen(fd, "wb") as f:
+            f.write(memoryview(arr).cast("B") if arr.size else b"")
+        self.dtype, self.shape = arr.dtype.str, arr.shape
+        self.a = arr
+        Shared._mine.append(self.path)
+
+    def __reduce__(self):
+        return (_attach_shared, (self.path, self.dtype, self.shape))
+
+    @classmethod
+    def cleanup(cls):
+        for p in cls._mine:
+            try:
+                os.unlink(p)
+            except OSError:
+                pass
+        cls._mine = []
 
 
-def _par_worker(i):
-    """One forked worker: pure CPU work over data the parent set up before forking (never touches the GPU).  fn
-    returns the units done, or (units, seconds) when it times its own measured part (after a private setup)."""
+class _Attached(object):
+    def __init__(self, a):
+        self.a = a
+
+
+def _attach_shared(path, dtype, shape):
+    n = int(np.prod(shape)) if shape else 1
+    if n == 0:
+        return _Attached(np.zeros(shape, dtype=np.dtype(dtype)))
+    return _Attached(np.memmap(path, dtype=np.dtype(dtype), mode="r", shape=shape))
+
+
+def _pool_task(payload):
+    """One pool task: (fn, shard) pickled with cloudpickle (closures included).  fn returns the units done, or
+    (units, seconds) when it times its own measured part after a private, untimed setup."""
+    import cloudpickle
+    fn, shard = cloudpickle.loads(payload)
     t0 = time.perf_counter()
-    r = _PAR["fn"](_PAR["shards"][i])
+    r = fn(shard)
     return r if isinstance(r, tuple) else (r, time.perf_counter() - t0)
 
 
-def cpu_parallel(fn, shards):
-    """Run fn(shard) for every shard in len(shards) forked processes at once; returns (units, wall seconds of the
-    slowest): the N-core rate is units / seconds.  fn must be CPU-only (hashlib / sqlite / numpy)."""
-    import multiprocessing as mp
-    _PAR.update(fn=fn, shards=shards)
-    with mp.get_context("fork").Pool(len(shards)) as pool:
-        res = pool.map(_par_worker, range(len(shards)))
-    _PAR.clear()
-    return sum(u for u, _ in res), max(t for _, t in res)
+class CpuPool(object):
+    """The N-core CPU legs' workers.  They are forked at start-up, before torch is imported or HIP is touched, so
+    no worker inherits device files or GPU runtime state; tasks reach them as cloudpickle payloads (large arrays as
+    `Shared` files), and they are shut down with close + join (no SIGTERM: a profiler's signal handler in a worker
+    would turn that into an abort)."""
+
+    def __init__(self, n):
+        import multiprocessing as mp
+        self.n = n
+        self.pool = mp.get_context("fork").Pool(n)
+
+    def run(self, fn, shards):
+        """fn(shard) for every shard at once (len(shards) <= n); returns (units, wall seconds of the slowest)."""
+        import cloudpickle
+        if len(shards) > self.n:
+            raise ValueError("%d shards for %d workers" % (len(shards), self.n))
+        res = self.pool.map(_pool_task, [cloudpickle.dumps((fn, s)) for s in shards], chunksize=1)
+        return sum(u for u, _ in res), max(t for _, t in res)
+
+    def close(self):
+        self.pool.close()
+        self.pool.join()
+
+
+POOL = None  # the CpuPool of this run (rank 0 at N = 1 with CPU legs), or None
 
 
 def n_core_leg(fn, shards, unit, sample):
-    model, cores = cpu_info()
-    units, secs = cpu_parallel(fn, shards)
+    model, _ = cpu_info()
+    if POOL is None:
+        return None
+    units, secs = POOL.run(fn, shards)
     return {"value": round(units / secs, 1), "unit": unit, "cores": len(shards), "cpu_model": model,
-            "sample": sample, "seconds": round(secs, 2)}
+            "sample": sample, "seconds": round(secs, 2),
+            "workers": "forked before the first GPU call (CpuPool), one per core of the job's share"}
+
+
+# ------------------------------------------------------------------------------------- N ranks from one command
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """`python bench.py --gpus N` without a launcher: start N ranks (one process per GPU) through
+    torch.distributed.run as a CHILD process and return its exit code.  This process has not touched the GPU
+    (nothing is imported but argparse/numpy) and it never exec's; the ranks find WORLD_SIZE = N in their env."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd)
 
 
 def parse():
@@ -91,7 +171,9 @@ def parse():
     ap.add_argument("--filter-bits", type=int, default=10160)
     ap.add_argument("--error-rate", type=float, default=0.01)
     ap.add_argument("--byte-limit", type=int, default=5120)
-    ap.add_argument("--cpu-claims", type=int, default=96, help="claims in the CPU-baseline sample (0: skip)")
+    ap.add_argument("--cpu-claims", type=int, default=1, help="0: skip the CPU-baseline legs (and the CPU pool)")
+    ap.add_argument("--cpu-pairs", type=int, default=100_000,
+                    help="responder CPU baselines: (claim, packet) pairs hashed in the 1-core sample (BASELINE.md:47)")
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--window", type=int, default=0, help="cap on the responder's window (pairs per claim; 0: default)")
     ap.add_argument("--sim-peers", type=int, default=1_000_000, help="config 3 gossip simulator peers (0: skip)")
@@ -111,11 +193,32 @@ def parse():
 
 
 def main():
+    global POOL
     args = parse()
-    import torch
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print("bench.py: %d ranks were launched for --gpus %d; refusing to report a wrong n_gpus" % (world, args.gpus),
+              file=sys.stderr)
+        sys.exit(2)
+    if os.environ.get("DSY_BENCH_PROBE"):  # launcher test (tests/test_bench_launch.py): report and stop, no GPU
+        print(json.dumps({"probe": True, "rank": rank, "world": world, "local_rank": local, "gpus": args.gpus}))
+        return
+    if rank == 0 and world == 1 and args.cpu_claims > 0:
+        POOL = CpuPool(cpu_info()[1])  # before torch / HIP: the workers inherit no GPU state
+    try:
+        run(args, rank, world, local)
+    finally:
+        if POOL is not None:
+            POOL.close()
+        Shared.cleanup()
+
+
+def run(args, rank, world, local):
+    import torch
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -252,7 +355,8 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_claims > 0:
-        cpu = cpu_baseline(args, ctx, lib, store, reqs, claims, blob, offsets, total_bytes, N, fblob)
+        cpu = responder_cpu(args, ctx, lib, store, reqs, claims, fblob, blob, offsets,
+                            np.arange(1, N + 1, dtype=np.uint64), N, dev, "cfg2 md5")
 
     extra = set(x for x in args.extra.split(",") if x and x != "none")
 
@@ -382,7 +486,8 @@ def sha1_respond(args, ctx, lib, store, N, dev, blob, offsets, total_bytes, meta
                         "hbm_gbs": round((kt["bytes"] / launches + total / steps * 17) / avg_s / 1e9, 1),
                         "lane_utilization": round(work["blocks"] / max(work["lane_slots"], 1), 4)}}
     if rank == 0 and world == 1 and args.cpu_claims > 0:
-        out["cpu_baseline"] = cpu_baseline(args, ctx, lib, store, reqs, claims, blob, offsets, total_bytes, N, fblob)
+        out["cpu_baseline"] = responder_cpu(args, ctx, lib, store, reqs, claims, fblob, blob, offsets,
+                                            np.arange(1, N + 1, dtype=np.uint64), N, dev, "sha1")
     return out
 
 
@@ -564,12 +669,14 @@ def dedup_bench(args, ctx, lib, store, blob, offsets, N, batch=10_000, reps=10, 
 
         conn.close()
 
+        m_pre, g_pre = member[:pre].copy(), gt[:pre].copy()  # what the workers' tables need (not 10 M rows)
+
         def table():
             c = sqlite3.connect(":memory:")
             c.executescript(SYNC_SCHEMA)
             r = np.random.Generator(np.random.PCG64(6))
             c.executemany("INSERT INTO sync (community, member, global_time, meta_message, packet) VALUES (1, ?, ?, 1, ?)",
-                          ((int(member[i]), int(gt[i]), r.bytes(int(l)))
+                          ((int(m_pre[i]), int(g_pre[i]), r.bytes(int(l)))
                            for i, l in zip(range(pre), r.integers(100, 1501, size=pre))))
             c.commit()
             return c
@@ -923,6 +1030,7 @@ def single_filter(args, ctx, lib, blob, offsets, N, dev, rank, world):
                                                           offsets.data_ptr(), n_add, filt.data_ptr()))
         test = lambda: _native.check(lib.dsy_bloom_test_dev(ctx.handle, ctypes.byref(bf.params), blob.data_ptr(),  # noqa: E731
                                                             offsets.data_ptr(), N, filt.data_ptr(), present.data_ptr()))
+        ctx.wait_torch(dev)  # the zeroed filter (torch's stream) before the ctx stream's build
         add()
         test()  # warm-up
         k_add, _ = _timed_bloom(ctx, add, 3)
@@ -948,16 +1056,29 @@ def single_filter(args, ctx, lib, blob, offsets, N, dev, rank, world):
     return out
 
 
-def single_filter_cpu(blob, offsets):
-    """oracle/bloom_ref (hashlib + Python int bit array, one core) on a bounded sample of the same packets."""
+def host_keys(blob, offsets, n):
+    """The first n packets of a device store as (Shared blob, Shared offsets) on the host."""
+    end = int(offsets[n].item())
+    return Shared(blob[:end].cpu().numpy()), Shared(offsets[:n + 1].cpu().numpy())
+
+
+def key_list(s_blob, s_off, lo=0, hi=None):
+    """bytes objects of packets [lo, hi) of a host_keys pair (the reference's keys are py2 str)."""
+    b, o = s_blob.a, s_off.a
+    hi = len(o) - 1 if hi is None else hi
+    return [bytes(b[int(o[i]):int(o[i + 1])]) for i in range(lo, hi)]
+
+
+def single_filter_cpu(blob, offsets, n_add=100_000, n_test=1_000_000):
+    """BASELINE config 1 in full on the CPU (BASELINE.md:46): oracle/bloom_ref (hashlib + Python int bit array)
+    adds 100 k packets and tests 1 M (the first 1 M packets of the store, the 100 k added among them), one core;
+    then one process per core, each building the same filter (untimed) and testing its disjoint share of the 1 M."""
     from oracle.bloom_ref import OracleBloom
-    n_add, n_test = 20_000, 200_000
-    end = int(offsets[n_test].item())
-    host = bytes(blob[:end].cpu().numpy())
-    off = offsets[:n_test + 1].cpu().numpy()
-    keys = [host[int(off[i]):int(off[i + 1])] for i in range(n_test)]
+    s_blob, s_off = host_keys(blob, offsets, n_test)
+    keys = key_list(s_blob, s_off)
     res = {}
-    for name, m, f, prefix in (("md5", 10160, 0.01, b"\x00\x01\x02\x03"), ("sha1", 4096, 0.001, b"x")):
+    fams = (("md5", 10160, 0.01, b"\x00\x01\x02\x03"), ("sha1", 4096, 0.001, b"x"))
+    for name, m, f, prefix in fams:
         ob = OracleBloom.from_m_f(m, f, prefix)
         t0 = time.perf_counter()
         ob.add_keys(keys[:n_add])
@@ -965,20 +1086,25 @@ def single_filter_cpu(blob, offsets):
         hits = sum(1 for k in keys if k in ob)
         t2 = time.perf_counter()
         res[name] = {"add_keys_per_s": round(n_add / (t1 - t0), 1), "test_keys_per_s": round(n_test / (t2 - t1), 1),
-                     "present": hits}
+                     "present": hits, "seconds": round(t2 - t0, 2)}
+    del keys
     model, cores = cpu_info()
-    for name, m, f, prefix in (("md5", 10160, 0.01, b"\x00\x01\x02\x03"), ("sha1", 4096, 0.001, b"x")):
-        ob = OracleBloom.from_m_f(m, f, prefix)
-        ob.add_keys(keys[:n_add])
-
-        def test(idx, ob=ob):
-            for i in idx:
-                keys[i] in ob  # noqa: B015 -- the membership test is the work
-            return len(idx)
-        res[name]["n_core"] = n_core_leg(test, [range(n_test)] * cores, "tests/s",
-                                         "the %d tests in every process, one process per core" % n_test)
+    for name, m, f, prefix in fams:
+        def test(w, m=m, f=f, prefix=prefix):
+            lo, hi = w * n_test // cores, (w + 1) * n_test // cores
+            ob = OracleBloom.from_m_f(m, f, prefix)
+            ob.add_keys(key_list(s_blob, s_off, 0, n_add))
+            mine = key_list(s_blob, s_off, lo, hi)
+            t1 = time.perf_counter()
+            for k in mine:
+                k in ob  # noqa: B015 -- the membership test is the work
+            return hi - lo, time.perf_counter() - t1
+        res[name]["n_core"] = n_core_leg(test, list(range(cores)), "tests/s",
+                                         "the %d tests split over the processes (disjoint shares), each against its "
+                                         "own copy of the filter of the %d adds" % (n_test, n_add))
     return {"kind": "port", "cores": 1, "cpu_model": model,
-            "sample": "%d adds + %d tests of the same packets per filter" % (n_add, n_test), "results": res}
+            "sample": "the full config: %d adds + %d tests (the first %d packets of the store) per filter"
+                      % (n_add, n_test, n_test), "results": res}
 
 
 def large_filter(args, ctx, lib, dev, rank, world, dist=None):
@@ -1017,6 +1143,7 @@ def large_filter(args, ctx, lib, dev, rank, world, dist=None):
                                                             test_off.data_ptr(), n_test, filt.data_ptr(),
                                                             present.data_ptr()))
         filt.zero_()
+        ctx.wait_torch(dev)  # torch's zeroing before the ctx stream's build
         k_add, _ = _timed_bloom(ctx, add, 1)
         union = None
         if dist is not None and world > 1:
@@ -1028,6 +1155,7 @@ def large_filter(args, ctx, lib, dev, rank, world, dist=None):
             t0 = time.perf_counter()
             add()
             union = union_filter(ctx, coll, filt)
+            torch.cuda.synchronize()  # union_filter returns with the OR queued on torch's stream
             t_job = coll.scalar(time.perf_counter() - t0, "max", device=dev)
             filt.copy_(union)
             torch.cuda.synchronize()
@@ -1055,33 +1183,36 @@ def large_filter(args, ctx, lib, dev, rank, world, dist=None):
     return out
 
 
-def large_filter_cpu(blob, offsets):
+def large_filter_cpu(blob, offsets, n_add=100_000, n_test=100_000):
     """oracle/bloom_ref at m = 2^20 (hashlib + Python int bit array: O(m) per set bit, the reference's cost
-    model), one core, on 3000 adds and 20000 tests of the same packets."""
+    model), one core, on 10^5 adds and 10^5 tests (BASELINE.md:50; the cost per op does not depend on the fill, so
+    the 100 M-key figure is an extrapolation); then one process per core adding its disjoint share of the 10^5
+    into its own partial filter, as a sharded build."""
     from oracle.bloom_ref import OracleBloom
-    n_add, n_test = 3000, 20000
-    end = int(offsets[n_add + n_test].item())
-    host = bytes(blob[:end].cpu().numpy())
-    off = offsets[:n_add + n_test + 1].cpu().numpy()
-    keys = [host[int(off[i]):int(off[i + 1])] for i in range(n_add + n_test)]
+    s_blob, s_off = host_keys(blob, offsets, n_add + n_test)
+    keys = key_list(s_blob, s_off)
     ob = OracleBloom.from_m_f(1 << 20, 0.01, b"\x07")
     t0 = time.perf_counter()
     ob.add_keys(keys[:n_add])
     t1 = time.perf_counter()
     sum(1 for k in keys[n_add:] if k in ob)
     t2 = time.perf_counter()
+    del keys
     model, cores = cpu_info()
 
-    def adds(idx):
-        mine = OracleBloom.from_m_f(1 << 20, 0.01, b"\x07")  # each process its own partial filter, as a sharded build
-        mine.add_keys(keys[i] for i in idx)
-        return len(idx)
-    ncore = n_core_leg(adds, [[(w * 997 + j) % n_add for j in range(n_add)] for w in range(cores)], "adds/s",
-                       "%d adds per process into its own 2^20 filter" % n_add)
+    def adds(w):
+        lo, hi = w * n_add // cores, (w + 1) * n_add // cores
+        mine = key_list(s_blob, s_off, lo, hi)
+        part = OracleBloom.from_m_f(1 << 20, 0.01, b"\x07")
+        t3 = time.perf_counter()
+        part.add_keys(mine)
+        return hi - lo, time.perf_counter() - t3
+    ncore = n_core_leg(adds, list(range(cores)), "adds/s",
+                       "the %d adds split over the processes (disjoint shares), each into its own 2^20 filter" % n_add)
     return {"kind": "port", "cores": 1, "filter": "2^20", "cpu_model": model,
             "sample": "%d adds + %d tests, extrapolated per key" % (n_add, n_test),
             "add_keys_per_s": round(n_add / (t1 - t0), 1), "test_keys_per_s": round(n_test / (t2 - t1), 1),
-            "n_core": ncore}
+            "seconds": round(t2 - t0, 2), "n_core": ncore}
 
 
 def heavy_tail(args, ctx, lib, dev, rank, world, dist):
@@ -1190,7 +1321,8 @@ def heavy_tail(args, ctx, lib, dev, rank, world, dist):
         hashed = int(coll.scalar(int(hashed), "sum", device=dev))
     cpu = None
     if rank == 0 and world == 1 and args.cpu_claims > 0:
-        cpu = heavy_tail_cpu(args, lib, ctx, store, reqs, claims, fblob, blob, offsets, total, h_gt, G_MAX)
+        cpu = responder_cpu(args, ctx, lib, store, reqs, claims, fblob, blob, offsets, h_gt.astype(np.uint64), G_MAX,
+                            dev, "cfg5 heavy tail")
     lib.dsy_store_free(store)
     secs = kt["ms"] / 1e3
     out = {"metric": "packets hashed+tested/sec", "value": round(useful / dt, 1), "unit": "packets/s", "n_gpus": world,
@@ -1216,102 +1348,96 @@ def heavy_tail(args, ctx, lib, dev, rank, world, dist):
     return out
 
 
-def heavy_tail_cpu(args, lib, ctx, store, reqs, claims, fblob, blob, offsets, total, h_gt, g_max, n_sample=24):
-    """cfg5's CPU legs: the oracle's array-form responder (numpy range/modulo selection + hashlib not_filter loop
-    exactly as the reference) on the first n_sample claims, 1 core, with the GPU's answers for those claims checked
-    against it (host-buffer dsy_sync_respond); then one process per core over disjoint claim shards."""
+def responder_cpu(args, ctx, lib, store, reqs, claims, fblob, blob, offsets, h_gts, g_time, dev, label,
+                  max_claims=1024):
+    """The responder's CPU baseline (configs 2 and 5, the SHA-1 leg): oracle/sync_ref.respond_arrays -- numpy for
+    the range / modulo predicate (faster than the reference's sqlite scan, so generous to the CPU), hashlib + Python
+    for the lazy not_filter / byte-limit loop exactly as the reference (community.py:2555-2567) -- over the first
+    claims of the step until >= --cpu-pairs (claim, packet) pairs are hashed (BASELINE.md:47), 1 core; the GPU's
+    answers for the same claims (host-buffer dsy_sync_respond) checked against it; then every worker of the pool
+    runs the same sample (rotated), one process per core.
+
+    Only the packets the lazy loop touches travel to the host: a claim walks its selected rows in send order up to
+    the packet that spends the budget (all of them when the budget is never spent), which the GPU's answer fixes.
+    They are gathered on the GPU into one compact blob shared with the workers through /dev/shm."""
+    import torch
     from oracle import sync_ref
     from oracle.bloom_ref import OracleBloom
-    host_blob = memoryview(blob[:total].cpu().numpy())
-    host_off = offsets.cpu().numpy()
-    N = len(h_gt)
-    gt_by_meta = {1: (np.arange(N, dtype=np.int64), h_gt.astype(np.uint64))}
-    packet_of = lambda r: host_blob[int(host_off[r]):int(host_off[r + 1])]  # noqa: E731
-    metas = [dict(name="bench", id=1, direction="ASC", priority=128, pruning=None)]
-
-    def run(idx, cnt):
-        outs = []
-        for i in idx:
-            lo, hi, offset, modulo, kf, prefix, raw = claims[i]
-            outs.append(sync_ref.respond_arrays(packet_of, gt_by_meta, metas, (lo, hi, offset, modulo),
-                                                OracleBloom.from_bytes(raw, kf, prefix), g_max, args.byte_limit, False,
-                                                cnt))
-        return outs
-    sample = list(range(min(n_sample, len(claims))))
-    counter = [0]
-    t0 = time.perf_counter()
-    outs = run(sample, counter)
-    dt = time.perf_counter() - t0
-    sub = (type(reqs[0]) * len(sample))(*[reqs[i] for i in sample])
-    out_off = np.zeros(len(sample) + 1, dtype=np.uint64)
-    out = np.zeros(1 << 22, dtype=np.uint64)
-    _native.check(lib.dsy_sync_respond(ctx.handle, store, sub, len(sample), fblob, len(fblob),
-                                       (_native.Meta * 1)(_native.Meta(1, 0, 0, 0, 0)), 1, g_max, 0, args.byte_limit,
+    n_try = min(max_claims, len(claims))
+    sub = (type(reqs[0]) * n_try)(*[reqs[i] for i in range(n_try)])
+    out_off = np.zeros(n_try + 1, dtype=np.uint64)
+    out = np.zeros(1 << 24, dtype=np.uint64)
+    _native.check(lib.dsy_sync_respond(ctx.handle, store, sub, n_try, fblob, len(fblob),
+                                       (_native.Meta * 1)(_native.Meta(1, 0, 0, 0, 0)), 1, g_time, 0, args.byte_limit,
                                        99, out.ctypes.data, len(out), out_off.ctypes.data))
-    gpu = [out[int(out_off[j]):int(out_off[j + 1])].tolist() for j in range(len(sample))]
-    model, cores = cpu_info()
-
-    def shard(idx):
-        cnt = [0]
-        run(idx, cnt)
-        return cnt[0]
-    per = max(1, n_sample // 2)
-    ncore = n_core_leg(shard, [[(w * per + j) % len(claims) for j in range(per)] for w in range(cores)], "packets/s",
-                       "%d claims per process, one process per core, same port" % per)
-    return {"value": round(counter[0] / dt, 1), "unit": "packets/s", "cores": 1, "kind": "port", "cpu_model": model,
-            "sample": "%d of the step's claims (%d pairs hashed lazily) through oracle/sync_ref.respond_arrays + "
-                      "oracle/bloom_ref (hashlib), %.1f s" % (len(sample), counter[0], dt),
-            "gpu_matches_cpu_on_sample": gpu == outs, "n_core": ncore}
-
-
-def cpu_baseline(args, ctx, lib, store, reqs, claims, blob, offsets, total_bytes, N, fblob):
-    """The oracle's CPU port of the responder (hashlib + Python, one core) on a bounded sample of the same claims,
-    with the GPU's answers for those claims checked against it."""
-    from oracle import sync_ref
-    from oracle.bloom_ref import OracleBloom
-    host_blob = memoryview(blob[:total_bytes].cpu().numpy())
-    host_off = offsets.cpu().numpy()
-    rows = np.arange(N, dtype=np.int64)
-    gts = np.arange(1, N + 1, dtype=np.uint64)
-    gt_by_meta = {1: (rows, gts)}
-    packet_of = lambda r: host_blob[int(host_off[r]):int(host_off[r + 1])]  # noqa: E731
+    gpu = [out[int(out_off[j]):int(out_off[j + 1])].tolist() for j in range(n_try)]
+    h_off = offsets.cpu().numpy()
+    touched, sample, pairs = [], [], 0
+    for i in range(n_try):  # the rows the reference's lazy loop hashes for claim i (ASC meta, gt sorted by row)
+        lo, hi, offset, modulo = claims[i][:4]
+        a = int(np.searchsorted(h_gts, lo, side="left"))
+        b = int(np.searchsorted(h_gts, hi, side="right"))
+        sel = np.arange(a, b, dtype=np.int64)
+        if modulo > 1 and b > a:
+            sel = sel[(h_gts[a:b] + np.uint64(offset)) % np.uint64(modulo) == 0]
+        sent = gpu[i]
+        if sent and int((h_off[np.asarray(sent) + 1] - h_off[np.asarray(sent)]).sum()) >= args.byte_limit:
+            sel = sel[:int(np.searchsorted(sel, sent[-1])) + 1]
+        touched.append(sel)
+        sample.append(i)
+        pairs += len(sel)
+        if pairs >= args.cpu_pairs:
+            break
+    rows = np.unique(np.concatenate(touched)) if touched else np.zeros(0, np.int64)
+    d_rows = torch.from_numpy(rows).to(dev)
+    st = offsets[d_rows]
+    ln = offsets[d_rows + 1] - st
+    co = torch.zeros(len(rows) + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(ln, 0, out=co[1:])
+    total = int(co[-1].item())
+    idx = torch.arange(total, device=dev, dtype=torch.int64) + torch.repeat_interleave(st - co[:-1], ln)
+    s_blob, s_off, s_rows, s_gts = (Shared(blob[idx].cpu().numpy()), Shared(co.cpu().numpy()), Shared(rows),
+                                    Shared(h_gts))
+    del idx, d_rows, st, ln, co
     metas = [dict(name="bench", id=1, direction="ASC", priority=128, pruning=None)]
-    k = args.cpu_claims
-    sample = list(range(0, min(k, len(claims))))
+    byte_limit = args.byte_limit
+
+    def prepare():
+        cb, co_, rw, gts = s_blob.a, s_off.a, s_rows.a, s_gts.a
+        pos = dict(zip(rw.tolist(), range(len(rw))))
+        mv = memoryview(cb)
+        packet_of = lambda r: mv[int(co_[pos[r]]):int(co_[pos[r] + 1])]  # noqa: E731
+        return packet_of, {1: (np.arange(len(gts), dtype=np.int64), gts)}
+
+    def run(order, packet_of, gt_by_meta, counter):
+        return [sync_ref.respond_arrays(packet_of, gt_by_meta, metas, claims[i][:4],
+                                        OracleBloom.from_bytes(claims[i][6], claims[i][4], claims[i][5]), g_time,
+                                        byte_limit, False, counter) for i in order]
+
+    packet_of, gt_by_meta = prepare()
     counter = [0]
-    outs = []
     t0 = time.perf_counter()
-    for i in sample:
-        lo, hi, offset, modulo, kf, prefix, raw = claims[i]
-        ob = OracleBloom.from_bytes(raw, kf, prefix)
-        outs.append(sync_ref.respond_arrays(packet_of, gt_by_meta, metas, (lo, hi, offset, modulo), ob, N,
-                                            args.byte_limit, False, counter))
+    outs = run(sample, packet_of, gt_by_meta, counter)
     dt = time.perf_counter() - t0
-    # the GPU's answer for the same claims, through the host-buffer C-ABI entry point
-    sub = (type(reqs[0]) * len(sample))(*[reqs[i] for i in sample])
-    out_off = np.zeros(len(sample) + 1, dtype=np.uint64)
-    out = np.zeros(1 << 20, dtype=np.uint64)
-    _native.check(lib.dsy_sync_respond(ctx.handle, store, sub, len(sample), fblob, len(fblob),
-                                       (_native.Meta * 1)(_native.Meta(1, 0, 0, 0, 0)), 1, N, 0, args.byte_limit, 99,
-                                       out.ctypes.data, len(out), out_off.ctypes.data))
-    gpu = [out[int(out_off[j]):int(out_off[j + 1])].tolist() for j in range(len(sample))]
+    match = outs == gpu[:len(sample)]
     model, cores = cpu_info()
 
-    def shard(idx):
+    def shard(w):
+        p_of, gbm = prepare()
+        order = sample[w % len(sample):] + sample[:w % len(sample)]
         cnt = [0]
-        for i in idx:
-            lo, hi, offset, modulo, kf, prefix, raw = claims[i]
-            sync_ref.respond_arrays(packet_of, gt_by_meta, metas, (lo, hi, offset, modulo),
-                                    OracleBloom.from_bytes(raw, kf, prefix), N, args.byte_limit, False, cnt)
-        return cnt[0]
-    per = max(1, k // 2)
-    ncore = n_core_leg(shard, [[(w * per + j) % len(claims) for j in range(per)] for w in range(cores)], "packets/s",
-                       "%d claims per process, one process per core, same port" % per)
+        t1 = time.perf_counter()
+        run(order, p_of, gbm, cnt)
+        return cnt[0], time.perf_counter() - t1
+    ncore = n_core_leg(shard, list(range(cores)), "packets/s",
+                       "the same %d claims in every process (rotated), one process per core, same port"
+                       % len(sample)) if match else None
     return {"value": round(counter[0] / dt, 1), "unit": "packets/s", "cores": 1, "kind": "port", "cpu_model": model,
-            "sample": "%d of the step's claims (%d pairs hashed lazily, as the reference stops at the byte limit) "
-                      "through oracle/sync_ref.respond_arrays + oracle/bloom_ref (hashlib), %.1f s"
-                      % (len(sample), counter[0], dt),
-            "gpu_matches_cpu_on_sample": gpu == outs, "n_core": ncore}
+            "sample": "%s: the first %d of the step's claims, %d (claim, packet) pairs hashed lazily as the reference "
+                      "does (it stops at the packet that spends the %d B budget), through oracle/sync_ref.respond_arrays "
+                      "+ oracle/bloom_ref (hashlib), %.1f s" % (label, len(sample), counter[0], byte_limit, dt),
+            "pairs": counter[0], "seconds": round(dt, 2),
+            "gpu_matches_cpu_on_sample": match, "n_core": ncore}
 
 
 from dispersy_amd import _native  # noqa: E402  (module-level name used in cpu_baseline)

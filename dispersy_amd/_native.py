@@ -70,6 +70,8 @@ SIGNATURES = {
     "dsy_ctx_destroy": (ctypes.c_int, [_P]),
     "dsy_ctx_synchronize": (ctypes.c_int, [_P]),
     "dsy_ctx_stream": (_P, [_P]),
+    "dsy_ctx_wait_stream": (ctypes.c_int, [_P, _P]),
+    "dsy_ctx_signal_stream": (ctypes.c_int, [_P, _P]),
     "dsy_ctx_set_timing": (ctypes.c_int, [_P, ctypes.c_int]),
     "dsy_ctx_kernel_time": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), _PU64, _PU64, _PU64]),
     "dsy_ctx_reset_timing": (ctypes.c_int, [_P]),
@@ -104,6 +106,7 @@ SIGNATURES = {
     "dsy_sim_setup": (ctypes.c_int, [_P]),
     "dsy_sim_seed": (ctypes.c_int, [_P, _P, _P, _U32]),
     "dsy_sim_claim_counts": (ctypes.c_int, [_P, _P, _U32, _P, _U32]),
+    "dsy_sim_claim_matrix": (ctypes.c_int, [_P, _P, _U32, _U32, _P, _U32]),
     "dsy_sim_build_claims": (ctypes.c_int, [_P, _P, _U32, _P, _P, _P, _P, _P, _U32]),
     "dsy_sim_resp_counts": (ctypes.c_int, [_P, _P, _P, _U64, _P, _U32]),
     "dsy_sim_respond": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _U64, _P, _P, _U32, _PU64]),
@@ -187,6 +190,20 @@ class Context(object):
 
     def synchronize(self):
         check(self.lib.dsy_ctx_synchronize(self.handle))
+
+    @staticmethod
+    def _torch_stream(device):
+        import torch
+        return torch.cuda.current_stream(device).cuda_stream
+
+    def wait_torch(self, device=None):
+        """The ctx stream waits (on the device) for what is queued on torch's current stream: e.g. tensors torch
+        filled, or an RCCL collective's result."""
+        check(self.lib.dsy_ctx_wait_stream(self.handle, self._torch_stream(device)))
+
+    def signal_torch(self, device=None):
+        """Torch's current stream waits (on the device) for what is queued on the ctx stream."""
+        check(self.lib.dsy_ctx_signal_stream(self.handle, self._torch_stream(device)))
 
     def set_timing(self, on, only=None):
         """on: bracket kernel launches with HIP events; only: an iterable of TIME_* classes to bracket (default all)."""

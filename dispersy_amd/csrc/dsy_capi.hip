@@ -79,6 +79,13 @@ struct dsy_ctx {
     uint64_t window_cap = 0; // dsy_ctx_set_window: upper bound on the responder's window (0: the default 2^18)
     void* stage = nullptr;   // grow-only pinned staging of the responder's uploads and status read-backs
     size_t stage_bytes = 0;
+    hipStream_t aux = nullptr;  // dsy_sim_claim_matrix: work that depends on nothing queued on `stream`
+    hipEvent_t xev = nullptr;   // dsy_ctx_wait_stream / dsy_ctx_signal_stream
+    // the simulator's device-side counters (work of build / respond, pairs tested, response overflow): the calls
+    // enqueue without reading them back; the synchronising accessors fold them (sim_collect)
+    void* sim_acc = nullptr;
+    bool sim_pending = false;
+    bool sim_overflow = false;
 };
 
 struct dsy_store {
@@ -336,6 +343,41 @@ int run_bloom(dsy_ctx* c, BloomOp op, const dsy_bloom_params* p, const uint8_t* 
     return DSY_OK;
 }
 
+// the simulator's accumulators: [kSimTestedSlots][4] work (build blocks, build slots, respond blocks, respond slots),
+// [kSimTestedSlots] pairs tested, then the response-overflow flag
+constexpr size_t kSimAccWork = 32 * kSimTestedSlots, kSimAccTested = 8 * kSimTestedSlots;
+constexpr size_t kSimAccBytes = kSimAccWork + kSimAccTested + 16;
+
+int sim_acc_get(dsy_ctx* c, uint8_t** out) {
+    bool fresh = false;
+    void* d;
+    int rc = ws_get(c, "sim_acc", kSimAccBytes, &d, &fresh);
+    if (rc) return rc;
+    if (fresh) HIP_TRY(hipMemsetAsync(d, 0, kSimAccBytes, c->stream));
+    c->sim_acc = d;
+    c->sim_pending = true;
+    *out = (uint8_t*)d;
+    return DSY_OK;
+}
+
+// fold the simulator's device counters into the ctx totals (the stream must be idle)
+int sim_collect(dsy_ctx* c) {
+    if (!c->sim_pending || !c->sim_acc) return DSY_OK;
+    std::vector<uint64_t> h(kSimAccBytes / 8);
+    HIP_TRY(hipMemcpy(h.data(), c->sim_acc, kSimAccBytes, hipMemcpyDeviceToHost));
+    for (uint32_t i = 0; i < kSimTestedSlots; ++i) {
+        c->blocks[kTimeSimBuild] += h[4 * i];
+        c->slots[kTimeSimBuild] += h[4 * i + 1];
+        c->blocks[kTimeSimRespond] += h[4 * i + 2];
+        c->slots[kTimeSimRespond] += h[4 * i + 3];
+        c->useful[kTimeSimRespond] += h[kSimAccWork / 8 + i];
+    }
+    if (h[(kSimAccWork + kSimAccTested) / 8]) c->sim_overflow = true;
+    HIP_TRY(hipMemsetAsync(c->sim_acc, 0, kSimAccBytes, c->stream));
+    c->sim_pending = false;
+    return DSY_OK;
+}
+
 struct Guard {
     dsy_ctx* c;
     explicit Guard(dsy_ctx* c) : c(c) { c->mu.lock(); hipSetDevice(c->device); }
@@ -395,6 +437,8 @@ int dsy_ctx_destroy(dsy_ctx* c) {
         timers_collect(c);
         for (auto& kv : c->ws) if (kv.second.ptr) hipFree(kv.second.ptr);
         for (auto e : c->event_pool) hipEventDestroy(e);
+        if (c->xev) hipEventDestroy(c->xev);
+        if (c->aux) hipStreamDestroy(c->aux);
         if (c->pinned) hipHostFree(c->pinned);
         if (c->stage) hipHostFree(c->stage);
         hipStreamDestroy(c->stream);
@@ -408,10 +452,35 @@ int dsy_ctx_synchronize(dsy_ctx* c) {
     Guard g(c);
     HIP_TRY(hipStreamSynchronize(c->stream));
     timers_collect(c);
-    return DSY_OK;
+    return sim_collect(c);
 }
 
 void* dsy_ctx_stream(dsy_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+static int xev_get(dsy_ctx* c) {
+    if (!c->xev) HIP_TRY(hipEventCreateWithFlags(&c->xev, hipEventDisableTiming));
+    return DSY_OK;
+}
+
+int dsy_ctx_wait_stream(dsy_ctx* c, void* stream) {
+    if (!c) return fail(DSY_EINVAL, "ctx is NULL");
+    Guard g(c);
+    int rc = xev_get(c);
+    if (rc) return rc;
+    HIP_TRY(hipEventRecord(c->xev, (hipStream_t)stream));
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->xev, 0));
+    return DSY_OK;
+}
+
+int dsy_ctx_signal_stream(dsy_ctx* c, void* stream) {
+    if (!c) return fail(DSY_EINVAL, "ctx is NULL");
+    Guard g(c);
+    int rc = xev_get(c);
+    if (rc) return rc;
+    HIP_TRY(hipEventRecord(c->xev, c->stream));
+    HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, c->xev, 0));
+    return DSY_OK;
+}
 
 int dsy_ctx_set_timing(dsy_ctx* c, int enable) {
     if (!c) return fail(DSY_EINVAL, "ctx is NULL");
@@ -426,6 +495,8 @@ int dsy_ctx_kernel_time(dsy_ctx* c, int which, double* out_ms, uint64_t* out_lau
     Guard g(c);
     HIP_TRY(hipStreamSynchronize(c->stream));
     timers_collect(c);
+    int rc = sim_collect(c);
+    if (rc) return rc;
     if (out_ms) *out_ms = c->time_ms[which];
     if (out_launches) *out_launches = c->launches[which];
     if (out_blocks) *out_blocks = c->blocks[which];
@@ -438,6 +509,8 @@ int dsy_ctx_reset_timing(dsy_ctx* c) {
     Guard g(c);
     HIP_TRY(hipStreamSynchronize(c->stream));
     timers_collect(c);
+    int rc = sim_collect(c);
+    if (rc) return rc;
     for (int i = 0; i < kTimeClasses; ++i)
         c->time_ms[i] = 0, c->launches[i] = 0, c->blocks[i] = 0, c->bytes[i] = 0, c->useful[i] = 0, c->slots[i] = 0;
     return DSY_OK;
@@ -453,6 +526,11 @@ int dsy_ctx_set_window(dsy_ctx* c, uint64_t max_pairs) {
 int dsy_ctx_work(dsy_ctx* c, int which, uint64_t* out4) {
     if (!c || !out4 || which < 0 || which >= kTimeClasses) return fail(DSY_EINVAL, "bad ctx, output or class");
     Guard g(c);
+    if (c->sim_pending) {  // the simulator's counters live on the device until the stream is idle
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        int rc = sim_collect(c);
+        if (rc) return rc;
+    }
     out4[0] = c->blocks[which];
     out4[1] = c->bytes[which];
     out4[2] = c->useful[which];
@@ -1905,12 +1983,48 @@ int dsy_sim_claim_counts(dsy_ctx* c, const dsy_sim_config* cfg, uint32_t round, 
     return sim_counts(c, L, kSimClaimCounts, h_counts, n_ranks);
 }
 
-static int sim_cursor(dsy_ctx* c, const uint32_t* h_offsets, uint32_t n_ranks, uint32_t** out) {
+// the per-destination record cursors start at h_offsets[]: passed to a one-workgroup kernel by value (the host array
+// is pageable: a copy from it would wait for the stream)
+static int sim_cursor(dsy_ctx* c, const SimLaunch& base, const uint32_t* h_offsets, uint32_t n_ranks, uint32_t** out) {
     void* d;
     int rc;
     if ((rc = ws_get(c, "sim_cursor", 4 * std::max<uint32_t>(n_ranks, 1), &d))) return rc;
-    HIP_TRY(hipMemcpyAsync(d, h_offsets, 4 * n_ranks, hipMemcpyHostToDevice, c->stream));
+    if (n_ranks > kSimMaxRanks) {  // beyond one launch's argument: a staged copy (synchronous)
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(hipMemcpy(d, h_offsets, 4 * n_ranks, hipMemcpyHostToDevice));
+    } else {
+        SimLaunch L = base;
+        L.cursor_init.n = n_ranks;
+        for (uint32_t i = 0; i < n_ranks; ++i) L.cursor_init.start[i] = h_offsets[i];
+        L.cursor = (uint32_t*)d;
+        HIP_TRY(launch_sim(kSimCursorInit, L));
+    }
     *out = (uint32_t*)d;
+    return DSY_OK;
+}
+
+int dsy_sim_claim_matrix(dsy_ctx* c, const dsy_sim_config* cfg, uint32_t round0, uint32_t n_rounds, uint32_t* h_matrix,
+                         uint32_t n_ranks) {
+    if (!c || !h_matrix || !n_ranks || !n_rounds) return fail(DSY_EINVAL, "NULL argument");
+    int rc = sim_check(cfg);
+    if (rc) return rc;
+    if ((cfg->n_peers + cfg->peers_per_rank - 1) / cfg->peers_per_rank > n_ranks) return fail(DSY_EINVAL, "n_ranks too small");
+    if (n_rounds > 65535) return fail(DSY_EINVAL, "at most 65535 rounds per call");
+    Guard g(c);
+    if (!c->aux) HIP_TRY(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+    const size_t bytes = 4ull * n_rounds * n_ranks * n_ranks;
+    void* d;
+    if ((rc = ws_get(c, "sim_matrix", bytes, &d))) return rc;
+    HIP_TRY(hipMemsetAsync(d, 0, bytes, c->aux));
+    SimLaunch L = sim_launch(c, cfg);
+    L.stream = c->aux;
+    L.round = round0;
+    L.n_rounds = n_rounds;
+    L.n_ranks = n_ranks;
+    L.counts = (uint32_t*)d;
+    HIP_TRY(launch_sim(kSimClaimMatrix, L));
+    HIP_TRY(hipMemcpyAsync(h_matrix, d, bytes, hipMemcpyDeviceToHost, c->aux));
+    HIP_TRY(hipStreamSynchronize(c->aux));
     return DSY_OK;
 }
 
@@ -1927,26 +2041,18 @@ int dsy_sim_build_claims(dsy_ctx* c, const dsy_sim_config* cfg, uint32_t round, 
     L.uoff = d_uoff;
     L.bits = (uint32_t*)d_bits;
     L.out = d_out;
-    if ((rc = sim_cursor(c, h_offsets, n_ranks, &L.cursor))) return rc;
+    if ((rc = sim_cursor(c, L, h_offsets, n_ranks, &L.cursor))) return rc;
     void* ds;
     if ((rc = ws_get(c, "sim_slots", 4 * std::max<uint64_t>(cfg->peer_end - cfg->peer_begin, 1), &ds))) return rc;
     L.slots = (uint32_t*)ds;
     HIP_TRY(launch_sim(kSimClaimSlots, L));
-    void* dw;
-    if ((rc = ws_get(c, "sim_work", 32 * kSimTestedSlots, &dw))) return rc;
-    HIP_TRY(hipMemsetAsync(dw, 0, 32 * kSimTestedSlots, c->stream));
-    L.work = (unsigned long long*)dw;
+    uint8_t* acc;
+    if ((rc = sim_acc_get(c, &acc))) return rc;
+    L.work = (unsigned long long*)acc;
     PendingTimer t;
     timer_begin(c, &t, kTimeSimBuild);
     HIP_TRY(launch_sim(kSimBuild, L));
     timer_end(c, &t);
-    uint64_t* h = (uint64_t*)c->pinned + 256;
-    HIP_TRY(hipMemcpyAsync(h, dw, 32 * kSimTestedSlots, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    for (uint32_t i = 0; i < kSimTestedSlots; ++i) {
-        c->blocks[kTimeSimBuild] += h[4 * i];
-        c->slots[kTimeSimBuild] += h[4 * i + 1];
-    }
     timers_collect_lazy(c);
     return DSY_OK;
 }
@@ -1971,6 +2077,10 @@ int dsy_sim_respond(dsy_ctx* c, const dsy_sim_config* cfg, const uint8_t* d_ublo
     int rc = sim_check(cfg);
     if (rc) return rc;
     Guard g(c);
+    if (out_tested) {  // fold earlier calls first, so the count below is this call's alone
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if ((rc = sim_collect(c))) return rc;
+    }
     SimLaunch L = sim_launch(c, cfg);
     L.ublob = d_ublob;
     L.uoff = d_uoff;
@@ -1978,37 +2088,26 @@ int dsy_sim_respond(dsy_ctx* c, const dsy_sim_config* cfg, const uint8_t* d_ublo
     L.in = d_claims;
     L.n_in = n_claims;
     L.out = d_out;
-    void* dt;
-    if ((rc = ws_get(c, "sim_tested", 8 * kSimTestedSlots, &dt))) return rc;
-    HIP_TRY(hipMemsetAsync(dt, 0, 8 * kSimTestedSlots, c->stream));
-    L.tested = (unsigned long long*)dt;
-    if ((rc = sim_cursor(c, h_offsets, n_ranks, &L.cursor))) return rc;
+    if ((rc = sim_cursor(c, L, h_offsets, n_ranks, &L.cursor))) return rc;
     void* ds;
     if ((rc = ws_get(c, "sim_slots", 4 * std::max<uint64_t>(n_claims, 1), &ds))) return rc;
     L.slots = (uint32_t*)ds;
     HIP_TRY(launch_sim(kSimRespSlots, L));
-    void* dw;
-    if ((rc = ws_get(c, "sim_work", 32 * kSimTestedSlots, &dw))) return rc;
-    HIP_TRY(hipMemsetAsync(dw, 0, 32 * kSimTestedSlots, c->stream));
-    L.work = (unsigned long long*)dw;
+    uint8_t* acc;
+    if ((rc = sim_acc_get(c, &acc))) return rc;
+    L.work = (unsigned long long*)acc;
+    L.tested = (unsigned long long*)(acc + kSimAccWork);
     PendingTimer t;
     timer_begin(c, &t, kTimeSimRespond);
     HIP_TRY(launch_sim(kSimRespond, L));
     timer_end(c, &t);
-    uint64_t* h = (uint64_t*)c->pinned + 128;
-    uint64_t* hw = (uint64_t*)c->pinned + 256;
-    HIP_TRY(hipMemcpyAsync(h, dt, 8 * kSimTestedSlots, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(hw, dw, 32 * kSimTestedSlots, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
     timers_collect_lazy(c);
-    uint64_t tested = 0;
-    for (uint32_t i = 0; i < kSimTestedSlots; ++i) {
-        tested += h[i];
-        c->blocks[kTimeSimRespond] += hw[4 * i + 2];
-        c->slots[kTimeSimRespond] += hw[4 * i + 3];
+    if (out_tested) {  // the caller wants this call's count now: wait for it
+        const uint64_t before = c->useful[kTimeSimRespond];
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if ((rc = sim_collect(c))) return rc;
+        *out_tested = c->useful[kTimeSimRespond] - before;
     }
-    c->useful[kTimeSimRespond] += tested;
-    if (out_tested) *out_tested = tested;
     return DSY_OK;
 }
 
@@ -2021,15 +2120,10 @@ int dsy_sim_merge(dsy_ctx* c, const dsy_sim_config* cfg, uint32_t* d_bits, const
     L.bits = d_bits;
     L.in = d_resps;
     L.n_in = n_resps;
-    void* d;
-    if ((rc = ws_get(c, "sim_overflow", 16, &d))) return rc;
-    HIP_TRY(hipMemsetAsync(d, 0, 16, c->stream));
-    L.counts = (uint32_t*)d;
+    uint8_t* acc;
+    if ((rc = sim_acc_get(c, &acc))) return rc;
+    L.counts = (uint32_t*)(acc + kSimAccWork + kSimAccTested);  // sticky overflow flag, reported by dsy_sim_stats
     HIP_TRY(launch_sim(kSimMerge, L));
-    uint32_t* h = (uint32_t*)c->pinned + 48;
-    HIP_TRY(hipMemcpyAsync(h, d, 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    if (h[0]) return fail(DSY_ECAPACITY, "a response exceeded DSY_SIM_RESP_MAX packets (byte_limit / shortest packet too large)");
     return DSY_OK;
 }
 
@@ -2047,6 +2141,11 @@ int dsy_sim_stats(dsy_ctx* c, const dsy_sim_config* cfg, const uint32_t* d_bits,
     HIP_TRY(launch_sim(kSimStats, L));
     HIP_TRY(hipMemcpyAsync(out, d, 16, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if ((rc = sim_collect(c))) return rc;
+    if (c->sim_overflow) {
+        c->sim_overflow = false;
+        return fail(DSY_ECAPACITY, "a response exceeded DSY_SIM_RESP_MAX packets (byte_limit / shortest packet too large)");
+    }
     return DSY_OK;
 }
 

@@ -285,7 +285,15 @@ hipError_t launch_ingest_merge(const uint64_t* live_gt, const uint64_t* live_row
 static constexpr uint32_t kSimFilterWordsMax = 2048;  // m <= 65536 bits
 static constexpr uint32_t kSimRespMax = DSY_SIM_RESP_MAX;
 enum { kSimSeed = 0, kSimClaimCounts, kSimBuild, kSimRespCounts, kSimRespond, kSimMerge, kSimStats, kSimClaimSlots,
-       kSimRespSlots };
+       kSimRespSlots, kSimClaimMatrix, kSimCursorInit };
+static constexpr uint32_t kSimMaxRanks = 64;  // cursor starts travel as a kernel argument up to this many ranks
+
+// the per-destination record cursors of a build / respond call, passed by value (no host-to-device copy of
+// pageable memory, which would wait for the stream)
+struct SimCursorInit {
+    uint32_t n;
+    uint32_t start[kSimMaxRanks];
+};
 static constexpr uint32_t kSimTestedSlots = 64;  // k_sim_respond spreads its tested-pair counter over 64 words
 
 struct SimLaunch {
@@ -305,6 +313,9 @@ struct SimLaunch {
     unsigned long long* stats;
     unsigned long long* work;  // [kSimTestedSlots][4]: build blocks, build lane-block slots, respond blocks, respond slots
     int or_mode;               // claim filter build: filter_set_all OR_MODE (dsy_message.h)
+    uint32_t n_rounds;         // kSimClaimMatrix: rounds round .. round + n_rounds - 1
+    uint32_t n_ranks;          // kSimClaimMatrix: matrix side
+    SimCursorInit cursor_init; // kSimCursorInit
     hipStream_t stream;
 };
 

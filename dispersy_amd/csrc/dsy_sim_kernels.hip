@@ -108,6 +108,21 @@ __global__ void k_sim_claim_counts(dsy_sim_config c, uint32_t round, uint32_t* _
     wave_count(counts, active ? sim_owner(c, sim_partner(c, round, c.peer_begin + lp)) : 0u, active);
 }
 
+// the round's whole claim traffic: m[r][src][dst] = claims the requesters of rank src send to responders of rank dst,
+// for n_rounds rounds from round0 (grid.y = rounds).  Every rank computes the same matrix from the counter RNG, so
+// the exchange needs no count all-to-all: a rank's send counts are its row, its receive counts its column.
+__global__ void k_sim_claim_matrix(dsy_sim_config c, uint32_t round0, uint32_t n_ranks, uint32_t* __restrict__ m) {
+    const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t r = blockIdx.y;
+    const bool active = p < c.n_peers;
+    const uint32_t key = active ? sim_owner(c, p) * n_ranks + sim_owner(c, sim_partner(c, round0 + r, p)) : 0u;
+    wave_count(m + (uint64_t)r * n_ranks * n_ranks, key, active);
+}
+
+__global__ void k_sim_cursor_init(SimCursorInit ci, uint32_t* __restrict__ cursor) {
+    if (threadIdx.x < ci.n) cursor[threadIdx.x] = ci.start[threadIdx.x];
+}
+
 // slot of every local requester's claim record: cursor[dest] starts at the destination's first record
 __global__ void k_sim_claim_slots(dsy_sim_config c, uint32_t round, uint32_t* __restrict__ cursor,
                                   uint32_t* __restrict__ slots) {
@@ -510,6 +525,14 @@ hipError_t launch_sim(int op, const SimLaunch& L) {
             return hipGetLastError();
         case kSimMerge:
             if (L.n_in) hipLaunchKernelGGL(k_sim_merge, dim3((uint32_t)((L.n_in + 255) / 256)), dim3(256), 0, L.stream, c, L.bits, L.in, L.n_in, L.counts);
+            return hipGetLastError();
+        case kSimClaimMatrix:
+            if (c.n_peers && L.n_rounds)
+                hipLaunchKernelGGL(k_sim_claim_matrix, dim3((uint32_t)((c.n_peers + 255) / 256), L.n_rounds), dim3(256), 0,
+                                   L.stream, c, L.round, L.n_ranks, L.counts);
+            return hipGetLastError();
+        case kSimCursorInit:
+            hipLaunchKernelGGL(k_sim_cursor_init, dim3(1), dim3(kSimMaxRanks), 0, L.stream, L.cursor_init, L.cursor);
             return hipGetLastError();
         case kSimStats:
             if (local) hipLaunchKernelGGL(k_sim_stats, dim3((uint32_t)((local + 255) / 256)), dim3(256), 0, L.stream, c, L.bits, L.stats);

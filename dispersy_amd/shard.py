@@ -81,18 +81,20 @@ class Collectives(object):
 
 def union_filter(ctx, coll, partial):
     """The OR of every rank's partial filter (int32 words on the device), on every rank: all-gather of the partials,
-    then dsy_filter_or_reduce on the GPU."""
+    then dsy_filter_or_reduce on the GPU.  The ctx stream and torch's stream (which the collective is ordered on)
+    are chained by device events, both ways: the result is ready for torch work queued after the call."""
     import torch
     words = partial.numel()
     if coll is None or coll.world == 1:
+        ctx.signal_torch(partial.device)  # the ctx kernels that built `partial` come first
         return partial.clone()
-    ctx.synchronize()
+    ctx.signal_torch(partial.device)
     parts = torch.empty(coll.world * words, dtype=torch.int32, device=partial.device)
     coll.all_gather_into(parts, partial)
-    torch.cuda.current_stream(partial.device).synchronize()
     union = torch.empty_like(partial)
+    ctx.wait_torch(partial.device)
     _native.check(ctx.lib.dsy_filter_or_reduce(ctx.handle, parts.data_ptr(), coll.world, words, union.data_ptr()))
-    ctx.synchronize()
+    ctx.signal_torch(partial.device)
     return union
 
 
@@ -103,6 +105,7 @@ def add_sharded(ctx, params, blob, offsets, n, coll, filt):
     import ctypes
     rank, world = (coll.rank, coll.world) if coll is not None else (0, 1)
     lo, hi = shard_range(n, rank, world)
+    ctx.wait_torch(filt.device)  # torch work that filled or zeroed blob / offsets / filt comes first
     if hi > lo:
         _native.check(ctx.lib.dsy_bloom_add_dev(ctx.handle, ctypes.byref(params), blob.data_ptr(),
                                                 offsets[lo:].data_ptr(), hi - lo, filt.data_ptr()))

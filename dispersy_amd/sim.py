@@ -64,7 +64,11 @@ def make_universe(universe, seed=11, lo=100, hi=1500):
 
 
 class GpuEngine(object):
-    """Per-rank simulator state in HBM + the dsy_sim_* kernels."""
+    """Per-rank simulator state in HBM + the dsy_sim_* kernels.  A round's calls only enqueue on the ctx stream (no
+    host wait); the claim / response buffers are the engine's own, grow-only, reused every round, so no buffer a
+    queued kernel still reads is ever handed back to torch's allocator."""
+
+    MATRIX_ROUNDS = 16  # claim matrices computed per dsy_sim_claim_matrix call
 
     def __init__(self, cfg, blob, offsets, device, ctx=None):
         import torch
@@ -81,9 +85,18 @@ class GpuEngine(object):
         self.uoff_t = torch.from_numpy(offsets.astype(np.int64)).to(device)
         local = cfg.peer_end - cfg.peer_begin
         self.bits = torch.zeros(max(local, 1) * cfg.words, dtype=torch.int32, device=device)
+        torch.cuda.current_stream(device).synchronize()  # the uploads above ran on torch's stream
+        self._bufs = {}
+        self._matrix = {}
 
-    def empty(self, nbytes):
-        return self.torch.empty(max(nbytes, 1), dtype=self.torch.uint8, device=self.dev)
+    def buffer(self, name, nbytes):
+        """The engine's grow-only device buffer `name`, at least nbytes long (a view of exactly nbytes)."""
+        b = self._bufs.get(name)
+        if b is None or b.numel() < nbytes:
+            if b is not None:
+                self.ctx.synchronize()  # queued kernels may still use the old one
+            b = self._bufs[name] = self.torch.empty(max(int(nbytes * 1.25), 1), dtype=self.torch.uint8, device=self.dev)
+        return b[:max(nbytes, 1)]
 
     def seed(self, initial):
         _native.check(self.lib.dsy_sim_seed(self.ctx.handle, ctypes.byref(self.cfg), self.bits.data_ptr(), initial))
@@ -94,8 +107,21 @@ class GpuEngine(object):
         _native.check(self.lib.dsy_sim_claim_counts(self.ctx.handle, ctypes.byref(self.cfg), rnd, out, world))
         return np.array(out, dtype=np.int64)
 
-    def build_claims(self, rnd, offsets, total):
-        buf = self.empty(total * self.cfg.claim_bytes)
+    def claim_matrix(self, rnd, world):
+        """[src, dst] claims of round rnd, every rank (dsy_sim_claim_matrix: one call per MATRIX_ROUNDS rounds, on a
+        second stream, so it does not wait for the queued rounds)."""
+        key = (rnd, world)
+        if key not in self._matrix:
+            n = self.MATRIX_ROUNDS
+            out = np.zeros(n * world * world, dtype=np.uint32)
+            _native.check(self.lib.dsy_sim_claim_matrix(self.ctx.handle, ctypes.byref(self.cfg), rnd, n,
+                                                        out.ctypes.data, world))
+            self._matrix = {(rnd + i, world): out[i * world * world:(i + 1) * world * world].reshape(world, world)
+                            .astype(np.int64) for i in range(n)}
+        return self._matrix[key]
+
+    def build_claims(self, rnd, offsets, total, buf=None):
+        buf = self.buffer("claims", total * self.cfg.claim_bytes) if buf is None else buf
         offs = (ctypes.c_uint32 * len(offsets))(*[int(x) for x in offsets])
         _native.check(self.lib.dsy_sim_build_claims(self.ctx.handle, ctypes.byref(self.cfg), rnd, self.ublob,
                                                     self.uoff_t.data_ptr(), self.bits.data_ptr(), buf.data_ptr(),
@@ -108,14 +134,18 @@ class GpuEngine(object):
                                                    out, world))
         return np.array(out, dtype=np.int64)
 
-    def respond(self, claims, n, offsets, total):
-        buf = self.empty(total * self.cfg.resp_bytes)
+    def respond(self, claims, n, offsets, total, buf=None):
+        """(response buffer, None): the pairs tested stay on the device (tested_total)."""
+        buf = self.buffer("resps", total * self.cfg.resp_bytes) if buf is None else buf
         offs = (ctypes.c_uint32 * len(offsets))(*[int(x) for x in offsets])
-        tested = ctypes.c_uint64()
         _native.check(self.lib.dsy_sim_respond(self.ctx.handle, ctypes.byref(self.cfg), self.ublob,
                                                self.uoff_t.data_ptr(), self.bits.data_ptr(), claims.data_ptr(), n,
-                                               buf.data_ptr(), offs, len(offsets), ctypes.byref(tested)))
-        return buf, tested.value
+                                               buf.data_ptr(), offs, len(offsets), None))
+        return buf, None
+
+    def tested_total(self):
+        """(claim, packet) pairs tested since the ctx's timing counters were last reset."""
+        return int(self.ctx.work(_native.TIME_SIM_RESPOND)["useful_pairs"])
 
     def merge(self, resps, n):
         _native.check(self.lib.dsy_sim_merge(self.ctx.handle, ctypes.byref(self.cfg), self.bits.data_ptr(),
@@ -126,64 +156,76 @@ class GpuEngine(object):
         _native.check(self.lib.dsy_sim_stats(self.ctx.handle, ctypes.byref(self.cfg), self.bits.data_ptr(), out))
         return int(out[0]), int(out[1])
 
+    def to_torch(self):
+        """torch's current stream (RCCL's collectives are ordered on it) waits for the queued kernels."""
+        self.ctx.signal_torch(self.dev)
+
+    def from_torch(self):
+        """The ctx stream waits for torch's current stream (a collective's output)."""
+        self.ctx.wait_torch(self.dev)
+
     def sync(self):
         self.ctx.synchronize()
 
 
 class EpidemicSim(object):
-    """Drives the rounds on one rank; `dist` is torch.distributed (or None for a single process)."""
+    """Drives the rounds on one rank; `dist` is torch.distributed (or None for a single process).
+
+    A round on rank q: the claim matrix M (computed identically on every rank, no count exchange) gives the send
+    counts M[q] and receive counts M[:, q]; build -> all-to-all(v) of the claims -> respond -> all-to-all(v) of the
+    responses (one per claim, so the counts reverse) -> merge.  The host never waits inside a round: the engine's
+    kernels and the collectives are ordered on the device (to_torch / from_torch events around each exchange)."""
 
     def __init__(self, engine, cfg, rank=0, world=1, dist=None, device=None):
         self.e, self.cfg, self.rank, self.world, self.dist = engine, cfg, rank, world, dist
         self.coll = Collectives(dist) if dist is not None and world > 1 else None
         self.device = device
-        self.tested = 0
+        self._tested = 0
         self.exchanged_bytes = 0
 
-    def _alltoall_counts(self, counts):
-        if self.world == 1:
-            return counts.copy()
-        import torch
-        send = torch.tensor(counts, dtype=torch.int64, device=self.device)
-        recv = torch.empty_like(send)
-        self.coll.all_to_all_single(recv, send)
-        return recv.cpu().numpy()
+    @property
+    def tested(self):
+        if hasattr(self.e, "tested_total"):
+            return self.e.tested_total()
+        return self._tested
 
-    def _alltoall_records(self, buf, send_counts, recv_counts, rec_bytes):
+    def _exchange(self, name, buf, send_counts, recv_counts, rec_bytes):
         if self.world == 1:
             return buf
-        import torch
-        self.e.sync()
-        out = torch.empty(max(int(recv_counts.sum()) * rec_bytes, 1), dtype=torch.uint8, device=self.device)
         in_splits = [int(c) * rec_bytes for c in send_counts]
         out_splits = [int(c) * rec_bytes for c in recv_counts]
-        if sum(in_splits) == 0:
-            buf = buf[:0]
+        total_in = sum(out_splits)
+        if hasattr(self.e, "buffer"):
+            out = self.e.buffer(name, total_in)
         else:
-            buf = buf[:sum(in_splits)]
-        self.coll.all_to_all_single(out[:sum(out_splits)] if sum(out_splits) else out[:0], buf, out_splits, in_splits)
-        if self.device is not None and self.device.type == "cuda":
-            torch.cuda.current_stream(self.device).synchronize()
+            import torch
+            out = torch.empty(max(total_in, 1), dtype=torch.uint8, device=self.device)
+        to_torch, from_torch = getattr(self.e, "to_torch", None), getattr(self.e, "from_torch", None)
+        if to_torch:
+            to_torch()
+        self.coll.all_to_all_single(out[:total_in], buf[:sum(in_splits)], out_splits, in_splits)
+        if from_torch:
+            from_torch()
         self.exchanged_bytes += sum(in_splits)
         return out
 
     def round(self, rnd):
         c = self.cfg
-        counts = self.e.claim_counts(rnd, self.world)
+        M = self.e.claim_matrix(rnd, self.world)
+        counts = M[self.rank]
+        rcounts = M[:, self.rank]
         offs = np.concatenate([[0], np.cumsum(counts)[:-1]])
         claims = self.e.build_claims(rnd, offs, int(counts.sum()))
-        rcounts = self._alltoall_counts(counts)
-        claims_in = self._alltoall_records(claims, counts, rcounts, c.claim_bytes)
+        claims_in = self._exchange("claims_in", claims, counts, rcounts, c.claim_bytes)
         n_in = int(rcounts.sum())
-        pcounts = self.e.resp_counts(claims_in, n_in, self.world)
-        poffs = np.concatenate([[0], np.cumsum(pcounts)[:-1]])
-        resps, tested = self.e.respond(claims_in, n_in, poffs, int(pcounts.sum()))
-        self.tested += tested
-        # every claim gets exactly one response record, so the responses rank d returns are the claims sent to d:
-        # no count exchange is needed on the way back
-        back = counts
-        resps_in = self._alltoall_records(resps, pcounts, back, c.resp_bytes)
-        self.e.merge(resps_in, int(back.sum()))
+        # every received claim gets exactly one response record, grouped by the requester's rank: what goes back to
+        # rank d is what came from d, so the response counts are the claim counts reversed
+        poffs = np.concatenate([[0], np.cumsum(rcounts)[:-1]])
+        resps, tested = self.e.respond(claims_in, n_in, poffs, n_in)
+        if tested is not None:
+            self._tested += tested
+        resps_in = self._exchange("resps_in", resps, rcounts, counts, c.resp_bytes)
+        self.e.merge(resps_in, int(counts.sum()))
 
     def global_stats(self):
         held, chk = self.e.stats()

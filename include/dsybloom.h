@@ -107,6 +107,12 @@ int dsy_ctx_destroy(dsy_ctx* ctx);
 int dsy_ctx_synchronize(dsy_ctx* ctx);
 /* The HIP stream (hipStream_t) the ctx enqueues on. */
 void* dsy_ctx_stream(dsy_ctx* ctx);
+/* Cross-stream ordering without a host wait (one event each): dsy_ctx_wait_stream makes the ctx stream wait for the
+ * work enqueued so far on `stream` (e.g. torch's current stream, which an RCCL collective's completion is ordered
+ * on); dsy_ctx_signal_stream makes `stream` wait for the work enqueued so far on the ctx stream.  stream may be
+ * NULL (the null stream). */
+int dsy_ctx_wait_stream(dsy_ctx* ctx, void* stream);
+int dsy_ctx_signal_stream(dsy_ctx* ctx, void* stream);
 /* Kernel timing: when enabled, HIP events bracket every launch of the hash kernels on the ctx stream.
  * dsy_ctx_kernel_time returns the accumulated milliseconds and launch count of kernel class `which`
  * (0 = hash/test of the responder, 1 = single-filter bloom kernels, 2 = selection, 3 = compaction, 4 = the
@@ -310,7 +316,10 @@ int dsy_sync_encode(const dsy_request* reqs, uint32_t n, const uint8_t* filters,
  * responder = _get_packets_for_bloomfilters + the byte-limited loop (community.py:2555-2567), then the requester
  * stores what it got.  Peers are block-sharded over ranks; claims and responses are fixed-size records the host
  * exchanges between ranks (RCCL all-to-all(v)).  Stores are bitsets over a universe of packets whose global time
- * is index + 1.  All buffers are device pointers; count queries synchronise the ctx stream. */
+ * is index + 1.  All buffers are device pointers.  build_claims, respond (out_tested NULL) and merge enqueue
+ * without waiting: their work counters stay on the device until a synchronising accessor (dsy_ctx_synchronize,
+ * _kernel_time, _work, dsy_sim_stats) folds them, and a response overflow is reported by the next dsy_sim_stats.
+ * The count queries (claim_counts, resp_counts, claim_matrix) return host values and wait for what they need. */
 #define DSY_SIM_RESP_MAX 64
 
 typedef struct dsy_sim_config {
@@ -345,13 +354,20 @@ int dsy_sim_setup(dsy_sim_config* cfg);
 int dsy_sim_seed(dsy_ctx* ctx, const dsy_sim_config* cfg, uint32_t* d_bits, uint32_t initial);
 /* claims this rank's requesters send to each rank in `round` (h_counts[n_ranks]) */
 int dsy_sim_claim_counts(dsy_ctx* ctx, const dsy_sim_config* cfg, uint32_t round, uint32_t* h_counts, uint32_t n_ranks);
+/* The claim traffic of n_rounds rounds from round0, all ranks: h_matrix[r][src][dst] (n_rounds x n_ranks x n_ranks)
+ * = claims the requesters of rank src send to rank dst in round round0 + r.  Pairing is a counter RNG, so every rank
+ * computes the same matrix and needs no count exchange.  Runs on a second stream of the ctx: it waits only for itself,
+ * not for the work queued on the ctx stream. */
+int dsy_sim_claim_matrix(dsy_ctx* ctx, const dsy_sim_config* cfg, uint32_t round0, uint32_t n_rounds,
+                         uint32_t* h_matrix, uint32_t n_ranks);
 /* build the claim records into d_out, grouped by destination rank at h_offsets[dest] (records, exclusive scan) */
 int dsy_sim_build_claims(dsy_ctx* ctx, const dsy_sim_config* cfg, uint32_t round, const uint8_t* d_ublob,
                          const uint64_t* d_uoff, const uint32_t* d_bits, uint8_t* d_out, const uint32_t* h_offsets,
                          uint32_t n_ranks);
 int dsy_sim_resp_counts(dsy_ctx* ctx, const dsy_sim_config* cfg, const uint8_t* d_claims, uint64_t n_claims,
                         uint32_t* h_counts, uint32_t n_ranks);
-/* answer the received claims (responders are this rank's peers); responses grouped by the requester's rank */
+/* answer the received claims (responders are this rank's peers); responses grouped by the requester's rank at
+ * h_offsets[rank].  out_tested (may be NULL: no wait) receives the (claim, packet) pairs this call tested. */
 int dsy_sim_respond(dsy_ctx* ctx, const dsy_sim_config* cfg, const uint8_t* d_ublob, const uint64_t* d_uoff,
                     const uint32_t* d_bits, const uint8_t* d_claims, uint64_t n_claims, uint8_t* d_out,
                     const uint32_t* h_offsets, uint32_t n_ranks, uint64_t* out_tested);

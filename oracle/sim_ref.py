@@ -79,6 +79,13 @@ class OracleEngine(object):
             out[owner(self.c, partner(self.c, rnd, self.c.peer_begin + lp))] += 1
         return out
 
+    def claim_matrix(self, rnd, world):
+        """[src, dst] claims of round rnd over every peer (dsy_sim_claim_matrix)."""
+        out = np.zeros((world, world), dtype=np.int64)
+        for p in range(self.c.n_peers):
+            out[owner(self.c, p), owner(self.c, partner(self.c, rnd, p))] += 1
+        return out
+
     def build_claims(self, rnd, offsets, total):
         c = self.c
         buf = bytearray(max(total, 1) * c.claim_bytes)

@@ -74,3 +74,29 @@ def test_cfg3_sim_two_ranks_equal_one(two_ranks):
     assert r0["cfg3"]["history"] == r1["cfg3"]["history"]
     assert r0["cfg3"]["history"][-1][0] > r0["cfg3"]["history"][0][0]
     assert r0["cfg3"]["exchanged_bytes"] > 0 and r1["cfg3"]["exchanged_bytes"] > 0
+
+
+def test_cfg4_one_rank_add_sharded_equals_single_build():
+    """The world == 1 path of add_sharded / union_filter (no collective): the filter torch zeroed is built on the
+    ctx stream and cloned on torch's stream, ordered by device events both ways."""
+    import numpy as np
+    import torch
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    from dispersy_amd import BloomFilter, _native
+    from dispersy_amd.shard import add_sharded
+    from keys import random_packets
+    dev = torch.device("cuda", 0)
+    ctx = _native.default_context()
+    blob, offs = random_packets(78, 30_000, 60, 1500)
+    G = _native.BLOB_GUARD
+    d_blob = torch.zeros(len(blob) + 2 * G, dtype=torch.uint8, device=dev)
+    d_blob[G:G + len(blob)] = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
+    d_offs = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    for m, f, prefix in [(10160, 0.01, b"\x00\x01\x02\x03"), (1 << 20, 0.01, b"\x07")]:
+        bf = BloomFilter(m, f, prefix)
+        filt = torch.full((int(ctx.lib.dsy_filter_words(m)),), -1, dtype=torch.int32, device=dev)
+        filt.zero_()  # queued on torch's stream right before the build
+        union = add_sharded(ctx, bf.params, d_blob[G:], d_offs, len(offs) - 1, None, filt)
+        whole = BloomFilter(m, f, prefix)
+        whole.add_packed(blob, offs)
+        assert union.cpu().numpy().tobytes()[:m // 8] == whole.bytes

@@ -67,3 +67,18 @@ def test_sim_config_matches_community_filter():
     assert (cfg.m_bits, cfg.k, cfg.hash_kind, cfg.chunk_bytes) == (10160, 7, 0, 2)  # MD5 MTU filter
     assert cfg.capacity == 1059
     assert cfg.peers_per_rank == 125_000 and cfg.peer_end == 125_000
+
+
+def test_claim_matrix_rows_are_each_ranks_counts():
+    """Every rank computes the same [src, dst] matrix (dsy_sim_claim_matrix restated): row r is what rank r's
+    claim_counts returns, column r what it receives, so the exchange needs no count all-to-all."""
+    blob, offs = make_universe(50, seed=3)
+    for world in (1, 2, 3):
+        engs = [OracleEngine(make_config(P, 50, r, world, bits=2048, seed=5), blob, offs) for r in range(world)]
+        for rnd in range(3):
+            mats = [e.claim_matrix(rnd, world) for e in engs]
+            for m in mats[1:]:
+                assert (m == mats[0]).all()
+            for r, e in enumerate(engs):
+                assert (mats[0][r] == e.claim_counts(rnd, world)).all()
+            assert int(mats[0].sum()) == P

@@ -59,11 +59,20 @@ def test_two_rank_routing_in_one_process():
     for rnd in range(ROUNDS):
         ss.round(rnd)
         counts = [e.claim_counts(rnd, 2) for e in engs]
+        # the matrix every rank computes for itself holds each rank's send counts as its row
+        for e in engs:
+            assert (e.claim_matrix(rnd, 2) == np.stack(counts)).all()
         bufs = [e.build_claims(rnd, np.concatenate([[0], np.cumsum(c)[:-1]]), int(c.sum())) for e, c in zip(engs, counts)]
+        for e in engs:  # the calls only enqueue on each engine's stream; the hand-made exchange below runs on torch's
+            e.sync()
         claims_in, n_in = exchange(bufs, counts, cfgs[0].claim_bytes)
         pcounts = [e.resp_counts(ci, n, 2) for e, ci, n in zip(engs, claims_in, n_in)]
+        # one response per claim: the counts going back are the received claims' counts by source rank
+        assert [list(pc) for pc in pcounts] == [[int(counts[r][d]) for r in range(2)] for d in range(2)]
         rbufs = [e.respond(ci, n, np.concatenate([[0], np.cumsum(pc)[:-1]]), int(pc.sum()))[0]
                  for e, ci, n, pc in zip(engs, claims_in, n_in, pcounts)]
+        for e in engs:
+            e.sync()
         resps_in, r_in = exchange(rbufs, pcounts, cfgs[0].resp_bytes)
         for e, ri, n in zip(engs, resps_in, r_in):
             e.merge(ri, n)
