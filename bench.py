@@ -175,6 +175,8 @@ def parse():
     ap.add_argument("--cpu-pairs", type=int, default=100_000,
                     help="responder CPU baselines: (claim, packet) pairs hashed in the 1-core sample (BASELINE.md:47)")
     ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="responder legs: 1 serve the batches two in flight (submit / wait), 0 one at a time")
     ap.add_argument("--window", type=int, default=0, help="cap on the responder's window (pairs per claim; 0: default)")
     ap.add_argument("--sim-peers", type=int, default=1_000_000, help="config 3 gossip simulator peers (0: skip)")
     ap.add_argument("--sim-universe", type=int, default=10_000)
@@ -263,45 +265,40 @@ def run(args, rank, world, local):
     metas = (_native.Meta * 1)()
     metas[0].meta_id, metas[0].direction = 1, _native.DSY_ASC
 
-    p_out, p_off, pairs = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
     if args.window:
         ctx.set_window(args.window)
+    batches = Batches(lib, ctx, store, reqs, R, d_filters.data_ptr(), metas, 1, N, args.byte_limit)
+    pipe = bool(args.pipeline)
+    step = batches.step
 
-    # the call's arguments built once (the claims and filters are the same every step; the library re-reads them)
-    respond_args = (ctx.handle, store, reqs, R, d_filters.data_ptr(), metas, 1, N, 0, args.byte_limit, 99,
-                    ctypes.byref(p_out), ctypes.byref(p_off), ctypes.byref(pairs))
-    respond_dev = lib.dsy_sync_respond_dev
-
-    def step():
-        _native.check(respond_dev(*respond_args))
-
-    for _ in range(args.warmup):
-        step()
+    batches.run(args.warmup, pipe)
     ctx.synchronize()
     ctx.reset_timing()
-    ctx.set_timing(True, only=[_native.TIME_PAIR_TEST])  # events around the dominant kernel only
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    total_pairs = 0
-    for _ in range(args.steps):
-        step()
-        total_pairs += pairs.value
+    total_pairs = batches.run(args.steps, pipe)
     ctx.synchronize()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    work = ctx.work(_native.TIME_PAIR_TEST)
+    # the dominant kernel's launches timed by HIP events in a serial pass (one batch at a time: with two batches in
+    # flight a launch's events would also span the other batch's kernels), then the selection / compaction kernels'
+    # times from a few more steps; all outside the timed region
+    ctx.reset_timing()
+    ctx.set_timing(True, only=[_native.TIME_PAIR_TEST])
+    t1 = time.perf_counter()
+    serial_pairs = batches.run(args.steps, False)
+    serial_s = time.perf_counter() - t1
     ctx.set_timing(False)
     kt = ctx.kernel_time(_native.TIME_PAIR_TEST)
-    # the selection / compaction kernels' times from a few extra steps outside the timed region
-    work = ctx.work(_native.TIME_PAIR_TEST)
     ctx.reset_timing()
     ctx.set_timing(True, only=[_native.TIME_SELECT, _native.TIME_COMPACT])
     n_side = min(max(args.steps, 1), 5)
-    for _ in range(n_side):
-        step()
+    batches.run(n_side, False)
     ctx.synchronize()
     ctx.set_timing(False)
     sel = ctx.kernel_time(_native.TIME_SELECT)
@@ -310,11 +307,12 @@ def run(args, rank, world, local):
         coll = Collectives(dist)
         elapsed = float(coll.scalar(elapsed, "max", device=dev))
         total_pairs = int(coll.scalar(int(total_pairs), "sum", device=dev))
+        serial_s = float(coll.scalar(serial_s, "max", device=dev))
 
     # ---------------------------------------------------------------- roofline of the dominant kernel
     launches = max(kt["launches"], 1)
     avg_s = kt["ms"] / 1e3 / launches
-    pairs_per_launch = total_pairs / max(args.steps, 1) / max(world, 1)
+    pairs_per_launch = serial_pairs / max(args.steps, 1)
     blocks_per_launch = kt["blocks"] / launches
     bytes_per_launch = kt["bytes"] / launches + pairs_per_launch * 17  # packet bytes + 16 B task record + miss flag
     hash_name = cap_probe.hash_name
@@ -376,7 +374,7 @@ def run(args, rank, world, local):
     if "dedup" in extra:
         dedup = dedup_bench(args, ctx, lib, store, blob, offsets, N, cpu_leg=rank == 0 and world == 1)
     if "ingest" in extra:
-        ingest = ingest_bench(args, ctx, lib, store, step, pairs, N, cpu_leg=rank == 0 and world == 1)
+        ingest = ingest_bench(args, ctx, lib, store, step, N, cpu_leg=rank == 0 and world == 1)
 
     gossip = None
     if "3" in extra and args.sim_peers > 0:
@@ -417,6 +415,9 @@ def run(args, rank, world, local):
             "value_counts": "(claim, packet) pairs the reference hashes+tests for these claims: its lazy not_filter "
                             "stops at the packet that spends the 5 KiB budget (community.py:2559-2567)",
             "pairs_hashed_per_s": round(total_pairs / elapsed, 1),
+            "pipeline": "two batches in flight (dsy_sync_respond_submit / _wait): one batch's selection and the host's "
+                        "staging overlap the other's hashing" if pipe else "one batch at a time (dsy_sync_respond_dev)",
+            "serial_ms_per_step": round(serial_s / max(args.steps, 1) * 1e3, 3),
             "claims_per_s": round(R * world * args.steps / elapsed, 1),
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -437,6 +438,46 @@ def run(args, rank, world, local):
         dist.destroy_process_group()
 
 
+class Batches(object):
+    """One batch of R claims served again and again by the responder: step() is the synchronous call
+    (dsy_sync_respond_dev); run(k, pipeline) serves k batches, two in flight when pipelined (dsy_sync_respond_submit /
+    dsy_sync_respond_wait: batch i+1 is staged and its first window's selection queued before batch i is waited for),
+    and returns the (claim, packet) pairs hashed."""
+
+    def __init__(self, lib, ctx, store, reqs, R, d_filters, metas, J, global_time, byte_limit, seed=99):
+        self.lib, self.h = lib, ctx.handle
+        self.p_out, self.p_off, self.pairs, self.ticket = (ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64(),
+                                                           ctypes.c_uint64())
+        self.sync_args = (ctx.handle, store, reqs, R, d_filters, metas, J, global_time, 0, byte_limit, seed,
+                          ctypes.byref(self.p_out), ctypes.byref(self.p_off), ctypes.byref(self.pairs))
+        self.sub_args = (ctx.handle, store, reqs, R, d_filters, metas, J, global_time, 0, byte_limit, seed,
+                         ctypes.byref(self.ticket))
+        self.wait_tail = (ctypes.byref(self.p_out), ctypes.byref(self.p_off), ctypes.byref(self.pairs))
+
+    def step(self):
+        _native.check(self.lib.dsy_sync_respond_dev(*self.sync_args))
+        return self.pairs.value
+
+    def submit(self):
+        _native.check(self.lib.dsy_sync_respond_submit(*self.sub_args))
+        return self.ticket.value
+
+    def wait(self, ticket):
+        _native.check(self.lib.dsy_sync_respond_wait(self.h, ticket, *self.wait_tail))
+        return self.pairs.value
+
+    def run(self, k, pipeline=True):
+        if not pipeline:
+            return sum(self.step() for _ in range(k))
+        total = 0
+        pending = self.submit() if k else None
+        for i in range(k):
+            nxt = self.submit() if i + 1 < k else None
+            total += self.wait(pending)
+            pending = nxt
+        return total
+
+
 def sha1_respond(args, ctx, lib, store, N, dev, blob, offsets, total_bytes, metas, rank, world, dist):
     """The headline step with SHA-1 claim filters: BloomFilter(512 * 8, 0.001, prefix="x") -- the filter the
     reference's own test node puts in every introduction request (tests/debugcommunity/node.py:617), k = 10, SHA-1
@@ -446,36 +487,32 @@ def sha1_respond(args, ctx, lib, store, N, dev, blob, offsets, total_bytes, meta
     rng = np.random.Generator(np.random.PCG64(args.seed + 1 + 1000 * rank))
     R = args.claims
     reqs, claims, fblob, d_filters, capacity = make_claims(ctx, lib, store, N, R, rng, 512 * 8, 0.001, b"x", dev)
-    p_out, p_off, pairs = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
-
-    # the call's arguments built once (the claims and filters are the same every step; the library re-reads them)
-    respond_args = (ctx.handle, store, reqs, R, d_filters.data_ptr(), metas, 1, N, 0, args.byte_limit, 99,
-                    ctypes.byref(p_out), ctypes.byref(p_off), ctypes.byref(pairs))
-    respond_dev = lib.dsy_sync_respond_dev
-
-    def step():
-        _native.check(respond_dev(*respond_args))
-    for _ in range(args.warmup):
-        step()
+    batches = Batches(lib, ctx, store, reqs, R, d_filters.data_ptr(), metas, 1, N, args.byte_limit)
+    pipe = bool(args.pipeline)
+    steps = max(args.steps, 1)
+    batches.run(args.warmup, pipe)
     ctx.synchronize()
     ctx.reset_timing()
-    ctx.set_timing(True, only=[_native.TIME_PAIR_TEST])
     t0 = time.perf_counter()
-    total = 0
-    steps = max(args.steps, 1)
-    for _ in range(steps):
-        step()
-        total += pairs.value
+    total = batches.run(steps, pipe)
     ctx.synchronize()
     elapsed = time.perf_counter() - t0
+    work = ctx.work(_native.TIME_PAIR_TEST)
+    # the kernel's launches timed by events in a serial pass (see the headline)
+    ctx.reset_timing()
+    ctx.set_timing(True, only=[_native.TIME_PAIR_TEST])
+    t1 = time.perf_counter()
+    serial_total = batches.run(steps, False)
+    serial_s = time.perf_counter() - t1
     ctx.set_timing(False)
     kt = ctx.kernel_time(_native.TIME_PAIR_TEST)
-    work = ctx.work(_native.TIME_PAIR_TEST)
+    swork = ctx.work(_native.TIME_PAIR_TEST)
     launches = max(kt["launches"], 1)
     avg_s = kt["ms"] / 1e3 / launches
     blocks = kt["blocks"] / launches
     out = {"filter": "BloomFilter(4096, 0.001, b'x'): sha1 k=10, capacity %d" % capacity, "claims": R,
-           "ms_per_step": round(elapsed / steps * 1e3, 3),
+           "ms_per_step": round(elapsed / steps * 1e3, 3), "serial_ms_per_step": round(serial_s / steps * 1e3, 3),
+           "pipeline": pipe,
            "pairs_per_s": round(total / elapsed, 1), "useful_pairs_per_s": round(work["useful_pairs"] / elapsed, 1),
            "pairs_per_step": int(total / steps),
            "roofline": {"kernel": "k_pair_test<sha1>", "bound": "valu", "unit": "Tops/s", "peak": PEAK_INT32_TOPS,
@@ -483,8 +520,9 @@ def sha1_respond(args, ctx, lib, store, N, dev, blob, offsets, total_bytes, meta
                         "frac": round(blocks * OPS_PER_BLOCK["sha1"] / avg_s / 1e12 / PEAK_INT32_TOPS, 4),
                         "avg_launch_us": round(avg_s * 1e6, 2), "launches": kt["launches"],
                         "gblocks_per_s": round(blocks / avg_s / 1e9, 2),
-                        "hbm_gbs": round((kt["bytes"] / launches + total / steps * 17) / avg_s / 1e9, 1),
-                        "lane_utilization": round(work["blocks"] / max(work["lane_slots"], 1), 4)}}
+                        "hbm_gbs": round((kt["bytes"] / launches + serial_total / steps * 17) / avg_s / 1e9, 1),
+                        "lane_utilization": round(swork["blocks"] / max(swork["lane_slots"], 1), 4),
+                        "measured": "HIP events around each launch in a serial pass (one batch at a time)"}}
     if rank == 0 and world == 1 and args.cpu_claims > 0:
         out["cpu_baseline"] = responder_cpu(args, ctx, lib, store, reqs, claims, fblob, blob, offsets,
                                             np.arange(1, N + 1, dtype=np.uint64), N, dev, "sha1")
@@ -806,7 +844,7 @@ def claim_largest_bench(args, ctx, lib, store, N, capacity, cpu, reps=20):
             "cpu_baseline": cpu}
 
 
-def ingest_bench(args, ctx, lib, store, step, pairs, N, batch=10_000, batches=10, cpu_leg=True):
+def ingest_bench(args, ctx, lib, store, step, N, batch=10_000, batches=10, cpu_leg=True):
     """SURVEY §8f row 1, requester-side ingest: `Dispersy._store` INSERTs each batch of received sync packets
     (dispersy.py:1475-1612).  Here batches of `batch` packets (100-1500 B, global times spread over the store's
     range, so they land everywhere in the index and tie with stored rows) go into the headline's 10 M-packet store
@@ -847,7 +885,7 @@ def ingest_bench(args, ctx, lib, store, step, pairs, N, batch=10_000, batches=10
     ms = sorted(times)[len(times) // 2] * 1e3
     rows = int(lib.dsy_store_rows(store))
     pkt_bytes = sum(len(b[0]) for b in work[1:]) / batches
-    step()
+    after_pairs = step()
     ctx.synchronize()
     torch.cuda.synchronize()
     cpu = None
@@ -900,7 +938,7 @@ def ingest_bench(args, ctx, lib, store, step, pairs, N, batch=10_000, batches=10
                          "achieved": round((32 * rows + pkt_bytes) / (ms / 1e3) / 1e9, 1),
                          "frac": round((32 * rows + pkt_bytes) / (ms / 1e3) / 1e9 / PEAK_HBM_GBS, 4),
                          "traffic": None},
-            "respond_after_ingest_pairs": int(pairs.value)}
+            "respond_after_ingest_pairs": int(after_pairs)}
 
 
 def gossip_sim(args, ctx, dev, rank, world, dist):
@@ -1287,31 +1325,30 @@ def heavy_tail(args, ctx, lib, dev, rank, world, dist):
     d_filters = torch.frombuffer(bytearray(fblob + bytes(64)), dtype=torch.uint8).to(dev)
     metas = (_native.Meta * 1)()
     metas[0].meta_id, metas[0].direction = 1, _native.DSY_ASC
-    p_out, p_off, pairs = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_uint64()
     if args.window:
         ctx.set_window(args.window)
-
-    def step():
-        _native.check(lib.dsy_sync_respond_dev(ctx.handle, store, reqs, R, d_filters.data_ptr(), metas, 1, G_MAX, 0,
-                                               args.byte_limit, 99, ctypes.byref(p_out), ctypes.byref(p_off),
-                                               ctypes.byref(pairs)))
-    step()
+    batches = Batches(lib, ctx, store, reqs, R, d_filters.data_ptr(), metas, 1, G_MAX, args.byte_limit)
+    pipe = bool(args.pipeline)
+    batches.run(2, pipe)
     steps = max(3, args.steps // 4)
     ctx.synchronize()
     ctx.reset_timing()
-    ctx.set_timing(True)
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
-    hashed = 0
-    for _ in range(steps):
-        step()
-        hashed += pairs.value
+    hashed = batches.run(steps, pipe)
     ctx.synchronize()
     dt = time.perf_counter() - t0
+    work = ctx.work(_native.TIME_PAIR_TEST)
+    # kernel times from a serial pass (events of overlapping batches would overlap)
+    ctx.reset_timing()
+    ctx.set_timing(True)
+    t1 = time.perf_counter()
+    batches.run(steps, False)
+    serial_dt = time.perf_counter() - t1
     ctx.set_timing(False)
     kt = ctx.kernel_time(_native.TIME_PAIR_TEST)
-    work = ctx.work(_native.TIME_PAIR_TEST)
+    swork = ctx.work(_native.TIME_PAIR_TEST)
     useful = work["useful_pairs"]
     if dist is not None and world > 1:  # the whole job: every rank's pairs over the slowest rank's time
         from dispersy_amd.shard import Collectives
@@ -1328,21 +1365,22 @@ def heavy_tail(args, ctx, lib, dev, rank, world, dist):
     out = {"metric": "packets hashed+tested/sec", "value": round(useful / dt, 1), "unit": "packets/s", "n_gpus": world,
            "cpu_baseline": cpu,
            "roofline": {"kernel": "k_pair_test<md5>", "bound": "valu+hbm",
-                        "valu_int32": {"achieved": round(work["blocks"] * OPS_PER_BLOCK["md5"] / secs / 1e12, 2)
+                        "valu_int32": {"achieved": round(swork["blocks"] * OPS_PER_BLOCK["md5"] / secs / 1e12, 2)
                                        if secs else None, "peak": PEAK_INT32_TOPS, "unit": "Tops/s",
-                                       "frac": round(work["blocks"] * OPS_PER_BLOCK["md5"] / secs / 1e12 /
+                                       "frac": round(swork["blocks"] * OPS_PER_BLOCK["md5"] / secs / 1e12 /
                                                      PEAK_INT32_TOPS, 4) if secs else None},
-                        "hbm": {"achieved": round(work["bytes"] / secs / 1e9, 1) if secs else None,
+                        "hbm": {"achieved": round(swork["bytes"] / secs / 1e9, 1) if secs else None,
                                 "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                                "frac": round(work["bytes"] / secs / 1e9 / PEAK_HBM_GBS, 4) if secs else None}},
+                                "frac": round(swork["bytes"] / secs / 1e9 / PEAK_HBM_GBS, 4) if secs else None}},
            "pairs_hashed_per_s": round(hashed / dt, 1), "ms_per_step": round(dt / steps * 1e3, 3), "steps": steps,
+           "serial_ms_per_step": round(serial_dt / steps * 1e3, 3), "pipeline": pipe,
            "stored_packets": N, "stored_bytes": total, "mean_packet_bytes": round(total / N, 1),
            "max_packet_bytes": int(lengths.max().item()), "selected_rows_per_step": int(sel_rows),
-           "lane_utilization": round(work["blocks"] / max(work["lane_slots"], 1), 4),
+           "lane_utilization": round(swork["blocks"] / max(swork["lane_slots"], 1), 4),
            "pair_test": {"avg_launch_us": round(kt["ms"] * 1e3 / max(kt["launches"], 1), 1),
                          "launches_per_step": round(kt["launches"] / steps, 1),
-                         "gblocks_per_s": round(work["blocks"] / (kt["ms"] / 1e3) / 1e9, 2) if kt["ms"] else None,
-                         "hbm_gbs": round(work["bytes"] / (kt["ms"] / 1e3) / 1e9, 1) if kt["ms"] else None}}
+                         "gblocks_per_s": round(swork["blocks"] / (kt["ms"] / 1e3) / 1e9, 2) if kt["ms"] else None,
+                         "hbm_gbs": round(swork["bytes"] / (kt["ms"] / 1e3) / 1e9, 1) if kt["ms"] else None}}
     del blob_full, blob, offsets, lengths, gt, meta, d_filters
     torch.cuda.empty_cache()
     return out

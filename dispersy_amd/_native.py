@@ -100,6 +100,9 @@ SIGNATURES = {
     "dsy_sync_respond_dev": (ctypes.c_int, [_P, _P, ctypes.POINTER(Request), _U32, _P, ctypes.POINTER(Meta), _U32,
                                             _U64, ctypes.c_int, ctypes.c_int64, _U64, ctypes.POINTER(_P),
                                             ctypes.POINTER(_P), _PU64]),
+    "dsy_sync_respond_submit": (ctypes.c_int, [_P, _P, ctypes.POINTER(Request), _U32, _P, ctypes.POINTER(Meta), _U32,
+                                                _U64, ctypes.c_int, ctypes.c_int64, _U64, _PU64]),
+    "dsy_sync_respond_wait": (ctypes.c_int, [_P, _U64, ctypes.POINTER(_P), ctypes.POINTER(_P), _PU64]),
     "dsy_filter_or_reduce": (ctypes.c_int, [_P, _P, _U32, _U64, _P]),
     "dsy_sync_decode": (ctypes.c_int, [_P, _P, _U32, _U64, ctypes.POINTER(Request), _P, _U64, _PU64, _P]),
     "dsy_sync_encode": (ctypes.c_int, [ctypes.POINTER(Request), _U32, _P, _P, _U64, _P]),

@@ -618,41 +618,58 @@ class SyncCommunity(object):
 
     def respond(self, requests, include_inactive=False, byte_limit=None, random_seed=None):
         """Batched responder (community.py:2531-2572): for each ClaimRequest (time_high already resolved), the store
-        rows the reference would send, in send order.  One call into the HIP library for the whole batch; the
-        dsy_request records are filled column by column (numpy view of the ctypes layout), not one ctypes field at
-        a time."""
+        rows the reference would send, in send order.  One call into the HIP library for the whole batch."""
+        reqs, R, blob = self.request_records(requests)
+        return self._respond_requests(reqs, R, blob, include_inactive, byte_limit, random_seed)
+
+    @staticmethod
+    def request_records(requests):
+        """(dsy_request records, R, packed filters) of a list of ClaimRequests, as the C-ABI takes them: the records
+        are filled column by column (numpy view of the ctypes layout), not one ctypes field at a time; each filter
+        sits 4-byte aligned in the blob at its record's filter_offset."""
         R = len(requests)
         reqs = np.zeros(max(R, 1), dtype=_REQUEST_DTYPE)
-        if R:
-            # one pass over the Python objects, then whole columns
-            kinds = _native.HASH_KINDS
-            c = np.fromiter(itertools.chain.from_iterable(
-                (min(q.time_low, MAX_GT), min(q.time_high, MAX_GT), q.modulo, q.offset, bf._m_size, bf._k_functions,
-                 kinds[bf._hash_name], bf._chunk, len(bf._prefix)) for q in requests for bf in (q.bloom_filter,)),
-                dtype=np.uint64, count=9 * R).reshape(R, 9)
-            raws = [q.bloom_filter._raw for q in requests]
-            prefixes = [q.bloom_filter._prefix for q in requests]
-            for j, name in enumerate(("time_low", "time_high", "modulo", "offset", "m_bits", "k", "hash_kind",
-                                      "chunk_bytes", "prefix_len")):
-                reqs[name][:R] = c[:, j]
-            plen = c[:, 8]
-            sizes = np.fromiter(((len(r) + 3) & ~3 for r in raws), dtype=np.uint64, count=R)
-            reqs["filter_offset"][:R] = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
-            if (plen == 1).all():
-                reqs["prefix"][:R, 0] = np.frombuffer(b"".join(prefixes), dtype=np.uint8)
-            else:
-                for i, p in enumerate(prefixes):
-                    reqs["prefix"][i, :len(p)] = np.frombuffer(p, dtype=np.uint8)
-            first = len(raws[0])
-            if all(len(r) == first for r in raws):
-                # one filter size (the MTU claim): the padding is the join's separator
-                pad = b"\x00" * ((-first) % 4)
-                blob = pad.join(raws) + pad
-            else:
-                blob = b"".join(bytes(r) + b"\x00" * ((-len(r)) % 4) for r in raws)
+        if not R:
+            return reqs, 0, b""
+        # one pass over the Python objects, then whole columns
+        kinds = _native.HASH_KINDS
+        c = np.fromiter(itertools.chain.from_iterable(
+            (min(q.time_low, MAX_GT), min(q.time_high, MAX_GT), q.modulo, q.offset, bf._m_size, bf._k_functions,
+             kinds[bf._hash_name], bf._chunk, len(bf._prefix)) for q in requests for bf in (q.bloom_filter,)),
+            dtype=np.uint64, count=9 * R).reshape(R, 9)
+        raws = [q.bloom_filter._raw for q in requests]
+        prefixes = [q.bloom_filter._prefix for q in requests]
+        for j, name in enumerate(("time_low", "time_high", "modulo", "offset", "m_bits", "k", "hash_kind",
+                                  "chunk_bytes", "prefix_len")):
+            reqs[name][:R] = c[:, j]
+        plen = c[:, 8]
+        sizes = np.fromiter(((len(r) + 3) & ~3 for r in raws), dtype=np.uint64, count=R)
+        reqs["filter_offset"][:R] = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+        if (plen == 1).all():
+            reqs["prefix"][:R, 0] = np.frombuffer(b"".join(prefixes), dtype=np.uint8)
         else:
-            blob = b""
-        return self._respond_requests(reqs, R, blob, include_inactive, byte_limit, random_seed)
+            for i, p in enumerate(prefixes):
+                reqs["prefix"][i, :len(p)] = np.frombuffer(p, dtype=np.uint8)
+        first = len(raws[0])
+        if all(len(r) == first for r in raws):
+            # one filter size (the MTU claim): the padding is the join's separator
+            pad = b"\x00" * ((-first) % 4)
+            blob = pad.join(raws) + pad
+        else:
+            blob = b"".join(bytes(r) + b"\x00" * ((-len(r)) % 4) for r in raws)
+        return reqs, R, blob
+
+    def meta_records(self):
+        """The served metas as dsy_meta records, in serving order (priority DESC, community.py:2790-2794)."""
+        metas = self._served_metas()
+        mt = (_native.Meta * max(len(metas), 1))()
+        for j, m in enumerate(metas):
+            mt[j].meta_id = m.database_id
+            mt[j].direction = _native.DIRECTIONS[m.distribution.synchronization_direction]
+            pr = m.distribution.pruning
+            mt[j].has_pruning = 1 if isinstance(pr, GlobalTimePruning) else 0
+            mt[j].inactive_threshold = pr.inactive_threshold if isinstance(pr, GlobalTimePruning) else 0
+        return mt, len(metas)
 
     def respond_wire(self, blocks, include_inactive=False, byte_limit=None, random_seed=None):
         """on_introduction_request's sync half for a receive batch of raw sync blocks: decode (conversion.py:732-799,
@@ -683,20 +700,13 @@ class SyncCommunity(object):
         seed = self._random.getrandbits(64) if random_seed is None else random_seed
         st = self._store
         ctx = st.ctx
-        metas = self._served_metas()
-        mt = (_native.Meta * max(len(metas), 1))()
-        for j, m in enumerate(metas):
-            mt[j].meta_id = m.database_id
-            mt[j].direction = _native.DIRECTIONS[m.distribution.synchronization_direction]
-            pr = m.distribution.pruning
-            mt[j].has_pruning = 1 if isinstance(pr, GlobalTimePruning) else 0
-            mt[j].inactive_threshold = pr.inactive_threshold if isinstance(pr, GlobalTimePruning) else 0
+        mt, n_metas = self.meta_records()
         out_off = np.zeros(R + 1, dtype=np.uint64)
         cap = 1 << 16
         while True:
             out = np.empty(cap, dtype=np.uint64)
             rc = ctx.lib.dsy_sync_respond(ctx.handle, st.handle, reqs.ctypes.data_as(ctypes.POINTER(_native.Request)),
-                                          R, blob, len(blob), mt, len(metas),
+                                          R, blob, len(blob), mt, n_metas,
                                           self.global_time, 1 if include_inactive else 0, int(byte_limit), seed,
                                           out.ctypes.data, cap, out_off.ctypes.data)
             if rc == _native.DSY_ECAPACITY and int(out_off[R]) > cap:

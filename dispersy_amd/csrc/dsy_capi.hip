@@ -54,12 +54,63 @@ struct PendingTimer {
 
 }  // namespace
 
+// grow-only named device buffers plus one grow-only pinned staging buffer
+struct Workspace {
+    std::map<std::string, DevBuf> ws;
+    std::unordered_map<const char*, DevBuf*> by_name;  // ws_get's cache, keyed by the literal's address
+    void* stage = nullptr;  // pinned: the responder's uploads and its host-mapped status
+    size_t stage_bytes = 0;
+    void release() {
+        for (auto& kv : ws) if (kv.second.ptr) hipFree(kv.second.ptr);
+        ws.clear();
+        by_name.clear();
+        if (stage) hipHostFree(stage);
+        stage = nullptr;
+        stage_bytes = 0;
+    }
+};
+
+// One responder batch between its first window and its end (respond_core's state across the host syncs).
+struct RespondJob {
+    uint32_t R = 0, J = 0;
+    const dsy_store* s = nullptr;
+    std::vector<std::vector<uint32_t>> fam_active;  // per family: its active claims
+    std::vector<int> fam_id;
+    RespondLaunch L{};
+    uint64_t pool = 0;
+    uint8_t* h_in = nullptr;   // pinned staging (upload region, then host-mapped status)
+    uint8_t* h_io = nullptr;
+    uint32_t* h_act0 = nullptr;
+    const uint32_t* d_slots = nullptr;
+    uint32_t* d_act = nullptr;
+    void* d_in = nullptr;
+    void* d_io = nullptr;
+    void* d_packed = nullptr;
+    void* d_packed_off = nullptr;
+    size_t in_b = 0, cnt_b = 0;
+    uint64_t per_claim = 0;
+    bool fused_first = false, first = true, ran = false, first_fill = true;
+    double hp[4] = {0, 0, 0, 0};
+    double hp_wait = 0;
+};
+
+// A responder slot: its own workspace, stream and job, so two batches can be in flight (dsy_sync_respond_submit).
+// Slot 0 runs on the ctx stream (the synchronous entry points use it), slot 1 on a stream of its own.
+struct RespondSlot {
+    Workspace w;
+    hipStream_t stream = nullptr;
+    bool busy = false;       // submitted, not yet waited for
+    uint64_t ticket = 0;
+    RespondJob job;
+};
+
 struct dsy_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;
-    std::map<std::string, DevBuf> ws;
-    std::unordered_map<const char*, DevBuf*> ws_by_name;  // ws_get's cache, keyed by the literal's address
+    Workspace main;  // every entry point but the responder's
+    RespondSlot rs[2];
+    uint64_t next_ticket = 1;
     uint32_t max_grid = 2048;
     int bloom_diag = 0;  // DSY_BLOOM_DIAG at creation: single-filter ceiling diagnostics (k_bloom DIAG)
     int pair_diag = 0;   // DSY_PAIR_DIAG at creation: responder ceiling diagnostics (k_pair_test DIAG)
@@ -77,8 +128,6 @@ struct dsy_ctx {
     uint64_t slots[kTimeClasses] = {};   // lane-block slots of the hashing waves (load balance)
     void* pinned = nullptr;  // small pinned staging for flags/counters
     uint64_t window_cap = 0; // dsy_ctx_set_window: upper bound on the responder's window (0: the default 2^18)
-    void* stage = nullptr;   // grow-only pinned staging of the responder's uploads and status read-backs
-    size_t stage_bytes = 0;
     hipStream_t aux = nullptr;  // dsy_sim_claim_matrix: work that depends on nothing queued on `stream`
     hipEvent_t xev = nullptr;   // dsy_ctx_wait_stream / dsy_ctx_signal_stream
     // the simulator's device-side counters (work of build / respond, pairs tested, response overflow): the calls
@@ -86,6 +135,7 @@ struct dsy_ctx {
     void* sim_acc = nullptr;
     bool sim_pending = false;
     bool sim_overflow = false;
+    int inflight() const { return (int)rs[0].busy + (int)rs[1].busy; }
 };
 
 struct dsy_store {
@@ -116,10 +166,10 @@ struct dsy_store {
 namespace {
 
 // grow-only named workspace buffer
-int ws_get(dsy_ctx* c, const char* name, size_t bytes, void** out, bool* fresh = nullptr) {
+int ws_get(Workspace& W, const char* name, size_t bytes, void** out, bool* fresh = nullptr) {
     // names are string literals: their address finds the buffer without building a std::string per call
-    DevBuf*& slot = c->ws_by_name[name];
-    if (!slot) slot = &c->ws[name];  // std::map nodes do not move
+    DevBuf*& slot = W.by_name[name];
+    if (!slot) slot = &W.ws[name];  // std::map nodes do not move
     DevBuf& b = *slot;
     if (fresh) *fresh = b.bytes < bytes;
     if (b.bytes < bytes) {
@@ -136,21 +186,24 @@ int ws_get(dsy_ctx* c, const char* name, size_t bytes, void** out, bool* fresh =
     *out = b.ptr;
     return DSY_OK;
 }
+int ws_get(dsy_ctx* c, const char* name, size_t bytes, void** out, bool* fresh = nullptr) {
+    return ws_get(c->main, name, bytes, out, fresh);
+}
 
 // grow-only pinned host staging (one H2D upload and one D2H status read per responder window)
-int stage_get(dsy_ctx* c, size_t bytes, uint8_t** out) {
-    if (c->stage_bytes < bytes) {
-        if (c->stage) hipHostFree(c->stage);
-        c->stage = nullptr;
-        c->stage_bytes = 0;
+int stage_get(Workspace& W, size_t bytes, uint8_t** out) {
+    if (W.stage_bytes < bytes) {
+        if (W.stage) hipHostFree(W.stage);
+        W.stage = nullptr;
+        W.stage_bytes = 0;
         const size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
-        if (hipHostMalloc(&c->stage, want, hipHostMallocDefault) != hipSuccess) {
-            c->stage = nullptr;
+        if (hipHostMalloc(&W.stage, want, hipHostMallocDefault) != hipSuccess) {
+            W.stage = nullptr;
             return fail(DSY_ENOMEM, "hipHostMalloc(%zu) for the staging buffer failed", want);
         }
-        c->stage_bytes = want;
+        W.stage_bytes = want;
     }
-    *out = (uint8_t*)c->stage;
+    *out = (uint8_t*)W.stage;
     return DSY_OK;
 }
 
@@ -165,18 +218,18 @@ hipEvent_t take_event(dsy_ctx* c) {
     return e;
 }
 
-void timer_begin(dsy_ctx* c, PendingTimer* t, int cls) {
+void timer_begin(dsy_ctx* c, PendingTimer* t, int cls, hipStream_t st = nullptr) {
     t->cls = cls;
     t->a = t->b = nullptr;
     if (!(c->timing & (1u << cls))) return;
     t->a = take_event(c);
     t->b = take_event(c);
-    hipEventRecord(t->a, c->stream);
+    hipEventRecord(t->a, st ? st : c->stream);
 }
 
-void timer_end(dsy_ctx* c, PendingTimer* t) {
+void timer_end(dsy_ctx* c, PendingTimer* t, hipStream_t st = nullptr) {
     if (!t->a) return;
-    hipEventRecord(t->b, c->stream);
+    hipEventRecord(t->b, st ? st : c->stream);
     c->pending.push_back(*t);
 }
 
@@ -435,12 +488,18 @@ int dsy_ctx_destroy(dsy_ctx* c) {
         hipSetDevice(c->device);
         hipStreamSynchronize(c->stream);
         timers_collect(c);
-        for (auto& kv : c->ws) if (kv.second.ptr) hipFree(kv.second.ptr);
+        for (auto& sl : c->rs) {
+            if (sl.stream && sl.stream != c->stream) {
+                hipStreamSynchronize(sl.stream);
+                hipStreamDestroy(sl.stream);
+            }
+            sl.w.release();
+        }
+        c->main.release();
         for (auto e : c->event_pool) hipEventDestroy(e);
         if (c->xev) hipEventDestroy(c->xev);
         if (c->aux) hipStreamDestroy(c->aux);
         if (c->pinned) hipHostFree(c->pinned);
-        if (c->stage) hipHostFree(c->stage);
         hipStreamDestroy(c->stream);
     }
     delete c;
@@ -809,6 +868,7 @@ int dsy_store_free(dsy_store* s) {
     if (!s) return DSY_OK;
     if (s->ctx) {
         std::lock_guard<std::mutex> lk(s->ctx->mu);
+        if (s->ctx->inflight()) return fail(DSY_EINVAL, "the store cannot be freed while submitted responder batches are in flight");
         hipSetDevice(s->ctx->device);
         hipStreamSynchronize(s->ctx->stream);
         for (void* p : s->owned) hipFree(p);
@@ -906,6 +966,7 @@ int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blo
     if (rc) return rc;
     if (a == 0) return DSY_OK;
     Guard g(c);
+    if (c->inflight()) return fail(DSY_EINVAL, "the store cannot change while submitted responder batches are in flight");
     const uint64_t n0 = s->n, base0 = offsets[0], add = offsets[a] - base0;
 
     // the new rows in index order (meta_message, global_time, rowid): argument order breaks ties
@@ -1052,6 +1113,7 @@ int dsy_store_prune(dsy_ctx* c, dsy_store* s, uint32_t meta, uint64_t max_gt, ui
     auto it = s->segs.find(meta);
     if (it == s->segs.end() || it->second.first == it->second.second) return DSY_OK;
     Guard g(c);
+    if (c->inflight()) return fail(DSY_EINVAL, "the store cannot change while submitted responder batches are in flight");
     const uint64_t a = it->second.first, b = it->second.second;
     void* d_k;
     int rc;
@@ -1114,6 +1176,7 @@ int dsy_store_delete(dsy_ctx* c, dsy_store* s, const uint64_t* rows, uint64_t k,
     *out_deleted = 0;
     if (!k) return DSY_OK;
     Guard g(c);
+    if (c->inflight()) return fail(DSY_EINVAL, "the store cannot change while submitted responder batches are in flight");
     // segment bounds (old positions) to remap: every meta's [a, b)
     std::vector<uint32_t> seg_ids;
     std::vector<uint64_t> bounds;
@@ -1242,6 +1305,7 @@ int dsy_store_replace(dsy_ctx* c, dsy_store* s, const uint64_t* rows, const uint
         if (rows[i] >= s->n) return fail(DSY_EINVAL, "row %llu out of range (%llu rows)", (unsigned long long)rows[i], (unsigned long long)s->n);
     if (!k) return DSY_OK;
     Guard g(c);
+    if (c->inflight()) return fail(DSY_EINVAL, "the store cannot change while submitted responder batches are in flight");
     HIP_TRY(hipStreamSynchronize(c->stream));
     const uint64_t base0 = offsets[0], add = offsets[k] - base0;
     std::vector<RowRec> nrec(k);
@@ -1544,13 +1608,104 @@ static double host_us() {
     return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, uint32_t R, const uint8_t* d_filters,
-                        uint64_t filters_len, const dsy_meta* metas, uint32_t J, uint64_t responder_gt,
-                        int include_inactive, int64_t byte_limit, uint64_t seed, uint64_t** d_packed,
-                        uint64_t** d_packed_off, uint64_t* total_pairs) {
-    static const bool host_profile = getenv("DSY_HOST_PROFILE") != nullptr;
-    double hp[6] = {host_profile ? host_us() : 0.0};
-    double hp_wait = 0.0;
+static const bool g_host_profile = getenv("DSY_HOST_PROFILE") != nullptr;
+
+// One window of a job: fill -> hash/test (one launch per hash family) -> compact -> speculative pack, enqueued on the
+// slot's stream without waiting.  Only the active claims take part; as they finish, the rest share the pool in bigger
+// windows.
+static int job_window(dsy_ctx* c, RespondSlot& sl) {
+    RespondJob& jb = sl.job;
+    RespondLaunch& L = jb.L;
+    const hipStream_t st = sl.stream;
+    std::vector<std::pair<size_t, size_t>> runs;  // per family: (first slot, slots)
+    size_t n_act = 0;
+    for (auto& fa : jb.fam_active) {
+        runs.push_back({n_act, fa.size()});
+        n_act += fa.size();
+    }
+    uint64_t W = jb.pool / n_act / 64 * 64;
+    W = std::min<uint64_t>(std::max<uint64_t>(W, kWindow), kMaxWindow);
+    if (c->window_cap) W = std::min<uint64_t>(W, c->window_cap);
+    L.window = W;
+    L.n_act = (uint32_t)n_act;
+    if (!jb.first) {  // the first window's list went up with the claims
+        uint32_t* h_act = (uint32_t*)jb.h_in;  // the staged claims are on the device already: reuse the space
+        size_t a = 0;
+        for (auto& fa : jb.fam_active)
+            for (uint32_t r : fa) h_act[a++] = r;
+        HIP_TRY(hipMemcpyAsync(jb.d_act, h_act, n_act * 4, hipMemcpyHostToDevice, st));
+    }
+    jb.first = false;
+    jb.ran = true;
+    int rc;
+    static const bool fill_profile = getenv("DSY_FILL_PROFILE") != nullptr;
+    void* d_fc = nullptr;
+    if (fill_profile) {
+        if ((rc = ws_get(sl.w, "fill_clock", n_act * 32 + 32, &d_fc))) return rc;
+        HIP_TRY(hipMemsetAsync(d_fc, 0, n_act * 32, st));
+        L.fill_clock = (uint64_t*)d_fc;
+    }
+    PendingTimer t;
+    timer_begin(c, &t, kTimeSelect, st);
+    if (jb.first_fill && jb.fused_first)
+        HIP_TRY(launch_fill_first(L, jb.h_in, jb.d_in, jb.in_b, jb.d_io, jb.cnt_b, jb.per_claim,
+                                  jb.fam_active.size() == 1 ? nullptr : jb.h_act0));
+    else
+        HIP_TRY(launch_fill(L));
+    jb.first_fill = false;
+    timer_end(c, &t, st);
+    if (fill_profile) {  // per-window stderr line: k_fill phase durations over the workgroups (s_memtime ticks)
+        std::vector<uint64_t> fc(n_act * 4);
+        HIP_TRY(hipMemcpyAsync(fc.data(), d_fc, n_act * 32, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        uint64_t t0 = ~0ull, t2 = 0, sel = 0, srt = 0, stp = 0, mx_sel = 0, mx_srt = 0, mx_stp = 0, n = 0;
+        for (size_t a = 0; a < n_act; ++a) {
+            if (!fc[a * 4]) continue;
+            t0 = std::min(t0, fc[a * 4 + 3]);
+            t2 = std::max(t2, fc[a * 4 + 2]);
+            stp += fc[a * 4] - fc[a * 4 + 3];
+            sel += fc[a * 4 + 1] - fc[a * 4];
+            srt += fc[a * 4 + 2] - fc[a * 4 + 1];
+            mx_stp = std::max(mx_stp, fc[a * 4] - fc[a * 4 + 3]);
+            mx_sel = std::max(mx_sel, fc[a * 4 + 1] - fc[a * 4]);
+            mx_srt = std::max(mx_srt, fc[a * 4 + 2] - fc[a * 4 + 1]);
+            ++n;
+        }
+        // shader-clock ticks; setup = k_fill_first's host reads + plan (0 for k_fill)
+        if (n) fprintf(stderr, "fill_profile n=%llu span=%llu setup avg=%llu max=%llu select avg=%llu max=%llu "
+                       "sort avg=%llu max=%llu\n", (unsigned long long)n, (unsigned long long)(t2 - t0),
+                       (unsigned long long)(stp / n), (unsigned long long)mx_stp, (unsigned long long)(sel / n),
+                       (unsigned long long)mx_sel, (unsigned long long)(srt / n), (unsigned long long)mx_srt);
+        L.fill_clock = nullptr;
+    }
+    for (size_t f = 0; f < jb.fam_active.size(); ++f) {
+        if (!runs[f].second) continue;
+        const int fid = jb.fam_id[f];
+        timer_dispatch(c, &t, kTimePairTest, &L.ev_start, &L.ev_stop);
+        const int kc = fid / 2;
+        HIP_TRY(launch_pair_test_list(L, kc / 3, kc % 3 == 0 ? 2 : kc % 3 == 1 ? 4 : 8, fid % 2 == 1,
+                                      jb.d_slots + runs[f].first, (uint32_t)runs[f].second));
+        timer_dispatched(c, &t);
+        L.ev_start = L.ev_stop = nullptr;
+    }
+    timer_begin(c, &t, kTimeCompact, st);
+    HIP_TRY(launch_compact(L));
+    timer_end(c, &t, st);
+    // speculatively pack the output now (it is redone if another window follows): the GPU packs while the host wakes
+    // up and reads the status
+    HIP_TRY(launch_pack(L, (uint64_t*)jb.d_packed, (uint64_t*)jb.d_packed_off, nullptr));
+    if (g_host_profile && !jb.hp[2]) jb.hp[2] = host_us();  // first window enqueued
+    return DSY_OK;
+}
+
+// Validate and stage a batch of claims into slot sl and enqueue its first window (no host wait).
+static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_request* reqs, uint32_t R,
+                     const uint8_t* d_filters, uint64_t filters_len, const dsy_meta* metas, uint32_t J,
+                     uint64_t responder_gt, int include_inactive, int64_t byte_limit, uint64_t seed) {
+    sl.job = RespondJob{};
+    RespondJob& jb = sl.job;
+    const hipStream_t st = sl.stream;
+    if (g_host_profile) jb.hp[0] = host_us();
     // ---- validate claims (payload.py:89-101, conversion.py:772-789) and their filters; group them by hash family
     // (kind x chunk width: one pair-test launch per family)
     // family id = (kind * 3 + chunk class) * 2 + long prefix (> 4 bytes: the byte-wise hashing path)
@@ -1584,7 +1739,14 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
         if (fm.empty()) fm.reserve(R);
         fm.push_back(r);
     }
-    const uint64_t pool = kWindow * std::max<uint64_t>(R, kMinSlots);
+    for (uint32_t j = 0; j < J; ++j)
+        if (metas[j].direction < DSY_ASC || metas[j].direction > DSY_RANDOM)
+            return fail(DSY_EINVAL, "meta %u: unknown synchronization direction %d", j, metas[j].direction);
+    jb.R = R;
+    jb.J = J;
+    jb.s = s;
+    jb.pool = kWindow * std::max<uint64_t>(R, kMinSlots);
+    const uint64_t pool = jb.pool;
     // ---- device layout: one upload region [claims | metas | window slots 0..R-1 | first active list] and one
     // device status region [counters kCntSpread x 64 B | flags 64 B | upper R x u64] (counters and flags zeroed by
     // k_setup); host-mapped status [totals kCntN x u64 | overflow | act_done R B]: k_compact writes the done flags
@@ -1598,26 +1760,33 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     const size_t cnt_b = kCntSpread * kCntN * 8, head_b = cnt_b + 64;
     const size_t io_b = head_b + (size_t)R * 8;
     constexpr size_t kHostHead = 128;
+    jb.in_b = in_b;
+    jb.cnt_b = cnt_b;
     int rc;
     void *d_in, *d_io, *d_plans, *d_state, *d_pairs, *d_off, *d_len, *d_miss, *d_task, *d_emit, *d_ticket;
-    if ((rc = ws_get(c, "resp_in", in_b, &d_in))) return rc;
-    if ((rc = ws_get(c, "emitted_n", std::max<size_t>(R, 1) * 8, &d_emit))) return rc;
+    Workspace& w = sl.w;
+    if ((rc = ws_get(w, "resp_in", in_b, &d_in))) return rc;
+    if ((rc = ws_get(w, "emitted_n", std::max<size_t>(R, 1) * 8, &d_emit))) return rc;
     bool fresh = false;
-    if ((rc = ws_get(c, "ticket", 64, &d_ticket, &fresh))) return rc;
-    if (fresh) HIP_TRY(hipMemsetAsync(d_ticket, 0, 64, c->stream));
+    if ((rc = ws_get(w, "ticket", 64, &d_ticket, &fresh))) return rc;
+    if (fresh) HIP_TRY(hipMemsetAsync(d_ticket, 0, 64, st));
     bool io_fresh = false;
-    if ((rc = ws_get(c, "resp_io", io_b, &d_io, &io_fresh))) return rc;
-    if (io_fresh) HIP_TRY(hipMemsetAsync(d_io, 0, io_b, c->stream));  // flags start (and stay, k_compact) at zero
-    if ((rc = ws_get(c, "plans", std::max<size_t>((size_t)R * J, 1) * sizeof(Plan), &d_plans))) return rc;
-    if ((rc = ws_get(c, "state", std::max<size_t>(R, 1) * sizeof(ReqState), &d_state))) return rc;
-    if ((rc = ws_get(c, "pairs", pool * 8, &d_pairs))) return rc;
-    if ((rc = ws_get(c, "pair_off", pool * 8, &d_off))) return rc;
-    if ((rc = ws_get(c, "pair_len", pool * 4, &d_len))) return rc;
-    if ((rc = ws_get(c, "miss_mask", pool / 8 + 64, &d_miss))) return rc;
-    if ((rc = ws_get(c, "task", pool * sizeof(PairTask), &d_task))) return rc;
+    if ((rc = ws_get(w, "resp_io", io_b, &d_io, &io_fresh))) return rc;
+    if (io_fresh) HIP_TRY(hipMemsetAsync(d_io, 0, io_b, st));  // flags start (and stay, k_compact) at zero
+    if ((rc = ws_get(w, "plans", std::max<size_t>((size_t)R * J, 1) * sizeof(Plan), &d_plans))) return rc;
+    if ((rc = ws_get(w, "state", std::max<size_t>(R, 1) * sizeof(ReqState), &d_state))) return rc;
+    if ((rc = ws_get(w, "pairs", pool * 8, &d_pairs))) return rc;
+    if ((rc = ws_get(w, "pair_off", pool * 8, &d_off))) return rc;
+    if ((rc = ws_get(w, "pair_len", pool * 4, &d_len))) return rc;
+    if ((rc = ws_get(w, "miss_mask", pool / 8 + 64, &d_miss))) return rc;
+    if ((rc = ws_get(w, "task", pool * sizeof(PairTask), &d_task))) return rc;
     uint8_t* h_in;
-    if ((rc = stage_get(c, in_b + kHostHead + act_done_b, &h_in))) return rc;
+    if ((rc = stage_get(w, in_b + kHostHead + act_done_b, &h_in))) return rc;
+    jb.h_in = h_in;
+    jb.d_in = d_in;
+    jb.d_io = d_io;
     uint8_t* h_io = h_in + in_b;  // host-mapped status
+    jb.h_io = h_io;
     std::memset(h_io, 0, kHostHead);  // totals stay zero if no window runs (R == 0)
     {
         DevRequest* dq = (DevRequest*)h_in;
@@ -1648,8 +1817,6 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     }
     SegMeta* sm = (SegMeta*)(h_in + reqs_b);
     for (uint32_t j = 0; j < J; ++j) {
-        if (metas[j].direction < DSY_ASC || metas[j].direction > DSY_RANDOM)
-            return fail(DSY_EINVAL, "meta %u: unknown synchronization direction %d", j, metas[j].direction);
         auto it = s->segs.find(metas[j].meta_id);
         SegMeta m{};
         m.seg_a = it == s->segs.end() ? 0 : it->second.first;
@@ -1661,24 +1828,23 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     }
     uint32_t* h_slots = (uint32_t*)(h_in + reqs_b + metas_b);
     uint32_t* h_act0 = h_slots + R;
+    jb.h_act0 = h_act0;
     // the active list, family by family (a family's active claims occupy a contiguous run of slots)
-    std::vector<std::vector<uint32_t>> fam_active;
-    std::vector<int> fam_id;
     for (int f = 0; f < kFamilies; ++f)
         if (!fam_members[f].empty()) {
-            fam_active.push_back(fam_members[f]);
-            fam_id.push_back(f);
+            jb.fam_active.push_back(std::move(fam_members[f]));
+            jb.fam_id.push_back(f);
         }
     {
         uint32_t a = 0;
         for (uint32_t i = 0; i < R; ++i) h_slots[i] = i;
-        for (auto& fa : fam_active)
+        for (auto& fa : jb.fam_active)
             for (uint32_t r : fa) h_act0[a++] = r;
     }
     uint8_t* io = (uint8_t*)d_io;
-    if (host_profile) hp[1] = host_us();  // claims validated and staged
+    if (g_host_profile) jb.hp[1] = host_us();  // claims validated and staged
 
-    RespondLaunch L{};
+    RespondLaunch& L = jb.L;
     L.st.blob = s->d_blob;
     L.st.offsets = s->d_offsets;
     L.st.lines = s->d_lines;
@@ -1688,8 +1854,8 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     L.st.n_live = s->n_live;
     L.reqs = (const DevRequest*)d_in;
     L.metas = (const SegMeta*)((uint8_t*)d_in + reqs_b);
-    const uint32_t* d_slots = (const uint32_t*)((uint8_t*)d_in + reqs_b + metas_b);
-    uint32_t* d_act = (uint32_t*)(d_slots + R);
+    jb.d_slots = (const uint32_t*)((uint8_t*)d_in + reqs_b + metas_b);
+    jb.d_act = (uint32_t*)(jb.d_slots + R);
     L.R = R;
     L.J = J;
     L.filters = d_filters;
@@ -1698,7 +1864,7 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     L.byte_limit = byte_limit;
     L.seed = seed;
     L.window = kWindow;
-    L.act = d_act;
+    L.act = jb.d_act;
     L.act_done = h_io + kHostHead;
     L.h_status = (uint64_t*)h_io;
     L.plans = (Plan*)d_plans;
@@ -1713,7 +1879,7 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     L.task = (PairTask*)d_task;
     L.flags = (uint32_t*)(io + cnt_b);
     L.counters = (uint64_t*)io;
-    L.stream = c->stream;
+    L.stream = st;
     L.diag = c->pair_diag;
     L.grid_cap = c->pair_grid ? c->pair_grid : c->max_grid;
 
@@ -1726,151 +1892,113 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     uint64_t cap_total = 0;
     const uint64_t per_claim = byte_limit <= 0 ? 1 : (s->min_len > 0 ? (uint64_t)byte_limit / s->min_len + 2 : ~0ull);
     const bool dev_caps = per_claim != ~0ull && per_claim <= (1ull << 26) / std::max<uint32_t>(R, 1);
+    jb.per_claim = per_claim;
     PendingTimer t;
     // one meta and device-side capacities (the common case): the setup runs inside the first window's fill
     // (k_fill_first); otherwise k_setup plans every (claim, meta) first
-    const bool fused_first = J == 1 && dev_caps && R > 0;
-    if (!fused_first) {
-        timer_begin(c, &t, kTimeSelect);
+    jb.fused_first = J == 1 && dev_caps && R > 0;
+    if (!jb.fused_first) {
+        timer_begin(c, &t, kTimeSelect, st);
         HIP_TRY(launch_setup(L, h_in, d_in, in_b, d_io, head_b, dev_caps ? per_claim : 0));
-        timer_end(c, &t);
+        timer_end(c, &t, st);
     }
     if (dev_caps) {
         cap_total = per_claim * R;
-        if ((rc = ws_get(c, "out", std::max<uint64_t>(cap_total, 1) * 8, &d_out))) return rc;
+        if ((rc = ws_get(w, "out", std::max<uint64_t>(cap_total, 1) * 8, &d_out))) return rc;
         L.out = (uint64_t*)d_out;
     } else {
         std::vector<uint64_t> upper(R);
-        if (R) HIP_TRY(hipMemcpyAsync(upper.data(), L.upper, (size_t)R * 8, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        std::vector<ReqState> st(R);
+        if (R) HIP_TRY(hipMemcpyAsync(upper.data(), L.upper, (size_t)R * 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        std::vector<ReqState> rst(R);
         for (uint32_t r = 0; r < R; ++r) {
-            st[r] = ReqState{};
-            st[r].cap = std::min<uint64_t>(upper[r], per_claim);
-            st[r].out_base = cap_total;
-            st[r].done = upper[r] == 0;
-            cap_total += st[r].cap;
+            rst[r] = ReqState{};
+            rst[r].cap = std::min<uint64_t>(upper[r], per_claim);
+            rst[r].out_base = cap_total;
+            rst[r].done = upper[r] == 0;
+            cap_total += rst[r].cap;
         }
-        if ((rc = ws_get(c, "out", std::max<uint64_t>(cap_total, 1) * 8, &d_out))) return rc;
+        if ((rc = ws_get(w, "out", std::max<uint64_t>(cap_total, 1) * 8, &d_out))) return rc;
         L.out = (uint64_t*)d_out;
-        if (R) HIP_TRY(hipMemcpy(d_state, st.data(), (size_t)R * sizeof(ReqState), hipMemcpyHostToDevice));
+        if (R) {
+            HIP_TRY(hipMemcpyAsync(d_state, rst.data(), (size_t)R * sizeof(ReqState), hipMemcpyHostToDevice, st));
+            HIP_TRY(hipStreamSynchronize(st));  // rst is pageable and goes out of scope
+        }
     }
+    if ((rc = ws_get(w, "packed", std::max<uint64_t>(cap_total, 1) * 8, &jb.d_packed))) return rc;
+    if ((rc = ws_get(w, "packed_off", ((size_t)R + 1) * 8, &jb.d_packed_off))) return rc;
+    size_t n_act = 0;
+    for (auto& fa : jb.fam_active) n_act += fa.size();
+    if (n_act) return job_window(c, sl);
+    return DSY_OK;
+}
 
-    // ---- windows: fill -> hash/test (one launch per hash family) -> compact; one host sync per window.  Only
-    // the active claims take part; as they finish, the rest share the pool in bigger windows.
-    void *d_packed_v, *d_packed_off_v;
-    if ((rc = ws_get(c, "packed", std::max<uint64_t>(cap_total, 1) * 8, &d_packed_v))) return rc;
-    if ((rc = ws_get(c, "packed_off", ((size_t)R + 1) * 8, &d_packed_off_v))) return rc;
-    bool first = true, ran = false, first_fill = true;
+// Wait for the job's windows, run the further windows its unfinished claims need, and return its results.
+static int job_finish(dsy_ctx* c, RespondSlot& sl, uint64_t** d_packed, uint64_t** d_packed_off, uint64_t* total_pairs) {
+    RespondJob& jb = sl.job;
+    RespondLaunch& L = jb.L;
+    const hipStream_t st = sl.stream;
+    constexpr size_t kHostHead = 128;
     for (;;) {
-        std::vector<std::pair<size_t, size_t>> runs;  // per family: (first slot, slots)
         size_t n_act = 0;
-        for (auto& fa : fam_active) {
-            runs.push_back({n_act, fa.size()});
-            n_act += fa.size();
-        }
+        for (auto& fa : jb.fam_active) n_act += fa.size();
         if (!n_act) break;
-        uint64_t W = pool / n_act / 64 * 64;
-        W = std::min<uint64_t>(std::max<uint64_t>(W, kWindow), kMaxWindow);
-        if (c->window_cap) W = std::min<uint64_t>(W, c->window_cap);
-        L.window = W;
-        L.n_act = (uint32_t)n_act;
-        if (!first) {  // the first window's list went up with the claims
-            uint32_t* h_act = (uint32_t*)h_in;  // the staged claims are on the device already: reuse the space
-            size_t a = 0;
-            for (auto& fa : fam_active)
-                for (uint32_t r : fa) h_act[a++] = r;
-            HIP_TRY(hipMemcpyAsync(d_act, h_act, n_act * 4, hipMemcpyHostToDevice, c->stream));
-        }
-        first = false;
-        ran = true;
-        static const bool fill_profile = getenv("DSY_FILL_PROFILE") != nullptr;
-        void* d_fc = nullptr;
-        if (fill_profile) {
-            if ((rc = ws_get(c, "fill_clock", n_act * 32 + 32, &d_fc))) return rc;
-            HIP_TRY(hipMemsetAsync(d_fc, 0, n_act * 32, c->stream));
-            L.fill_clock = (uint64_t*)d_fc;
-        }
-        timer_begin(c, &t, kTimeSelect);
-        if (first_fill && fused_first)
-            HIP_TRY(launch_fill_first(L, h_in, d_in, in_b, d_io, cnt_b, per_claim,
-                                      fam_active.size() == 1 ? nullptr : h_act0));
-        else
-            HIP_TRY(launch_fill(L));
-        first_fill = false;
-        timer_end(c, &t);
-        if (fill_profile) {  // per-window stderr line: k_fill phase durations over the workgroups (s_memtime ticks)
-            std::vector<uint64_t> fc(n_act * 4);
-            HIP_TRY(hipMemcpyAsync(fc.data(), d_fc, n_act * 32, hipMemcpyDeviceToHost, c->stream));
-            HIP_TRY(hipStreamSynchronize(c->stream));
-            uint64_t t0 = ~0ull, t2 = 0, sel = 0, srt = 0, stp = 0, mx_sel = 0, mx_srt = 0, mx_stp = 0, n = 0;
-            for (size_t a = 0; a < n_act; ++a) {
-                if (!fc[a * 4]) continue;
-                t0 = std::min(t0, fc[a * 4 + 3]);
-                t2 = std::max(t2, fc[a * 4 + 2]);
-                stp += fc[a * 4] - fc[a * 4 + 3];
-                sel += fc[a * 4 + 1] - fc[a * 4];
-                srt += fc[a * 4 + 2] - fc[a * 4 + 1];
-                mx_stp = std::max(mx_stp, fc[a * 4] - fc[a * 4 + 3]);
-                mx_sel = std::max(mx_sel, fc[a * 4 + 1] - fc[a * 4]);
-                mx_srt = std::max(mx_srt, fc[a * 4 + 2] - fc[a * 4 + 1]);
-                ++n;
-            }
-            // shader-clock ticks; setup = k_fill_first's host reads + plan (0 for k_fill)
-            if (n) fprintf(stderr, "fill_profile n=%llu span=%llu setup avg=%llu max=%llu select avg=%llu max=%llu "
-                           "sort avg=%llu max=%llu\n", (unsigned long long)n, (unsigned long long)(t2 - t0),
-                           (unsigned long long)(stp / n), (unsigned long long)mx_stp, (unsigned long long)(sel / n),
-                           (unsigned long long)mx_sel, (unsigned long long)(srt / n), (unsigned long long)mx_srt);
-            L.fill_clock = nullptr;
-        }
-        for (size_t f = 0; f < fam_active.size(); ++f) {
-            if (!runs[f].second) continue;
-            const int fid = fam_id[f];
-            timer_dispatch(c, &t, kTimePairTest, &L.ev_start, &L.ev_stop);
-            const int kc = fid / 2;
-            HIP_TRY(launch_pair_test_list(L, kc / 3, kc % 3 == 0 ? 2 : kc % 3 == 1 ? 4 : 8, fid % 2 == 1, d_slots + runs[f].first,
-                                          (uint32_t)runs[f].second));
-            timer_dispatched(c, &t);
-            L.ev_start = L.ev_stop = nullptr;
-        }
-        timer_begin(c, &t, kTimeCompact);
-        HIP_TRY(launch_compact(L));
-        timer_end(c, &t);
-        // speculatively pack the output now (it is redone if another window follows): the GPU packs while the
-        // host wakes up and reads the status
-        HIP_TRY(launch_pack(L, (uint64_t*)d_packed_v, (uint64_t*)d_packed_off_v, nullptr));
-        const double w0 = host_profile ? host_us() : 0.0;
-        if (host_profile && !hp[2]) hp[2] = w0;  // first window enqueued
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        if (host_profile) hp_wait += host_us() - w0;
+        const double w0 = g_host_profile ? host_us() : 0.0;
+        HIP_TRY(hipStreamSynchronize(st));
+        if (g_host_profile) jb.hp_wait += host_us() - w0;
         // capacity overflow can only come from a wrong min_len bound; report it loudly
-        if (((const volatile uint64_t*)h_io)[kCntN]) return fail(DSY_ECAPACITY, "internal: a claim overflowed its output capacity");
-        const volatile uint8_t* done = h_io + kHostHead;
-        size_t a = 0;
-        for (auto& fa : fam_active) {
+        if (((const volatile uint64_t*)jb.h_io)[kCntN]) return fail(DSY_ECAPACITY, "internal: a claim overflowed its output capacity");
+        const volatile uint8_t* done = jb.h_io + kHostHead;
+        size_t a = 0, left = 0;
+        for (auto& fa : jb.fam_active) {
             size_t keep = 0;
             for (uint32_t r : fa)
                 if (!done[a++]) fa[keep++] = r;
             fa.resize(keep);
+            left += keep;
         }
+        if (!left) break;
+        int rc = job_window(c, sl);
+        if (rc) return rc;
     }
     uint64_t h_tot[kCntN];
-    for (uint32_t k = 0; k < kCntN; ++k) h_tot[k] = ((const volatile uint64_t*)h_io)[k];
-    if (!ran) HIP_TRY(launch_pack(L, (uint64_t*)d_packed_v, (uint64_t*)d_packed_off_v, nullptr));
+    if (!jb.ran) {
+        HIP_TRY(launch_pack(L, (uint64_t*)jb.d_packed, (uint64_t*)jb.d_packed_off, nullptr));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    for (uint32_t k = 0; k < kCntN; ++k) h_tot[k] = ((const volatile uint64_t*)jb.h_io)[k];
     timers_collect_lazy(c);
     c->blocks[kTimePairTest] += h_tot[kCntBlocks];
     c->bytes[kTimePairTest] += h_tot[kCntBytes];
     c->useful[kTimePairTest] += h_tot[kCntUseful];
     c->slots[kTimePairTest] += h_tot[kCntSlots];
     *total_pairs = h_tot[kCntPairs];
-    *d_packed = (uint64_t*)d_packed_v;
-    *d_packed_off = (uint64_t*)d_packed_off_v;
-    if (host_profile) {
-        hp[3] = host_us();
-        fprintf(stderr, "host_profile R=%u stage=%.1f enqueue=%.1f wait=%.1f total=%.1f\n", R, hp[1] - hp[0],
-                hp[2] ? hp[2] - hp[1] : 0.0, hp_wait, hp[3] - hp[0]);
+    *d_packed = (uint64_t*)jb.d_packed;
+    *d_packed_off = (uint64_t*)jb.d_packed_off;
+    if (g_host_profile) {
+        jb.hp[3] = host_us();
+        fprintf(stderr, "host_profile R=%u stage=%.1f enqueue=%.1f wait=%.1f total=%.1f\n", jb.R, jb.hp[1] - jb.hp[0],
+                jb.hp[2] ? jb.hp[2] - jb.hp[1] : 0.0, jb.hp_wait, jb.hp[3] - jb.hp[0]);
     }
     return DSY_OK;
+}
+
+static RespondSlot& sync_slot(dsy_ctx* c) {
+    RespondSlot& sl = c->rs[0];
+    sl.stream = c->stream;
+    return sl;
+}
+
+static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, uint32_t R, const uint8_t* d_filters,
+                        uint64_t filters_len, const dsy_meta* metas, uint32_t J, uint64_t responder_gt,
+                        int include_inactive, int64_t byte_limit, uint64_t seed, uint64_t** d_packed,
+                        uint64_t** d_packed_off, uint64_t* total_pairs) {
+    if (c->inflight()) return fail(DSY_EINVAL, "submitted responder batches are in flight: dsy_sync_respond_wait them first");
+    RespondSlot& sl = sync_slot(c);
+    int rc = job_start(c, sl, s, reqs, R, d_filters, filters_len, metas, J, responder_gt, include_inactive, byte_limit,
+                       seed);
+    if (rc) return rc;
+    return job_finish(c, sl, d_packed, d_packed_off, total_pairs);
 }
 
 int dsy_sync_respond(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, uint32_t R, const uint8_t* filters,
@@ -1909,6 +2037,59 @@ int dsy_sync_respond_dev(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs
     int rc = respond_core(c, s, reqs, R, d_filters, 0, metas, nmeta, responder_global_time, include_inactive,
                           byte_limit, random_seed, &d_packed, &d_off, &pairs);
     if (rc) return rc;
+    if (d_out_idx) *d_out_idx = d_packed;
+    if (d_out_offsets) *d_out_offsets = d_off;
+    if (out_total_pairs) *out_total_pairs = pairs;
+    return DSY_OK;
+}
+
+int dsy_sync_respond_submit(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, uint32_t R,
+                            const uint8_t* d_filters, const dsy_meta* metas, uint32_t nmeta,
+                            uint64_t responder_global_time, int include_inactive, int64_t byte_limit,
+                            uint64_t random_seed, uint64_t* out_ticket) {
+    if (!c || !s || (R && (!reqs || !d_filters)) || (nmeta && !metas) || !out_ticket)
+        return fail(DSY_EINVAL, "NULL argument");
+    Guard g(c);
+    int k = !c->rs[0].busy ? 0 : !c->rs[1].busy ? 1 : -1;
+    if (k < 0) return fail(DSY_EINVAL, "two responder batches are in flight: dsy_sync_respond_wait one first");
+    RespondSlot& sl = c->rs[k];
+    if (k == 0) {
+        sl.stream = c->stream;
+    } else {
+        if (!sl.stream) HIP_TRY(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
+        // the batch sees everything queued on the ctx stream before it (store builds, filter uploads)
+        int rc = xev_get(c);
+        if (rc) return rc;
+        HIP_TRY(hipEventRecord(c->xev, c->stream));
+        HIP_TRY(hipStreamWaitEvent(sl.stream, c->xev, 0));
+    }
+    int rc = job_start(c, sl, s, reqs, R, d_filters, 0, metas, nmeta, responder_global_time, include_inactive,
+                       byte_limit, random_seed);
+    if (rc) {
+        hipStreamSynchronize(sl.stream);  // whatever was enqueued before the failure
+        return rc;
+    }
+    sl.busy = true;
+    sl.ticket = c->next_ticket++;
+    *out_ticket = sl.ticket;
+    return DSY_OK;
+}
+
+int dsy_sync_respond_wait(dsy_ctx* c, uint64_t ticket, const uint64_t** d_out_idx, const uint64_t** d_out_offsets,
+                          uint64_t* out_total_pairs) {
+    if (!c) return fail(DSY_EINVAL, "NULL argument");
+    Guard g(c);
+    RespondSlot* sl = nullptr;
+    for (auto& x : c->rs)
+        if (x.busy && x.ticket == ticket) sl = &x;
+    if (!sl) return fail(DSY_EINVAL, "ticket %llu is not in flight", (unsigned long long)ticket);
+    uint64_t *d_packed, *d_off, pairs = 0;
+    int rc = job_finish(c, *sl, &d_packed, &d_off, &pairs);
+    sl->busy = false;
+    if (rc) {
+        hipStreamSynchronize(sl->stream);
+        return rc;
+    }
     if (d_out_idx) *d_out_idx = d_packed;
     if (d_out_offsets) *d_out_offsets = d_off;
     if (out_total_pairs) *out_total_pairs = pairs;

@@ -270,6 +270,21 @@ int dsy_sync_respond_dev(dsy_ctx* ctx, const dsy_store* store, const dsy_request
                          uint64_t random_seed, const uint64_t** d_out_idx, const uint64_t** d_out_offsets,
                          uint64_t* out_total_pairs);
 
+/* Pipelined form of dsy_sync_respond_dev for a stream of batches (a responder serving receive batch after receive
+ * batch): submit validates and stages the claims and enqueues the batch's first window without waiting; wait finishes
+ * it (the further windows its unfinished claims need) and returns what dsy_sync_respond_dev returns.  Up to two
+ * batches are in flight per ctx, each with its own workspace and stream, so one batch's selection and the host's
+ * staging overlap the other's hashing.  Results are the same as the synchronous call's; a batch's output buffers stay
+ * valid until the next-but-one submit.  While a batch is in flight the store must not change (append, prune, delete,
+ * replace and free return DSY_EINVAL) and the synchronous responder calls return DSY_EINVAL; d_filters must stay valid
+ * until wait returns.  A third submit returns DSY_EINVAL. */
+int dsy_sync_respond_submit(dsy_ctx* ctx, const dsy_store* store, const dsy_request* reqs, uint32_t R,
+                            const uint8_t* d_filters, const dsy_meta* metas, uint32_t nmeta,
+                            uint64_t responder_global_time, int include_inactive, int64_t byte_limit,
+                            uint64_t random_seed, uint64_t* out_ticket);
+int dsy_sync_respond_wait(dsy_ctx* ctx, uint64_t ticket, const uint64_t** d_out_idx, const uint64_t** d_out_offsets,
+                          uint64_t* out_total_pairs);
+
 /* Union of G partial filters of one (m, k, prefix) built over disjoint key shards (the large-filter
  * build shards keys over GPUs; RCCL reduces only sum/prod/min/max, so the partials are all-gathered over xGMI and
  * OR-ed here): d_out[w] = OR_g d_parts[g * words + w].  Device pointers; enqueued on the ctx stream. */
