@@ -175,8 +175,9 @@ def parse():
     ap.add_argument("--cpu-pairs", type=int, default=100_000,
                     help="responder CPU baselines: (claim, packet) pairs hashed in the 1-core sample (BASELINE.md:47)")
     ap.add_argument("--seed", type=int, default=7)
-    ap.add_argument("--pipeline", type=int, default=1,
-                    help="responder legs: 1 serve the batches two in flight (submit / wait), 0 one at a time")
+    ap.add_argument("--pipeline", type=int, default=3,
+                    help="responder legs: batches in flight (dsy_sync_respond_submit / _wait, at most 3); 1 one at a time "
+                         "(dsy_sync_respond_dev)")
     ap.add_argument("--window", type=int, default=0, help="cap on the responder's window (pairs per claim; 0: default)")
     ap.add_argument("--sim-peers", type=int, default=1_000_000, help="config 3 gossip simulator peers (0: skip)")
     ap.add_argument("--sim-universe", type=int, default=10_000)
@@ -268,7 +269,7 @@ def run(args, rank, world, local):
     if args.window:
         ctx.set_window(args.window)
     batches = Batches(lib, ctx, store, reqs, R, d_filters.data_ptr(), metas, 1, N, args.byte_limit)
-    pipe = bool(args.pipeline)
+    pipe = args.pipeline
     step = batches.step
 
     batches.run(args.warmup, pipe)
@@ -291,14 +292,14 @@ def run(args, rank, world, local):
     ctx.reset_timing()
     ctx.set_timing(True, only=[_native.TIME_PAIR_TEST])
     t1 = time.perf_counter()
-    serial_pairs = batches.run(args.steps, False)
+    serial_pairs = batches.run(args.steps, 1)
     serial_s = time.perf_counter() - t1
     ctx.set_timing(False)
     kt = ctx.kernel_time(_native.TIME_PAIR_TEST)
     ctx.reset_timing()
     ctx.set_timing(True, only=[_native.TIME_SELECT, _native.TIME_COMPACT])
     n_side = min(max(args.steps, 1), 5)
-    batches.run(n_side, False)
+    batches.run(n_side, 1)
     ctx.synchronize()
     ctx.set_timing(False)
     sel = ctx.kernel_time(_native.TIME_SELECT)
@@ -415,8 +416,9 @@ def run(args, rank, world, local):
             "value_counts": "(claim, packet) pairs the reference hashes+tests for these claims: its lazy not_filter "
                             "stops at the packet that spends the 5 KiB budget (community.py:2559-2567)",
             "pairs_hashed_per_s": round(total_pairs / elapsed, 1),
-            "pipeline": "two batches in flight (dsy_sync_respond_submit / _wait): one batch's selection and the host's "
-                        "staging overlap the other's hashing" if pipe else "one batch at a time (dsy_sync_respond_dev)",
+            "pipeline": "%d batches in flight (dsy_sync_respond_submit / _wait): one batch's selection, another's "
+                        "compaction and the host's staging overlap the hashing" % pipe if pipe > 1
+                        else "one batch at a time (dsy_sync_respond_dev)",
             "serial_ms_per_step": round(serial_s / max(args.steps, 1) * 1e3, 3),
             "claims_per_s": round(R * world * args.steps / elapsed, 1),
             "roofline": roofline,
@@ -466,15 +468,17 @@ class Batches(object):
         _native.check(self.lib.dsy_sync_respond_wait(self.h, ticket, *self.wait_tail))
         return self.pairs.value
 
-    def run(self, k, pipeline=True):
-        if not pipeline:
+    def run(self, k, depth=2):
+        """k batches, `depth` in flight (1: the synchronous call)."""
+        if depth <= 1:
             return sum(self.step() for _ in range(k))
-        total = 0
-        pending = self.submit() if k else None
-        for i in range(k):
-            nxt = self.submit() if i + 1 < k else None
-            total += self.wait(pending)
-            pending = nxt
+        total, pending = 0, []
+        for _ in range(k):
+            pending.append(self.submit())
+            if len(pending) == depth:
+                total += self.wait(pending.pop(0))
+        for t in pending:
+            total += self.wait(t)
         return total
 
 
@@ -488,7 +492,7 @@ def sha1_respond(args, ctx, lib, store, N, dev, blob, offsets, total_bytes, meta
     R = args.claims
     reqs, claims, fblob, d_filters, capacity = make_claims(ctx, lib, store, N, R, rng, 512 * 8, 0.001, b"x", dev)
     batches = Batches(lib, ctx, store, reqs, R, d_filters.data_ptr(), metas, 1, N, args.byte_limit)
-    pipe = bool(args.pipeline)
+    pipe = args.pipeline
     steps = max(args.steps, 1)
     batches.run(args.warmup, pipe)
     ctx.synchronize()
@@ -502,7 +506,7 @@ def sha1_respond(args, ctx, lib, store, N, dev, blob, offsets, total_bytes, meta
     ctx.reset_timing()
     ctx.set_timing(True, only=[_native.TIME_PAIR_TEST])
     t1 = time.perf_counter()
-    serial_total = batches.run(steps, False)
+    serial_total = batches.run(steps, 1)
     serial_s = time.perf_counter() - t1
     ctx.set_timing(False)
     kt = ctx.kernel_time(_native.TIME_PAIR_TEST)
@@ -1328,7 +1332,7 @@ def heavy_tail(args, ctx, lib, dev, rank, world, dist):
     if args.window:
         ctx.set_window(args.window)
     batches = Batches(lib, ctx, store, reqs, R, d_filters.data_ptr(), metas, 1, G_MAX, args.byte_limit)
-    pipe = bool(args.pipeline)
+    pipe = args.pipeline
     batches.run(2, pipe)
     steps = max(3, args.steps // 4)
     ctx.synchronize()
@@ -1344,7 +1348,7 @@ def heavy_tail(args, ctx, lib, dev, rank, world, dist):
     ctx.reset_timing()
     ctx.set_timing(True)
     t1 = time.perf_counter()
-    batches.run(steps, False)
+    batches.run(steps, 1)
     serial_dt = time.perf_counter() - t1
     ctx.set_timing(False)
     kt = ctx.kernel_time(_native.TIME_PAIR_TEST)

@@ -94,11 +94,16 @@ struct RespondJob {
     double hp_wait = 0;
 };
 
-// A responder slot: its own workspace, stream and job, so two batches can be in flight (dsy_sync_respond_submit).
-// Slot 0 runs on the ctx stream (the synchronous entry points use it), slot 1 on a stream of its own.
+// A responder slot: its own workspace and job, so several batches can be in flight (dsy_sync_respond_submit).  Every
+// batch runs on the ctx stream: the GPU executes the batches back to back, the next batch's selection right behind
+// this one's packing, while the host stages the next batch and waits for this one on its own event (ev_done, recorded
+// after each window's packing) instead of on the stream.  Measured and dropped (same box, tools/pipe_timeline.py):
+// each slot on streams of its own, and selection / compaction on high-priority streams beside a low-priority hashing
+// stream -- concurrent launches only slowed each other (a k_compact beside a hashing launch took 50-145 us instead of
+// 6, the hashing launch 280-355 us instead of 210).
 struct RespondSlot {
     Workspace w;
-    hipStream_t stream = nullptr;
+    hipEvent_t ev_done = nullptr;
     bool busy = false;       // submitted, not yet waited for
     uint64_t ticket = 0;
     RespondJob job;
@@ -109,7 +114,8 @@ struct dsy_ctx {
     hipStream_t stream = nullptr;
     std::mutex mu;
     Workspace main;  // every entry point but the responder's
-    RespondSlot rs[2];
+    static constexpr int kSlots = 3;  // responder batches in flight at most (dsy_sync_respond_submit)
+    RespondSlot rs[kSlots];
     uint64_t next_ticket = 1;
     uint32_t max_grid = 2048;
     int bloom_diag = 0;  // DSY_BLOOM_DIAG at creation: single-filter ceiling diagnostics (k_bloom DIAG)
@@ -135,7 +141,11 @@ struct dsy_ctx {
     void* sim_acc = nullptr;
     bool sim_pending = false;
     bool sim_overflow = false;
-    int inflight() const { return (int)rs[0].busy + (int)rs[1].busy; }
+    int inflight() const {
+        int n = 0;
+        for (const auto& x : rs) n += x.busy;
+        return n;
+    }
 };
 
 struct dsy_store {
@@ -489,10 +499,7 @@ int dsy_ctx_destroy(dsy_ctx* c) {
         hipStreamSynchronize(c->stream);
         timers_collect(c);
         for (auto& sl : c->rs) {
-            if (sl.stream && sl.stream != c->stream) {
-                hipStreamSynchronize(sl.stream);
-                hipStreamDestroy(sl.stream);
-            }
+            if (sl.ev_done) hipEventDestroy(sl.ev_done);
             sl.w.release();
         }
         c->main.release();
@@ -1616,7 +1623,8 @@ static const bool g_host_profile = getenv("DSY_HOST_PROFILE") != nullptr;
 static int job_window(dsy_ctx* c, RespondSlot& sl) {
     RespondJob& jb = sl.job;
     RespondLaunch& L = jb.L;
-    const hipStream_t st = sl.stream;
+    const hipStream_t st = c->stream;
+    L.stream = st;
     std::vector<std::pair<size_t, size_t>> runs;  // per family: (first slot, slots)
     size_t n_act = 0;
     for (auto& fa : jb.fam_active) {
@@ -1694,6 +1702,7 @@ static int job_window(dsy_ctx* c, RespondSlot& sl) {
     // speculatively pack the output now (it is redone if another window follows): the GPU packs while the host wakes
     // up and reads the status
     HIP_TRY(launch_pack(L, (uint64_t*)jb.d_packed, (uint64_t*)jb.d_packed_off, nullptr));
+    HIP_TRY(hipEventRecord(sl.ev_done, st));
     if (g_host_profile && !jb.hp[2]) jb.hp[2] = host_us();  // first window enqueued
     return DSY_OK;
 }
@@ -1704,7 +1713,8 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
                      uint64_t responder_gt, int include_inactive, int64_t byte_limit, uint64_t seed) {
     sl.job = RespondJob{};
     RespondJob& jb = sl.job;
-    const hipStream_t st = sl.stream;
+    const hipStream_t st = c->stream;
+    if (!sl.ev_done) HIP_TRY(hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming));
     if (g_host_profile) jb.hp[0] = host_us();
     // ---- validate claims (payload.py:89-101, conversion.py:772-789) and their filters; group them by hash family
     // (kind x chunk width: one pair-test launch per family)
@@ -1937,14 +1947,14 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
 static int job_finish(dsy_ctx* c, RespondSlot& sl, uint64_t** d_packed, uint64_t** d_packed_off, uint64_t* total_pairs) {
     RespondJob& jb = sl.job;
     RespondLaunch& L = jb.L;
-    const hipStream_t st = sl.stream;
+    const hipStream_t st = c->stream;
     constexpr size_t kHostHead = 128;
     for (;;) {
         size_t n_act = 0;
         for (auto& fa : jb.fam_active) n_act += fa.size();
         if (!n_act) break;
         const double w0 = g_host_profile ? host_us() : 0.0;
-        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipEventSynchronize(sl.ev_done));  // this job's window, not what later batches queued behind it
         if (g_host_profile) jb.hp_wait += host_us() - w0;
         // capacity overflow can only come from a wrong min_len bound; report it loudly
         if (((const volatile uint64_t*)jb.h_io)[kCntN]) return fail(DSY_ECAPACITY, "internal: a claim overflowed its output capacity");
@@ -1983,11 +1993,7 @@ static int job_finish(dsy_ctx* c, RespondSlot& sl, uint64_t** d_packed, uint64_t
     return DSY_OK;
 }
 
-static RespondSlot& sync_slot(dsy_ctx* c) {
-    RespondSlot& sl = c->rs[0];
-    sl.stream = c->stream;
-    return sl;
-}
+static RespondSlot& sync_slot(dsy_ctx* c) { return c->rs[0]; }
 
 static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, uint32_t R, const uint8_t* d_filters,
                         uint64_t filters_len, const dsy_meta* metas, uint32_t J, uint64_t responder_gt,
@@ -2050,23 +2056,15 @@ int dsy_sync_respond_submit(dsy_ctx* c, const dsy_store* s, const dsy_request* r
     if (!c || !s || (R && (!reqs || !d_filters)) || (nmeta && !metas) || !out_ticket)
         return fail(DSY_EINVAL, "NULL argument");
     Guard g(c);
-    int k = !c->rs[0].busy ? 0 : !c->rs[1].busy ? 1 : -1;
-    if (k < 0) return fail(DSY_EINVAL, "two responder batches are in flight: dsy_sync_respond_wait one first");
+    int k = -1;
+    for (int i = 0; i < dsy_ctx::kSlots && k < 0; ++i)
+        if (!c->rs[i].busy) k = i;
+    if (k < 0) return fail(DSY_EINVAL, "%d responder batches are in flight: dsy_sync_respond_wait one first", dsy_ctx::kSlots);
     RespondSlot& sl = c->rs[k];
-    if (k == 0) {
-        sl.stream = c->stream;
-    } else {
-        if (!sl.stream) HIP_TRY(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
-        // the batch sees everything queued on the ctx stream before it (store builds, filter uploads)
-        int rc = xev_get(c);
-        if (rc) return rc;
-        HIP_TRY(hipEventRecord(c->xev, c->stream));
-        HIP_TRY(hipStreamWaitEvent(sl.stream, c->xev, 0));
-    }
     int rc = job_start(c, sl, s, reqs, R, d_filters, 0, metas, nmeta, responder_global_time, include_inactive,
                        byte_limit, random_seed);
     if (rc) {
-        hipStreamSynchronize(sl.stream);  // whatever was enqueued before the failure
+        hipStreamSynchronize(c->stream);  // whatever was enqueued before the failure
         return rc;
     }
     sl.busy = true;
@@ -2087,7 +2085,7 @@ int dsy_sync_respond_wait(dsy_ctx* c, uint64_t ticket, const uint64_t** d_out_id
     int rc = job_finish(c, *sl, &d_packed, &d_off, &pairs);
     sl->busy = false;
     if (rc) {
-        hipStreamSynchronize(sl->stream);
+        hipStreamSynchronize(c->stream);
         return rc;
     }
     if (d_out_idx) *d_out_idx = d_packed;

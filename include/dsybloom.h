@@ -272,12 +272,14 @@ int dsy_sync_respond_dev(dsy_ctx* ctx, const dsy_store* store, const dsy_request
 
 /* Pipelined form of dsy_sync_respond_dev for a stream of batches (a responder serving receive batch after receive
  * batch): submit validates and stages the claims and enqueues the batch's first window without waiting; wait finishes
- * it (the further windows its unfinished claims need) and returns what dsy_sync_respond_dev returns.  Up to two
- * batches are in flight per ctx, each with its own workspace and stream, so one batch's selection and the host's
- * staging overlap the other's hashing.  Results are the same as the synchronous call's; a batch's output buffers stay
- * valid until the next-but-one submit.  While a batch is in flight the store must not change (append, prune, delete,
- * replace and free return DSY_EINVAL) and the synchronous responder calls return DSY_EINVAL; d_filters must stay valid
- * until wait returns.  A third submit returns DSY_EINVAL. */
+ * it (the further windows its unfinished claims need) and returns what dsy_sync_respond_dev returns.  Up to three
+ * batches are in flight per ctx, each with its own workspace; they run back to back on the ctx stream, so the GPU
+ * goes from one batch's packing straight into the next one's selection while the host stages batches and collects
+ * results.  Results are the same as the synchronous call's; a batch's
+ * output buffers stay valid until its slot is reused by a later submit (after two more submits at the earliest).
+ * While a batch is in flight the store must not change (append, prune, delete, replace and free return DSY_EINVAL)
+ * and the synchronous responder calls return DSY_EINVAL; d_filters must stay valid until wait returns.  A fourth
+ * submit returns DSY_EINVAL. */
 int dsy_sync_respond_submit(dsy_ctx* ctx, const dsy_store* store, const dsy_request* reqs, uint32_t R,
                             const uint8_t* d_filters, const dsy_meta* metas, uint32_t nmeta,
                             uint64_t responder_global_time, int include_inactive, int64_t byte_limit,

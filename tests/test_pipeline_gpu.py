@@ -1,6 +1,6 @@
-"""The pipelined responder (dsy_sync_respond_submit / dsy_sync_respond_wait): two batches in flight on their own
-workspaces and streams must answer exactly what the synchronous call answers, batch by batch, and the ctx must
-refuse what would race with them (a third batch, a store change, a synchronous call)."""
+"""The pipelined responder (dsy_sync_respond_submit / dsy_sync_respond_wait): up to three batches in flight on
+their own workspaces and streams must answer exactly what the synchronous call answers, batch by batch, and the ctx
+must refuse what would race with them (a fourth batch, a store change, a synchronous call)."""
 import ctypes
 
 import numpy as np
@@ -38,7 +38,7 @@ def _setup(n=30_000, seed=3):
     metas = [MetaMessage("a", 1, SyncDistribution("ASC", 128)), MetaMessage("d", 2, SyncDistribution("DESC", 200))]
     com = SyncCommunity(store, metas, global_time=12_000)
     batches = []
-    for b in range(3):
+    for b in range(4):
         claims = []
         for i in range(64 + 32 * b):
             lo = int(rng.integers(1, 11_000))
@@ -79,50 +79,58 @@ def _wait(ctx, ticket, R):
 
 
 @pytest.mark.parametrize("byte_limit", [5120, 60_000])
-def test_two_in_flight_equal_synchronous(byte_limit):
+def test_in_flight_batches_equal_synchronous(byte_limit):
     store, com, claim_batches = _setup()
     ctx = store.ctx
     want = [[r.tolist() for r in com.respond(c, byte_limit=byte_limit, random_seed=7)] for c in claim_batches]
     bs = [_Batch(com, c) for c in claim_batches]
-    rc0, t0 = _submit(ctx, store, com, bs[0], byte_limit)
-    rc1, t1 = _submit(ctx, store, com, bs[1], byte_limit)
-    assert rc0 == 0 and rc1 == 0 and t0 != t1
-    # a third batch, a store change and a synchronous call would race with the two in flight
-    rc2, _ = _submit(ctx, store, com, bs[2], byte_limit)
-    assert rc2 == _native.DSY_EINVAL
+    tickets = []
+    for b in bs[:3]:
+        rc, t = _submit(ctx, store, com, b, byte_limit)
+        assert rc == 0
+        tickets.append(t)
+    assert len(set(tickets)) == 3
+    # a fourth batch, a store change and a synchronous call would race with the three in flight
+    rc3, _ = _submit(ctx, store, com, bs[3], byte_limit)
+    assert rc3 == _native.DSY_EINVAL
     with pytest.raises(_native.DsyError):
-        com.respond(claim_batches[2], byte_limit=byte_limit, random_seed=7)
+        com.respond(claim_batches[3], byte_limit=byte_limit, random_seed=7)
     one = np.asarray([10], dtype=np.uint64)
     assert ctx.lib.dsy_store_delete(ctx.handle, store.handle, one.ctypes.data, 1, None) == _native.DSY_EINVAL
-    got0, pairs0 = _wait(ctx, t0, bs[0].R)
-    assert got0 == want[0]
-    rc2, t2 = _submit(ctx, store, com, bs[2], byte_limit)  # a slot is free again
-    assert rc2 == 0
-    got1, _ = _wait(ctx, t1, bs[1].R)
-    got2, _ = _wait(ctx, t2, bs[2].R)
+    got1, _ = _wait(ctx, tickets[1], bs[1].R)  # out of submission order
     assert got1 == want[1]
+    rc3, t3 = _submit(ctx, store, com, bs[3], byte_limit)  # a slot is free again
+    assert rc3 == 0
+    got0, pairs0 = _wait(ctx, tickets[0], bs[0].R)
+    got3, _ = _wait(ctx, t3, bs[3].R)
+    got2, _ = _wait(ctx, tickets[2], bs[2].R)
+    assert got0 == want[0]
     assert got2 == want[2]
+    assert got3 == want[3]
     assert pairs0 > 0
     with pytest.raises(_native.DsyError):
-        _wait(ctx, t2, bs[2].R)  # already waited for
+        _wait(ctx, t3, bs[3].R)  # already waited for
     # nothing in flight: the synchronous call runs again
     assert [r.tolist() for r in com.respond(claim_batches[0], byte_limit=byte_limit, random_seed=7)] == want[0]
 
 
-def test_pipelined_stream_of_batches():
-    """Ten batches served two deep, as bench.py does: every answer equals the synchronous one."""
+@pytest.mark.parametrize("depth", [2, 3])
+def test_pipelined_stream_of_batches(depth):
+    """Ten batches served `depth` deep, as bench.py does: every answer equals the synchronous one."""
     store, com, claim_batches = _setup(seed=4)
     ctx = store.ctx
     want = [[r.tolist() for r in com.respond(c, byte_limit=5120, random_seed=7)] for c in claim_batches]
     bs = [_Batch(com, c) for c in claim_batches]
-    order = [i % 3 for i in range(10)]
-    pending = None
-    for k, i in enumerate(order):
+    pending = []
+    for k in range(10):
+        i = k % len(bs)
         rc, t = _submit(ctx, store, com, bs[i], 5120)
         assert rc == 0
-        if pending is not None:
-            got, _ = _wait(ctx, pending[1], bs[pending[0]].R)
-            assert got == want[pending[0]], k
-        pending = (i, t)
-    got, _ = _wait(ctx, pending[1], bs[pending[0]].R)
-    assert got == want[pending[0]]
+        pending.append((i, t))
+        if len(pending) == depth:
+            j, tj = pending.pop(0)
+            got, _ = _wait(ctx, tj, bs[j].R)
+            assert got == want[j], k
+    for j, tj in pending:
+        got, _ = _wait(ctx, tj, bs[j].R)
+        assert got == want[j]
