@@ -90,6 +90,7 @@ SIGNATURES = {
     "dsy_store_index_members": (ctypes.c_int, [_P, _P, _P, _P, _U64]),
     "dsy_store_prune": (ctypes.c_int, [_P, _P, _U32, _U64, _PU64]),
     "dsy_store_delete": (ctypes.c_int, [_P, _P, _P, _U64, _PU64]),
+    "dsy_store_set_undone": (ctypes.c_int, [_P, _P, _P, _U64, _P, _P, ctypes.c_int, _PU64]),
     "dsy_dup_check": (ctypes.c_int, [_P, _P, _P, _P, _P, _U64, _P, _U64, _P, _P, _P]),
     "dsy_store_replace": (ctypes.c_int, [_P, _P, _P, _P, _U64, _P, _U64]),
     "dsy_bloom_add_rows": (ctypes.c_int, [_P, ctypes.POINTER(BloomParams), _P, _P, _U64, _P]),

@@ -307,6 +307,34 @@ class SyncCommunity(object):
         if replaces:
             self._store.replace_packet([r for r, _ in replaces], [p for _, p in replaces])
 
+    # ---------------------------------------------------------------------------------------- undo / redo
+    def on_undo(self, entries):
+        """The UPDATE of Community.on_undo (community.py:3457-3481) for a batch of undo messages: entries are
+        (undo packet id, member, global_time) -- for an undo message its own packet id and the payload's member and
+        global time; for a DispersyDuplicatedUndo the lower undo's packet id and the higher one's member and global
+        time -- as `UPDATE sync SET undone = ? WHERE community = ? AND member = ? AND global_time = ?`, executed in
+        order.  The undone packets leave the responder's index; their rows stay for the duplicate check's undo proof.
+        (The meta's undo_callback is the application's.)  Returns the number of rows whose undone-ness changed."""
+        entries = list(entries)
+        if not entries:
+            return 0
+        rows = self._store.rows_of_keys([e[1] for e in entries], [e[2] for e in entries])
+        hit = rows >= 0
+        return self._store.set_undone(rows[hit], np.asarray([e[0] for e in entries], dtype=np.int64)[hit])
+
+    def update_undone(self, packet_ids, undone):
+        """_update_timerange's UPDATEs (community.py:3633-3642): `UPDATE sync SET undone = 1 WHERE id = ?` for the
+        messages the timeline no longer allows (undone=1) and `... undone = 0 WHERE id = ?` for the ones it allows
+        again (undone=0).  Which messages those are is the timeline's decision (permissions, out of this path).
+        Returns the number of rows whose undone-ness changed."""
+        rows = []
+        for pid in packet_ids:
+            try:
+                rows.append(self._store.row_of_id(int(pid)))
+            except KeyError:
+                pass
+        return self._store.set_undone(np.asarray(rows, dtype=np.int64), int(undone))
+
     def _highest(self, meta_id, member):
         """SELECT MAX(global_time), MAX(sequence), COUNT(*) FROM sync WHERE member = ? AND meta_message = ?
         (dispersy.py:959-961, :1010-1012) -> (last_global_time or 0, last_sequence or 0)."""

@@ -964,29 +964,23 @@ int dup_insert(dsy_ctx* c, dsy_store* s, const uint64_t* member, const uint64_t*
 
 }  // namespace
 
-int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blob_len, const uint64_t* offsets,
-                     uint64_t a, const uint64_t* gt, const uint32_t* meta, const uint64_t* member) {
-    if (!c || !s || !offsets || (a && (!gt || !meta || (blob_len && !blob)))) return fail(DSY_EINVAL, "NULL argument");
-    if (s->ctx != c) return fail(DSY_EINVAL, "store belongs to another context");
-    if (s->dup && a && !member) return fail(DSY_EINVAL, "the store has a (member, global_time) table: members required");
-    int rc = check_offsets(offsets, a, blob_len);
-    if (rc) return rc;
-    if (a == 0) return DSY_OK;
-    Guard g(c);
-    if (c->inflight()) return fail(DSY_EINVAL, "the store cannot change while submitted responder batches are in flight");
-    const uint64_t n0 = s->n, base0 = offsets[0], add = offsets[a] - base0;
-
-    // the new rows in index order (meta_message, global_time, rowid): argument order breaks ties
+// New live-index entries: rows (store positions, any order) with their meta and global time join the index at their
+// (meta_message, global_time, row) place -- appended rows (positions past every stored row: after the stored rows of
+// equal global time) and redone rows alike -- merged on the device into the spare buffer pair, which then becomes the
+// index.  check_present: fail (index unchanged) when a row is in the index already.  Caller holds the ctx lock.
+static int live_insert(dsy_ctx* c, dsy_store* s, const uint32_t* meta, const uint64_t* gt, const uint64_t* row,
+                       uint64_t a, bool check_present) {
+    if (!a) return DSY_OK;
+    // the new entries in index order (meta_message, global_time, row)
     std::vector<uint64_t> ord(a);
     for (uint64_t j = 0; j < a; ++j) ord[j] = j;
-    std::stable_sort(ord.begin(), ord.end(), [&](uint64_t x, uint64_t y) {
-        return meta[x] != meta[y] ? meta[x] < meta[y] : gt[x] < gt[y];
+    std::sort(ord.begin(), ord.end(), [&](uint64_t x, uint64_t y) {
+        return meta[x] != meta[y] ? meta[x] < meta[y] : gt[x] != gt[y] ? gt[x] < gt[y] : row[x] < row[y];
     });
-    // each new row's meta segment in the old live index; a new meta sits after every smaller meta's segment
+    // each entry's meta segment in the old live index; a new meta sits after every smaller meta's segment
     std::vector<std::pair<uint32_t, std::pair<uint64_t, uint64_t>>> old(s->segs.begin(), s->segs.end());
     std::sort(old.begin(), old.end());
     std::vector<IngestRow> rows(a);
-    uint64_t minlen = ~0ull;
     for (uint64_t t = 0; t < a; ++t) {
         const uint64_t j = ord[t];
         auto it = s->segs.find(meta[j]);
@@ -999,9 +993,94 @@ int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blo
                 if (e.first < meta[j]) sa = std::max(sa, e.second.second);
             sb = sa;
         }
-        rows[t] = IngestRow{gt[j], sa, sb, n0 + j};
-        minlen = std::min(minlen, offsets[j + 1] - offsets[j]);
+        rows[t] = IngestRow{gt[j], sa, sb, row[j]};
     }
+    const size_t b_rows = a * sizeof(IngestRow);
+    void* d_up;
+    int rc;
+    if ((rc = ws_get(c, "live_insert", b_rows + a * 8 + 64, &d_up))) return rc;
+    uint8_t* up_rows = (uint8_t*)d_up;
+    unsigned int* d_present = (unsigned int*)(up_rows + b_rows + a * 8);
+    HIP_TRY(hipMemcpyAsync(up_rows, rows.data(), b_rows, hipMemcpyHostToDevice, c->stream));
+    if (check_present) HIP_TRY(hipMemsetAsync(d_present, 0, 4, c->stream));
+    // the live index, merged into fresh buffers (the old ones are read by the merge); double-buffered: the previous
+    // merge's index becomes the next one's target, so a steady stream of appends allocates nothing
+    const uint64_t live = s->n_live + a;
+    if (s->spare_cap < live) {
+        store_release(s, s->spare_gt);
+        store_release(s, s->spare_row);
+        s->spare_gt = s->spare_row = nullptr;
+        s->spare_cap = 0;
+        const uint64_t cap = grown(live, s->n_live);
+        void *pg, *pr;
+        if (hipMalloc(&pg, cap * 8) != hipSuccess) return fail(DSY_ENOMEM, "store live index growth");
+        s->owned.push_back(pg);
+        if (hipMalloc(&pr, cap * 8) != hipSuccess) { store_release(s, pg); return fail(DSY_ENOMEM, "store live index growth"); }
+        s->owned.push_back(pr);
+        s->spare_gt = (uint64_t*)pg;
+        s->spare_row = (uint64_t*)pr;
+        s->spare_cap = cap;
+    }
+    HIP_TRY(launch_ingest_merge(s->d_live_gt, s->d_live_row, s->n_live, (const IngestRow*)up_rows, a,
+                                (uint64_t*)(up_rows + b_rows), s->spare_gt, s->spare_row,
+                                check_present ? d_present : nullptr, c->max_grid, c->stream));
+    unsigned int present = 0;
+    if (check_present) HIP_TRY(hipMemcpyAsync(&present, d_present, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (present) return fail(DSY_EINVAL, "a row to insert is in the live index already");
+    uint64_t* prev_gt = const_cast<uint64_t*>(s->d_live_gt);
+    uint64_t* prev_row = const_cast<uint64_t*>(s->d_live_row);
+    const uint64_t prev_cap = s->live_cap;
+    s->d_live_gt = s->spare_gt;
+    s->d_live_row = s->spare_row;
+    s->live_cap = s->spare_cap;
+    if (prev_cap) {  // the index an earlier merge built: the next target
+        s->spare_gt = prev_gt;
+        s->spare_row = prev_row;
+        s->spare_cap = prev_cap;
+    } else {         // the index of the upload/attach (possibly the caller's global_time column)
+        store_release(s, prev_gt);
+        store_release(s, prev_row);
+        s->spare_gt = s->spare_row = nullptr;
+        s->spare_cap = 0;
+    }
+    // segments: a meta's segment moves by the new entries of smaller metas and grows by its own
+    std::map<uint32_t, uint64_t> cnt;
+    for (uint64_t j = 0; j < a; ++j) ++cnt[meta[j]];
+    for (auto& e : s->segs) {
+        uint64_t before = 0;
+        for (auto& m : cnt)
+            if (m.first < e.first) before += m.second;
+        auto own = cnt.find(e.first);
+        e.second.first += before;
+        e.second.second += before + (own == cnt.end() ? 0 : own->second);
+    }
+    for (auto& m : cnt) {
+        if (s->segs.count(m.first)) continue;
+        uint64_t start = 0;
+        for (auto& e : old)
+            if (e.first < m.first) start = std::max(start, e.second.second);
+        for (auto& m2 : cnt)
+            if (m2.first < m.first) start += m2.second;
+        s->segs[m.first] = {start, start + m.second};
+    }
+    s->n_live = live;
+    return DSY_OK;
+}
+
+int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blob_len, const uint64_t* offsets,
+                     uint64_t a, const uint64_t* gt, const uint32_t* meta, const uint64_t* member) {
+    if (!c || !s || !offsets || (a && (!gt || !meta || (blob_len && !blob)))) return fail(DSY_EINVAL, "NULL argument");
+    if (s->ctx != c) return fail(DSY_EINVAL, "store belongs to another context");
+    if (s->dup && a && !member) return fail(DSY_EINVAL, "the store has a (member, global_time) table: members required");
+    int rc = check_offsets(offsets, a, blob_len);
+    if (rc) return rc;
+    if (a == 0) return DSY_OK;
+    Guard g(c);
+    if (c->inflight()) return fail(DSY_EINVAL, "the store cannot change while submitted responder batches are in flight");
+    const uint64_t n0 = s->n, base0 = offsets[0], add = offsets[a] - base0;
+    uint64_t minlen = ~0ull;
+    for (uint64_t j = 0; j < a; ++j) minlen = std::min(minlen, offsets[j + 1] - offsets[j]);
 
     HIP_TRY(hipStreamSynchronize(c->stream));  // nothing in flight reads a buffer that is about to be replaced
     // the line copy the responder hashes from, and its row records
@@ -1025,93 +1104,34 @@ int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blo
         s->rec_cap = cap;
     }
 
-    // staged uploads (one workspace): the packets, their offsets, records and index rows; the packets then move to
-    // their line-aligned places
+    // staged uploads (one workspace): the packets, their offsets and records; the packets then move to their
+    // line-aligned places
     std::vector<uint64_t> noff(a + 1);
     for (uint64_t j = 0; j <= a; ++j) noff[j] = offsets[j] - base0;
-    const size_t b_blob = (add + 15) / 16 * 16, b_off = (a + 1) * 8, b_rec = a * sizeof(RowRec),
-                 b_rows = a * sizeof(IngestRow);
+    const size_t b_blob = (add + 15) / 16 * 16, b_off = (a + 1) * 8, b_rec = a * sizeof(RowRec);
     void* d_up;
-    if ((rc = ws_get(c, "ingest", b_blob + b_off + b_rec + b_rows + a * 8, &d_up))) return rc;
+    if ((rc = ws_get(c, "ingest", b_blob + b_off + b_rec, &d_up))) return rc;
     uint8_t* up = (uint8_t*)d_up;
     uint8_t* up_off = up + b_blob;
     uint8_t* up_rec = up_off + b_off;
-    uint8_t* up_rows = up_rec + b_rec;
     if (add) HIP_TRY(hipMemcpyAsync(up, blob + base0, add, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(up_off, noff.data(), b_off, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(up_rec, nrec.data(), b_rec, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(up_rows, rows.data(), b_rows, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(const_cast<RowRec*>(s->d_rec) + n0, up_rec, b_rec, hipMemcpyDeviceToDevice, c->stream));
     HIP_TRY(launch_store_lines(up, (const uint64_t*)up_off, s->d_rec + n0, a, const_cast<uint8_t*>(s->d_lines),
                                c->stream));
-
-    // the live index, merged into fresh buffers (the old ones are read by the merge)
-    // (double-buffered: the previous append's index becomes the next one's target, so a steady stream of appends
-    // allocates nothing)
-    const uint64_t live = s->n_live + a;
-    if (s->spare_cap < live) {
-        store_release(s, s->spare_gt);
-        store_release(s, s->spare_row);
-        s->spare_gt = s->spare_row = nullptr;
-        s->spare_cap = 0;
-        const uint64_t cap = grown(live, s->n_live);
-        void *pg, *pr;
-        if (hipMalloc(&pg, cap * 8) != hipSuccess) return fail(DSY_ENOMEM, "store live index growth");
-        s->owned.push_back(pg);
-        if (hipMalloc(&pr, cap * 8) != hipSuccess) { store_release(s, pg); return fail(DSY_ENOMEM, "store live index growth"); }
-        s->owned.push_back(pr);
-        s->spare_gt = (uint64_t*)pg;
-        s->spare_row = (uint64_t*)pr;
-        s->spare_cap = cap;
-    }
-    HIP_TRY(launch_ingest_merge(s->d_live_gt, s->d_live_row, s->n_live, (const IngestRow*)up_rows, a,
-                                (uint64_t*)(up_rows + b_rows), s->spare_gt, s->spare_row, c->max_grid, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    uint64_t* prev_gt = const_cast<uint64_t*>(s->d_live_gt);
-    uint64_t* prev_row = const_cast<uint64_t*>(s->d_live_row);
-    const uint64_t prev_cap = s->live_cap;
-    s->d_live_gt = s->spare_gt;
-    s->d_live_row = s->spare_row;
-    s->live_cap = s->spare_cap;
-    if (prev_cap) {  // the index an earlier append built: the next target
-        s->spare_gt = prev_gt;
-        s->spare_row = prev_row;
-        s->spare_cap = prev_cap;
-    } else {         // the index of the upload/attach (possibly the caller's global_time column)
-        store_release(s, prev_gt);
-        store_release(s, prev_row);
-        s->spare_gt = s->spare_row = nullptr;
-        s->spare_cap = 0;
-    }
-
-    // segments: a meta's segment moves by the new rows of smaller metas and grows by its own
-    std::map<uint32_t, uint64_t> cnt;
-    for (uint64_t j = 0; j < a; ++j) ++cnt[meta[j]];
-    for (auto& e : s->segs) {
-        uint64_t before = 0;
-        for (auto& m : cnt)
-            if (m.first < e.first) before += m.second;
-        auto own = cnt.find(e.first);
-        e.second.first += before;
-        e.second.second += before + (own == cnt.end() ? 0 : own->second);
-    }
-    for (auto& m : cnt) {
-        if (s->segs.count(m.first)) continue;
-        uint64_t start = 0;
-        for (auto& e : old)
-            if (e.first < m.first) start = std::max(start, e.second.second);
-        for (auto& m2 : cnt)
-            if (m2.first < m.first) start += m2.second;
-        s->segs[m.first] = {start, start + m.second};
-    }
+    // the new rows join the live index (positions n0 .. n0+a-1: after every stored row of equal global time)
+    std::vector<uint64_t> pos(a);
+    for (uint64_t j = 0; j < a; ++j) pos[j] = n0 + j;
+    if ((rc = live_insert(c, s, meta, gt, pos.data(), a, false))) return rc;
     if (s->dup && (rc = dup_insert(c, s, member, gt, n0, a))) return rc;
     s->min_len = n0 ? std::min(s->min_len, minlen) : minlen;
     s->n += a;
-    s->n_live = live;
     s->blob_len += add;
     s->lines_used = at;
     return DSY_OK;
 }
+
 
 int dsy_store_prune(dsy_ctx* c, dsy_store* s, uint32_t meta, uint64_t max_gt, uint64_t* out_deleted) {
     if (!c || !s || !out_deleted) return fail(DSY_EINVAL, "NULL argument");
@@ -1175,15 +1195,12 @@ int dsy_store_prune(dsy_ctx* c, dsy_store* s, uint32_t meta, uint64_t max_gt, ui
     return DSY_OK;
 }
 
-int dsy_store_delete(dsy_ctx* c, dsy_store* s, const uint64_t* rows, uint64_t k, uint64_t* out_deleted) {
-    if (!c || !s || !out_deleted || (k && !rows)) return fail(DSY_EINVAL, "NULL argument");
-    if (s->ctx != c) return fail(DSY_EINVAL, "store belongs to another context");
-    for (uint64_t i = 0; i < k; ++i)
-        if (rows[i] >= s->n) return fail(DSY_EINVAL, "row %llu out of range (%llu rows)", (unsigned long long)rows[i], (unsigned long long)s->n);
-    *out_deleted = 0;
-    if (!k) return DSY_OK;
-    Guard g(c);
-    if (c->inflight()) return fail(DSY_EINVAL, "the store cannot change while submitted responder batches are in flight");
+// The given rows leave the live index (a stable compaction on the device; rows not in it are ignored); erase_dup: their
+// (member, global_time) slots become tombstones too (a DELETE; an undo keeps them).  *out_removed = index entries
+// removed.  The caller holds the ctx lock and has validated the rows.
+static int live_remove(dsy_ctx* c, dsy_store* s, const uint64_t* rows, uint64_t k, bool erase_dup,
+                       uint64_t* out_removed) {
+    uint64_t* out_deleted = out_removed;
     // segment bounds (old positions) to remap: every meta's [a, b)
     std::vector<uint32_t> seg_ids;
     std::vector<uint64_t> bounds;
@@ -1208,7 +1225,7 @@ int dsy_store_delete(dsy_ctx* c, dsy_store* s, const uint64_t* rows, uint64_t k,
     HIP_TRY(hipMemcpyAsync(d_bounds, bounds.data(), b_bounds, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(launch_mark_rows(d_rows, k, s->n, d_bits, c->stream));
     // the deleted rows' (member, global_time) slots become tombstones (also rows outside the live index: undone ones)
-    if (s->dup) HIP_TRY(launch_dup_erase(d_rows, nullptr, 0, k, s->dup_keys, s->dup, s->dup_cap - 1, c->stream));
+    if (erase_dup && s->dup) HIP_TRY(launch_dup_erase(d_rows, nullptr, 0, k, s->dup_keys, s->dup, s->dup_cap - 1, c->stream));
     const uint64_t cap_need = std::max<uint64_t>(s->n_live, 1);
     if (s->spare_cap < cap_need) {  // the ingest's second buffer pair is the target, as for a merge
         store_release(s, s->spare_gt);
@@ -1250,6 +1267,39 @@ int dsy_store_delete(dsy_ctx* c, dsy_store* s, const uint64_t* rows, uint64_t k,
     }
     for (size_t j = 0; j < seg_ids.size(); ++j) s->segs[seg_ids[j]] = {bounds[2 * j], bounds[2 * j + 1]};
     s->n_live = live;
+    return DSY_OK;
+}
+
+int dsy_store_delete(dsy_ctx* c, dsy_store* s, const uint64_t* rows, uint64_t k, uint64_t* out_deleted) {
+    if (!c || !s || !out_deleted || (k && !rows)) return fail(DSY_EINVAL, "NULL argument");
+    if (s->ctx != c) return fail(DSY_EINVAL, "store belongs to another context");
+    for (uint64_t i = 0; i < k; ++i)
+        if (rows[i] >= s->n) return fail(DSY_EINVAL, "row %llu out of range (%llu rows)", (unsigned long long)rows[i], (unsigned long long)s->n);
+    *out_deleted = 0;
+    if (!k) return DSY_OK;
+    Guard g(c);
+    if (c->inflight()) return fail(DSY_EINVAL, "the store cannot change while submitted responder batches are in flight");
+    return live_remove(c, s, rows, k, true, out_deleted);
+}
+
+int dsy_store_set_undone(dsy_ctx* c, dsy_store* s, const uint64_t* rows, uint64_t k, const uint32_t* meta,
+                         const uint64_t* gt, int undone, uint64_t* out_changed) {
+    if (!c || !s || !out_changed || (k && (!rows || (!undone && (!meta || !gt))))) return fail(DSY_EINVAL, "NULL argument");
+    if (s->ctx != c) return fail(DSY_EINVAL, "store belongs to another context");
+    for (uint64_t i = 0; i < k; ++i)
+        if (rows[i] >= s->n) return fail(DSY_EINVAL, "row %llu out of range (%llu rows)", (unsigned long long)rows[i], (unsigned long long)s->n);
+    *out_changed = 0;
+    if (!k) return DSY_OK;
+    Guard g(c);
+    if (c->inflight()) return fail(DSY_EINVAL, "the store cannot change while submitted responder batches are in flight");
+    if (undone) return live_remove(c, s, rows, k, false, out_changed);
+    std::vector<uint64_t> r(rows, rows + k);
+    std::vector<uint64_t> sorted_r(r);
+    std::sort(sorted_r.begin(), sorted_r.end());
+    if (std::adjacent_find(sorted_r.begin(), sorted_r.end()) != sorted_r.end()) return fail(DSY_EINVAL, "a row is given twice");
+    int rc = live_insert(c, s, meta, gt, r.data(), k, true);
+    if (rc) return rc;
+    *out_changed = k;
     return DSY_OK;
 }
 

@@ -236,8 +236,9 @@ hipError_t launch_rec_scatter(RowRec* rec, const uint64_t* rows, const RowRec* s
 struct IngestRow {
     uint64_t gt, seg_a, seg_b, row;
 };
-// merge the appended rows into the live index: (live_gt, live_row | identity)[n_live] + rows[a] ->
-// (out_gt, out_row)[n_live + a]; rank[a] is scratch
+// merge new index entries (appended or redone rows, in (meta, global_time, row) order) into the live index:
+// (live_gt, live_row | identity)[n_live] + rows[a] -> (out_gt, out_row)[n_live + a]; rank[a] is scratch; present
+// (optional): set to 1 when a row is in the index already
 // GlobalTimePruning DELETE: k = rows of live_gt[a, b) with global_time <= max_gt (device u64), then the index
 // without live rows [a, a + k) -> (out_gt, out_row)[n_out]
 hipError_t launch_prune_count(const uint64_t* live_gt, uint64_t a, uint64_t b, uint64_t max_gt, uint64_t* out_k,
@@ -279,7 +280,7 @@ hipError_t launch_live_delete(const uint64_t* live_gt, const uint64_t* live_row,
                               uint64_t* bounds, uint32_t nb, hipStream_t stream);
 hipError_t launch_ingest_merge(const uint64_t* live_gt, const uint64_t* live_row, uint64_t n_live,
                                const IngestRow* rows, uint64_t a, uint64_t* rank, uint64_t* out_gt, uint64_t* out_row,
-                               uint32_t max_grid, hipStream_t stream);
+                               unsigned int* present, uint32_t max_grid, hipStream_t stream);
 
 // ---------------------------------------------------------------------------------------- simulator
 static constexpr uint32_t kSimFilterWordsMax = 2048;  // m <= 65536 bits

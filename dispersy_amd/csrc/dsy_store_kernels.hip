@@ -19,17 +19,24 @@ static constexpr uint32_t kIngestPerThread = 4;
 static constexpr uint64_t kIngestTile = (uint64_t)kIngestThreads * kIngestPerThread;
 
 __global__ void __launch_bounds__(kIngestThreads) k_ingest_rank(const uint64_t* __restrict__ live_gt,
+                                                                 const uint64_t* __restrict__ live_row,
                                                                  const IngestRow* __restrict__ rows, uint64_t a,
-                                                                 uint64_t* __restrict__ rank) {
+                                                                 uint64_t* __restrict__ rank,
+                                                                 unsigned int* __restrict__ present) {
     const uint64_t j = (uint64_t)blockIdx.x * kIngestThreads + threadIdx.x;
     if (j >= a) return;
     const IngestRow r = rows[j];
+    // the first index entry of the segment at or after (gt, row) in (global_time, row) order: for an appended row
+    // (a row position past every stored one) the upper bound of its global time, for a redone row its place among
+    // the rows of equal global time
     uint64_t lo = r.seg_a, hi = r.seg_b;
     while (lo < hi) {
         const uint64_t mid = lo + ((hi - lo) >> 1);
-        if (live_gt[mid] <= r.gt) lo = mid + 1; else hi = mid;
+        const uint64_t g = live_gt[mid], w = live_row ? live_row[mid] : mid;
+        if (g < r.gt || (g == r.gt && w < r.row)) lo = mid + 1; else hi = mid;
     }
     rank[j] = lo;
+    if (present && lo < r.seg_b && live_gt[lo] == r.gt && (live_row ? live_row[lo] : lo) == r.row) atomicOr(present, 1u);
 }
 
 // number of j in [lo, hi) with rank[j] <= i (rank is non-decreasing)
@@ -121,10 +128,11 @@ hipError_t launch_live_cut(const uint64_t* live_gt, const uint64_t* live_row, ui
 
 hipError_t launch_ingest_merge(const uint64_t* live_gt, const uint64_t* live_row, uint64_t n_live,
                                const IngestRow* rows, uint64_t a, uint64_t* rank, uint64_t* out_gt, uint64_t* out_row,
-                               uint32_t max_grid, hipStream_t stream) {
+                               unsigned int* present, uint32_t max_grid, hipStream_t stream) {
     if (!a) return hipSuccess;
     const uint32_t gnew = (uint32_t)((a + kIngestThreads - 1) / kIngestThreads);
-    hipLaunchKernelGGL(k_ingest_rank, dim3(gnew), dim3(kIngestThreads), 0, stream, live_gt, rows, a, rank);
+    hipLaunchKernelGGL(k_ingest_rank, dim3(gnew), dim3(kIngestThreads), 0, stream, live_gt, live_row, rows, a, rank,
+                       present);
     if (n_live) {
         uint64_t g = (n_live + kIngestTile - 1) / kIngestTile;
         if (g > (uint64_t)max_grid * 4) g = (uint64_t)max_grid * 4;

@@ -86,6 +86,7 @@ class SyncStore(object):
                 self._nlive[int(self.meta[seg[0]])] = len(seg)
         self._empty = np.zeros(0, dtype=np.int64)
         self._groups = None  # (meta, member) -> rows, built on first use (member_rows)
+        self._keys = None    # (member, global_time) -> row, built on first use (rows_of_keys)
         self._gpending = {}
         self._blob_base = 0  # offsets[] of the host blob's first byte (attach: earlier packets are device-only)
         self._owns_handle = True
@@ -133,14 +134,15 @@ class SyncStore(object):
                              communities={r[6] for r in rows} if rows else ({community} if community is not None else None))
 
     @classmethod
-    def attach(cls, ctx, handle, global_time, meta, lengths, member=None):
+    def attach(cls, ctx, handle, global_time, meta, lengths, member=None, undone=None):
         """A store exported straight into HBM (dsy_store_attach / dsy_store_upload made by the caller): the host keeps
-        the small columns only (rows in index order, all live), the packets of these rows stay on the device --
-        packet() serves only rows appended later.  `handle` is the dsy_store* (the caller keeps ownership)."""
+        the small columns only (rows in index order), the packets of these rows stay on the device -- packet() serves
+        only rows appended later.  `handle` is the dsy_store* (the caller keeps ownership); `undone` must be the
+        column the device index was built from (None: every row live), so host and device agree on the live rows."""
         lengths = np.ascontiguousarray(lengths, dtype=np.uint64)
         offsets = np.zeros(len(lengths) + 1, dtype=np.uint64)
         np.cumsum(lengths, out=offsets[1:])
-        st = cls(bytearray(), offsets, global_time, meta, ctx=ctx, member=member)
+        st = cls(bytearray(), offsets, global_time, meta, ctx=ctx, member=member, undone=undone)
         st._blob_base = int(offsets[-1])
         st._handle = handle if isinstance(handle, ctypes.c_void_p) else ctypes.c_void_p(handle)
         st._owns_handle = False
@@ -173,6 +175,17 @@ class SyncStore(object):
             keep = np.flatnonzero(~self.deleted)
             self._row_of_id = dict(zip(self.rowid[keep].tolist(), keep.tolist()))
         return self._row_of_id[int(rowid)]
+
+    def rows_of_keys(self, members, global_times):
+        """The row of each (member, global_time) -- the sync table's UNIQUE(community, member, global_time) key
+        within one community -- or -1 when no (undeleted) row has it: the WHERE of `UPDATE sync SET undone = ? WHERE
+        community = ? AND member = ? AND global_time = ?` (community.py:3479-3480)."""
+        if self.member is None:
+            raise ValueError("rows_of_keys needs the store's member column")
+        if self._keys is None:
+            keep = np.flatnonzero(~self.deleted)
+            self._keys = dict(zip(zip(self.member[keep].tolist(), self.global_time[keep].tolist()), keep.tolist()))
+        return np.asarray([self._keys.get((int(m), int(g)), -1) for m, g in zip(members, global_times)], dtype=np.int64)
 
     def live_rows(self, meta_id):
         """Store rows of one meta with undone == 0 (not deleted), in (global_time, rowid) order."""
@@ -277,6 +290,8 @@ class SyncStore(object):
         self._top = int(ids[-1])
         if self._row_of_id is not None:
             self._row_of_id.update(zip(ids.tolist(), rows.tolist()))
+        if self._keys is not None and mem is not None:
+            self._keys.update(zip(zip(mem.tolist(), gts.tolist()), rows.tolist()))
         if self._groups is not None and mem is not None:
             for r, m, b_ in zip(rows.tolist(), metas.tolist(), mem.tolist()):
                 self._gpending.setdefault((m, b_), []).append(np.asarray([r], dtype=np.int64))
@@ -298,23 +313,36 @@ class SyncStore(object):
     # ------------------------------------------------------------------------------------------ DELETEs
     def prune(self, meta_id, max_global_time):
         """DELETE FROM sync WHERE meta_message = ? AND global_time <= ? (community.py:1092-1096, GlobalTimePruning):
-        the rows leave the live index (host and device) and the duplicate table.  Returns the number of rows deleted."""
-        seg = self.live_rows(meta_id)
-        if not len(seg) or max_global_time < 0:
+        the rows -- live and undone alike, as the SQL DELETE does -- leave the store: the live ones the index (host and
+        device), all of them the duplicate table and row_of_id.  Returns the number of rows deleted."""
+        m = int(meta_id)
+        seg = self.live_rows(m)
+        if max_global_time < 0:
             return 0
-        k = int(np.searchsorted(self.global_time[seg], np.uint64(max_global_time), side="right"))
-        if not k:
-            return 0
-        self._mark_deleted(seg[:k])
-        self._live[int(meta_id)] = seg[k:]
-        self._nlive[int(meta_id)] -= k
-        self._ops.append(("prune", int(meta_id), int(max_global_time), self.n))
-        if self._handle is not None:
-            out = ctypes.c_uint64()
-            _native.check(self.ctx.lib.dsy_store_prune(self.ctx.handle, self._handle, int(meta_id),
-                                                       int(max_global_time), ctypes.byref(out)))
-            assert out.value == k, (out.value, k)
-        return k
+        k = int(np.searchsorted(self.global_time[seg], np.uint64(max_global_time), side="right")) if len(seg) else 0
+        gone = np.flatnonzero((self.meta == m) & (self.undone != 0) & ~self.deleted &
+                              (self.global_time <= np.uint64(max_global_time)))
+        if k:
+            self._mark_deleted(seg[:k])
+            self._live[m] = seg[k:]
+            self._nlive[m] -= k
+            self._ops.append(("prune", m, int(max_global_time), self.n))
+            if self._handle is not None:
+                out = ctypes.c_uint64()
+                _native.check(self.ctx.lib.dsy_store_prune(self.ctx.handle, self._handle, m, int(max_global_time),
+                                                           ctypes.byref(out)))
+                if out.value != k:
+                    raise RuntimeError("device and host stores disagree: the device pruned %d rows, the host %d"
+                                       % (out.value, k))
+        if len(gone):  # undone rows are outside the index: only their duplicate-table slots go
+            self._mark_deleted(gone)
+            self._ops.append(("delete", gone, self.n))
+            if self._handle is not None:
+                out = ctypes.c_uint64()
+                rws = gone.astype(np.uint64)
+                _native.check(self.ctx.lib.dsy_store_delete(self.ctx.handle, self._handle, rws.ctypes.data, len(rws),
+                                                            ctypes.byref(out)))
+        return k + len(gone)
 
     def delete_rows(self, rows):
         """DELETE FROM sync WHERE id = ? for the given store rows (the sequence-number conflict DELETE,
@@ -341,11 +369,68 @@ class SyncStore(object):
             rws = rows.astype(np.uint64)  # keep the array alive across the call
             _native.check(self.ctx.lib.dsy_store_delete(self.ctx.handle, self._handle, rws.ctypes.data, len(rws),
                                                         ctypes.byref(out)))
-            assert out.value == len(live), (out.value, len(live))
+            if out.value != len(live):
+                raise RuntimeError("device and host stores disagree: the device removed %d index entries, the host "
+                                   "counts %d live rows" % (out.value, len(live)))
         return len(rows)
+
+    # ------------------------------------------------------------------------------------------ undo / redo
+    def set_undone(self, rows, values):
+        """UPDATE sync SET undone = ? WHERE id = ? for the given store rows: Community.on_undo (community.py:3457-3481,
+        the undo message's packet id) and _update_timerange (:3633-3642, 1 to undo, 0 to redo).  A row given several
+        times keeps its last value (executemany order); deleted rows are left alone (the UPDATE finds no row).  Rows
+        that become undone leave the responder's index (host and device) but keep their duplicate-table slots (the
+        duplicate check still finds them and sends the undo proof, dispersy.py:886-892); rows that become live again
+        re-enter it at their (global_time, rowid) place.  Returns the number of rows whose undone-ness changed."""
+        rows = np.atleast_1d(np.asarray(rows, dtype=np.int64))
+        values = np.broadcast_to(np.asarray(values, dtype=np.int64), rows.shape)
+        if not len(rows):
+            return 0
+        if rows.min() < 0 or rows.max() >= self.n:
+            raise IndexError("set_undone: row out of range")
+        last = dict(zip(rows.tolist(), values.tolist()))
+        rows = np.fromiter(last.keys(), dtype=np.int64, count=len(last))
+        vals = np.fromiter(last.values(), dtype=np.int64, count=len(last))
+        alive = ~self.deleted[rows]
+        rows, vals = rows[alive], vals[alive]
+        cur = self.undone[rows]
+        undo = np.sort(rows[(cur == 0) & (vals != 0)])
+        redo = np.sort(rows[(cur != 0) & (vals == 0)])
+        self._buf["undone"][rows] = vals
+        for m in np.unique(self.meta[undo]).tolist():
+            seg = self.live_rows(m)
+            drop = undo[self.meta[undo] == m]
+            self._live[m] = seg[~np.isin(seg, drop, assume_unique=True)]
+            self._nlive[m] -= len(drop)
+        for m in np.unique(self.meta[redo]).tolist():
+            seg = np.concatenate([self.live_rows(m), redo[self.meta[redo] == m]])
+            self._live[m] = seg[np.lexsort((seg, self.global_time[seg]))]
+            self._nlive[m] = self._nlive.get(m, 0) + int((self.meta[redo] == m).sum())
+        if self._handle is not None:
+            self._set_undone_device(undo, redo)
+        return len(undo) + len(redo)
+
+    def _set_undone_device(self, undo, redo):
+        lib, out = self.ctx.lib, ctypes.c_uint64()
+        if len(undo):
+            u = undo.astype(np.uint64)
+            _native.check(lib.dsy_store_set_undone(self.ctx.handle, self._handle, u.ctypes.data, len(u), None, None, 1,
+                                                   ctypes.byref(out)))
+            if out.value != len(u):
+                raise RuntimeError("device and host stores disagree: %d of %d rows to undo were in the device index"
+                                   % (out.value, len(u)))
+        if len(redo):
+            r = redo.astype(np.uint64)
+            mt = np.ascontiguousarray(self.meta[redo])
+            gt = np.ascontiguousarray(self.global_time[redo])
+            _native.check(lib.dsy_store_set_undone(self.ctx.handle, self._handle, r.ctypes.data, len(r), mt.ctypes.data,
+                                                   gt.ctypes.data, 0, ctypes.byref(out)))
 
     def _mark_deleted(self, rows):
         self._buf["deleted"][rows] = True
+        if self._keys is not None:
+            for k in zip(self.member[rows].tolist(), self.global_time[rows].tolist()):
+                self._keys.pop(k, None)
         if self._row_of_id is not None:
             for rid in self.rowid[rows].tolist():
                 self._row_of_id.pop(rid, None)
@@ -445,6 +530,12 @@ class SyncStore(object):
             if self._replaced:  # UPDATEs made before the first upload
                 rows = sorted(self._replaced)
                 self._replace_device(rows, [self._replaced[r] for r in rows])
+            # rows appended before the upload went in live; the ones undone since leave the index (the upload's own
+            # rows took their current undone column)
+            late = np.arange(n0, self.n, dtype=np.int64)
+            late = late[(self.undone[late] != 0) & ~self.deleted[late]]
+            if len(late):
+                self._set_undone_device(late, np.zeros(0, dtype=np.int64))
         return self._handle
 
     def close(self):

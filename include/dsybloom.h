@@ -194,6 +194,18 @@ int dsy_store_prune(dsy_ctx* ctx, dsy_store* store, uint32_t meta, uint64_t max_
  * deleted already.  *out_deleted = live index entries removed. */
 int dsy_store_delete(dsy_ctx* ctx, dsy_store* store, const uint64_t* rows, uint64_t k, uint64_t* out_deleted);
 
+/* UPDATE sync SET undone = ? for k store rows (0-based positions): Community.on_undo's UPDATE ... WHERE community = ?
+ * AND member = ? AND global_time = ? (community.py:3479-3480) and _update_timerange's UPDATE ... WHERE id = ?
+ * (:3635, :3642), as the device index sees them.  undone != 0: the rows leave the responder's live index (it serves
+ * undone = 0 only, community.py:2764-2787; rows out of the index already are ignored) but keep their
+ * (member, global_time) slots, so the duplicate check still finds them and the caller sends the undo proof
+ * (dispersy.py:886-892); *out_changed = index entries removed.  undone == 0 (redo): the rows -- undone, not deleted,
+ * each once, meta[k] / global_time[k] their columns -- re-enter the index at their (meta_message, global_time, row)
+ * place; a row in the index already gives DSY_EINVAL (nothing changes); *out_changed = k.  Which undo packet undid a
+ * row (the value of the column) is the caller's: only "undone or not" reaches the device. */
+int dsy_store_set_undone(dsy_ctx* ctx, dsy_store* store, const uint64_t* rows, uint64_t k, const uint32_t* meta,
+                         const uint64_t* global_time, int undone, uint64_t* out_changed);
+
 /* ------------------------------------------------------------------------------------ duplicate check */
 /* Received sync packets are checked against the store by (member, global_time) before they are stored
  * (_is_duplicate_sync_message, dispersy.py:831-918; the sync table is UNIQUE(community, member, global_time)).

@@ -241,14 +241,18 @@ def test_global_time_pruning_deletes_from_the_responder(lazy):
 
 
 def test_prune_host_index():
-    """SyncStore.prune on the host columns: the meta's live rows up to the threshold leave, others stay (CPU)."""
+    """SyncStore.prune on the host columns: the meta's rows up to the threshold -- live and undone, as the SQL DELETE
+    (community.py:1094-1096) -- leave, others stay (CPU)."""
     rows = make_rows(5, 2000, 2000)
     store = SyncStore.from_rows(rows, ctx=object())
     before = {m: store.rowid[store.live_rows(m)].tolist() for m in (1, 2, 3, 7)}
+    undone_cut = [r[0] for r in rows if r[2] == 3 and r[3] != 0 and r[1] <= 1500]
+    assert undone_cut
     k = store.prune(3, 1500)
     after = store.rowid[store.live_rows(3)].tolist()
     gt_of = {r[0]: r[1] for r in rows}
-    assert k == len(before[3]) - len(after) > 0
+    assert k == len(before[3]) - len(after) + len(undone_cut) > len(undone_cut)
+    assert all(bool(store.deleted[int(np.flatnonzero(store.rowid == i)[0])]) for i in undone_cut)
     assert after == [r for r in before[3] if gt_of[r] > 1500]
     assert all(store.rowid[store.live_rows(m)].tolist() == before[m] for m in (1, 2, 7))
     assert store.prune(3, 1500) == 0 and store.prune(99, 10 ** 6) == 0
