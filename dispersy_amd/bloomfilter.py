@@ -103,6 +103,7 @@ class BloomFilter(object):
         self._hash_name, self._chunk = hash_family(m_size, k_functions)
         self._raw = bytearray(raw) if raw is not None else bytearray(m_size // 8)
         self._params = None
+        self._record = None
 
     # ------------------------------------------------------------------------------------------ device
     @property
@@ -112,6 +113,20 @@ class BloomFilter(object):
             self._params = _native.bloom_params(self._m_size, self._k_functions, _native.HASH_KINDS[self._hash_name],
                                                 self._chunk, self._prefix)
         return self._params
+
+    @property
+    def request_record(self):
+        """This filter's part of a dsy_request record (m, k, hash family, prefix; the claim's range and the filter
+        offset left zero), as bytes: built once -- the shape and prefix never change -- so a batch of claims is one
+        join of records (SyncCommunity.request_records), not a field-by-field fill per claim."""
+        if self._record is None:
+            q = _native.Request()
+            q.m_bits, q.k, q.hash_kind, q.chunk_bytes = (self._m_size, self._k_functions,
+                                                         _native.HASH_KINDS[self._hash_name], self._chunk)
+            q.prefix_len = len(self._prefix)
+            ctypes.memmove(q.prefix, self._prefix, len(self._prefix))
+            self._record = bytes(q)
+        return self._record
 
     @staticmethod
     def _ctx():

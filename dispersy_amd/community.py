@@ -17,6 +17,7 @@ _select_and_fix) and dsy_claim_modulo (the residue class).
 """
 import ctypes
 import itertools
+import operator
 import random as _random_module
 import time as _time
 from collections import OrderedDict, namedtuple
@@ -30,10 +31,44 @@ from .distribution import FullSyncDistribution, GlobalTimePruning, LastSyncDistr
 
 MAX_GT = 2 ** 63 - 1  # sqlite's signed 64-bit ceiling (community.py:2545-2548)
 _REQUEST_DTYPE = np.dtype(_native.Request)  # the dsy_request layout, as a numpy record
+_RANGE_DTYPE = np.dtype([("time_low", np.uint64), ("time_high", np.uint64), ("modulo", np.uint64),
+                         ("offset", np.uint64)])
+_RANGE_OF = operator.itemgetter(0, 1, 2, 3)  # a ClaimRequest's (time_low, time_high, modulo, offset)
+_BLOOM_OF = operator.itemgetter(4)
+_RECORD_OF = operator.attrgetter("request_record")
+_RAW_OF = operator.attrgetter("_raw")
 
 # the sync part of an introduction-request payload (payload.py:31-153): time_high == 0 means "up to the
 # responder's global time"
 ClaimRequest = namedtuple("ClaimRequest", "time_low time_high modulo offset bloom_filter")
+
+
+class RowLists(object):
+    """The responder's answer for a batch of claims: claim i's store rows, in send order, are rows[offsets[i]:
+    offsets[i + 1]].  A sequence of per-claim int64 arrays (len, indexing, iteration) built on access, so a caller
+    that reads the packed form (rows, offsets) pays for no per-claim objects."""
+
+    __slots__ = ("rows", "offsets")
+
+    def __init__(self, rows, offsets):
+        self.rows, self.offsets = rows, offsets
+
+    def __len__(self):
+        return len(self.offsets) - 1
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self)))]
+        n = len(self)
+        if i < 0:
+            i += n
+        if not 0 <= i < n:
+            raise IndexError(i)
+        return self.rows[self.offsets[i]:self.offsets[i + 1]]
+
+    def __iter__(self):
+        rows, off = self.rows, self.offsets.tolist()
+        return (rows[off[i]:off[i + 1]] for i in range(len(off) - 1))
 
 
 class DropMessage(object):
@@ -652,38 +687,36 @@ class SyncCommunity(object):
 
     @staticmethod
     def request_records(requests):
-        """(dsy_request records, R, packed filters) of a list of ClaimRequests, as the C-ABI takes them: the records
-        are filled column by column (numpy view of the ctypes layout), not one ctypes field at a time; each filter
-        sits 4-byte aligned in the blob at its record's filter_offset."""
+        """(dsy_request records, R, packed filters) of a list of ClaimRequests, as the C-ABI takes them: the filters'
+        static record parts (BloomFilter.request_record) joined into the record array in one pass, the claims'
+        (time_low, time_high, modulo, offset) filled as columns, time bounds clamped to 2^63-1 (community.py:2545-2548);
+        each filter sits 4-byte aligned in the blob at its record's filter_offset."""
         R = len(requests)
-        reqs = np.zeros(max(R, 1), dtype=_REQUEST_DTYPE)
         if not R:
-            return reqs, 0, b""
-        # one pass over the Python objects, then whole columns
-        kinds = _native.HASH_KINDS
-        c = np.fromiter(itertools.chain.from_iterable(
-            (min(q.time_low, MAX_GT), min(q.time_high, MAX_GT), q.modulo, q.offset, bf._m_size, bf._k_functions,
-             kinds[bf._hash_name], bf._chunk, len(bf._prefix)) for q in requests for bf in (q.bloom_filter,)),
-            dtype=np.uint64, count=9 * R).reshape(R, 9)
-        raws = [q.bloom_filter._raw for q in requests]
-        prefixes = [q.bloom_filter._prefix for q in requests]
-        for j, name in enumerate(("time_low", "time_high", "modulo", "offset", "m_bits", "k", "hash_kind",
-                                  "chunk_bytes", "prefix_len")):
-            reqs[name][:R] = c[:, j]
-        plen = c[:, 8]
-        sizes = np.fromiter(((len(r) + 3) & ~3 for r in raws), dtype=np.uint64, count=R)
-        reqs["filter_offset"][:R] = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
-        if (plen == 1).all():
-            reqs["prefix"][:R, 0] = np.frombuffer(b"".join(prefixes), dtype=np.uint8)
+            return np.zeros(1, dtype=_REQUEST_DTYPE), 0, b""
+        bfs = list(map(_BLOOM_OF, requests))
+        reqs = np.frombuffer(bytearray(b"".join(map(_RECORD_OF, bfs))), dtype=_REQUEST_DTYPE)
+        try:
+            t = np.fromiter(map(_RANGE_OF, requests), dtype=_RANGE_DTYPE, count=R)
+        except OverflowError:  # a bound past 2^64: clamp in Python first
+            t = np.fromiter(((min(q.time_low, MAX_GT), min(q.time_high, MAX_GT), q.modulo, q.offset) for q in requests),
+                            dtype=_RANGE_DTYPE, count=R)
+        reqs["time_low"] = np.minimum(t["time_low"], np.uint64(MAX_GT))
+        reqs["time_high"] = np.minimum(t["time_high"], np.uint64(MAX_GT))
+        reqs["modulo"] = t["modulo"]
+        reqs["offset"] = t["offset"]
+        raws = list(map(_RAW_OF, bfs))
+        if len(set(map(len, raws))) == 1:
+            # one filter size (the MTU claim): the padding is the join's separator (an empty last item adds the
+            # last filter's)
+            first = len(raws[0])
+            step = (first + 3) & ~3
+            reqs["filter_offset"] = np.arange(R, dtype=np.uint64) * np.uint64(step)
+            raws.append(b"")
+            blob = (b"\x00" * (step - first)).join(raws)
         else:
-            for i, p in enumerate(prefixes):
-                reqs["prefix"][i, :len(p)] = np.frombuffer(p, dtype=np.uint8)
-        first = len(raws[0])
-        if all(len(r) == first for r in raws):
-            # one filter size (the MTU claim): the padding is the join's separator
-            pad = b"\x00" * ((-first) % 4)
-            blob = pad.join(raws) + pad
-        else:
+            sizes = np.fromiter(((len(r) + 3) & ~3 for r in raws), dtype=np.uint64, count=R)
+            reqs["filter_offset"] = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
             blob = b"".join(bytes(r) + b"\x00" * ((-len(r)) % 4) for r in raws)
         return reqs, R, blob
 
@@ -742,9 +775,7 @@ class SyncCommunity(object):
                 continue
             _native.check(rc)
             break
-        rows = out[:int(out_off[R])].astype(np.int64)
-        offs = out_off.tolist()
-        return [rows[offs[i]:offs[i + 1]] for i in range(R)]
+        return RowLists(out[:int(out_off[R])].view(np.int64), out_off.view(np.int64))
 
     def on_introduction_request_sync(self, messages, include_inactive=False):
         """The sync half of on_introduction_request (community.py:2531-2572) for a receive batch.
