@@ -461,6 +461,20 @@ class SyncCommunity(object):
         double_signed_sync table) is outside this path.  Returns the new store rows."""
         if not messages:
             return np.zeros(0, dtype=np.int64)
+        # what this batch needs is checked before anything is stored, so a refused batch changes neither copy
+        for m in messages:
+            meta = getattr(m, "meta", None)
+            dist = getattr(meta, "distribution", None)
+            history = isinstance(dist, LastSyncDistribution)
+            if history and getattr(meta, "double_signed", False) and not dist.custom_callback:
+                # the reference's history of a double-signed meta is per member pair, through double_signed_sync
+                # (dispersy.py:1567-1578, :1593-1594); pruning it per single member would delete the wrong rows
+                raise NotImplementedError("LastSyncDistribution history of a double-member-signed meta (%s): the "
+                                          "double_signed_sync table is outside this path" % getattr(meta, "name", "?"))
+            if self._store.member is None and (history or (isinstance(dist, FullSyncDistribution) and
+                                                           dist.enable_sequence_number)):
+                raise ValueError("store_messages: meta %s keeps per-member history; the store needs its member column"
+                                 % getattr(meta, "name", "?"))
         metas = [_meta_id(m) for m in messages]
         gts = [m.distribution.global_time for m in messages]
         members = [_member_id(m) for m in messages] if self._store.member is not None else None

@@ -129,6 +129,9 @@ struct ReqState {
     uint64_t out_base; // where this claim's output starts
     uint32_t exhausted;// every candidate of every meta visited
     uint32_t overflow; // output capacity exceeded (host retries with a larger capacity)
+    uint64_t cand_next;// a split window's next cursor (k_fill's parts run concurrently): k_compact commits it to cand
+    uint32_t commit;   // cand_next is pending
+    uint32_t pad;
 };
 
 // Device copy of one claim: the fields of dsy_request the kernels read, with the prefix bytes moved to a side

@@ -475,7 +475,9 @@ hipError_t launch_select_and_fix(const uint64_t* live_gt, const uint64_t* spans,
                                  uint64_t to_select, int higher, uint64_t* cand, uint64_t* out_spans, SelResult* res,
                                  hipStream_t stream) {
     const uint64_t cap = (uint64_t)J * (to_select + 1);
-    const bool lds = J > 1 && cap * 8 <= 64 * 1024;
+    // dynamic LDS beside the kernel's static __shared__ words (a few hundred bytes): stay under 64 KiB per workgroup so
+    // the launch also fits parts with 64 KiB of LDS (gfx950 has 160 KiB)
+    const bool lds = J > 1 && cap * 8 <= 64 * 1024 - 1024;
     hipLaunchKernelGGL(k_select_and_fix, dim3(1), dim3(kSelThreads), lds ? (size_t)cap * 8 : 0, stream, live_gt, spans,
                        J, pivot, to_select, higher, cand, lds ? 1u : 0u, out_spans, res);
     return hipGetLastError();

@@ -329,9 +329,11 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
     while (j < L.J && filled < W) {
         const Plan p = plan_at(j);
         if (c >= p.ncand) { ++j; c = 0; s = 0; continue; }
-        if (p.dense && p.dir != DSY_RANDOM && (p.mode == 1 || mod <= 1)) {
-            // One row per global time, consecutive: candidate -> row is arithmetic, no lookup and no scan.
-            // Candidates (ascending) whose global time lies in [g_lo, g_hi] are [i0, i1); the others have no row.
+        if (p.dir != DSY_RANDOM && ((p.dense && p.mode == 1) || (p.mode == 0 && mod <= 1))) {
+            // Candidate -> row is arithmetic, no lookup and no scan: a scan that keeps every live row of the span
+            // (candidate i is live row a + i), or an enumeration over a span with one row per global time,
+            // consecutive.  Candidates (ascending) whose global time lies in [g_lo, g_hi] are [i0, i1); the others
+            // have no row.
             uint64_t i0 = 0, i1 = p.ncand;
             if (p.mode == 1) {
                 i0 = p.g_lo > p.g0 ? (p.g_lo - p.g0 + mod - 1) / mod : 0;
@@ -622,16 +624,124 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
     }
 }
 
+// A split window: a claim that keeps every live row of a span (a scan with modulo 1, ASC or DESC) and has at least W
+// candidates left in its current meta fills its window with gridDim.y workgroups, part p taking pairs
+// [p * kBulkChunk, (p + 1) * kBulkChunk) -- candidate -> row is arithmetic, so every part knows its pairs' slots without
+// the others.  Each part sorts its own pairs by block count (the hashing kernel's lanes stay balanced: its 64-pair
+// chunks lie inside one part's sorted run).  Part 0 files the window; the cursor is committed by k_compact, since the
+// other parts read it while this launch runs.  (A config 5 claim whose filter covers its 10^5-10^6 rows walks them in
+// 2^18-pair windows: one workgroup per claim left the chip idle, 1-2 ms per window.)
+static constexpr uint64_t kBulkChunk = (uint64_t)kFillThreads * 8;
+
+__device__ __forceinline__ bool bulk_window(const RespondLaunch& L, const DevRequest& q, const ReqState& S,
+                                            const Plan& p) {
+    return S.meta < L.J && S.sub == 0 && p.mode == 0 && q.modulo <= 1 && p.dir != DSY_RANDOM && S.cand < p.ncand &&
+           p.ncand - S.cand >= L.window;
+}
+
+__device__ __forceinline__ void fill_bulk_part(const RespondLaunch& L, uint32_t a_slot, uint32_t part,
+                                               const DevRequest& q, ReqState* S, const Plan& p, uint64_t c) {
+    __shared__ uint32_t hist[kSortBins];
+    const uint64_t W = L.window;
+    const uint64_t base = (uint64_t)part * kBulkChunk;
+    if (base >= W) return;
+    const uint64_t n = W - base < kBulkChunk ? W - base : kBulkChunk;  // W is a multiple of 64
+    uint64_t* mask = L.miss_mask + (uint64_t)a_slot * (W / 64) + base / 64;
+    for (uint64_t w = threadIdx.x; w < n / 64; w += kFillThreads) mask[w] = 0;
+    uint64_t* out = L.pair_row + (uint64_t)a_slot * W;
+    uint32_t* out_len = L.pair_len + (uint64_t)a_slot * W;
+    const RowRec* __restrict__ rec = L.st.rec;
+    constexpr int kU = (int)(kBulkChunk / kFillThreads);
+    uint64_t row[kU];
+    uint32_t reg_off[kU], reg_len[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        const uint64_t t = threadIdx.x + (uint64_t)kFillThreads * u;
+        const uint64_t ci = c + base + (t < n ? t : 0);
+        const uint64_t lr = p.a + (p.dir == DSY_DESC ? p.ncand - 1 - ci : ci);
+        row[u] = L.st.live_row ? L.st.live_row[lr] : lr;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        const uint64_t t = threadIdx.x + (uint64_t)kFillThreads * u;
+        const RowRec rr = t < n ? rec[row[u]] : RowRec{};
+        reg_off[u] = (uint32_t)(rr.off >> 7);
+        reg_len[u] = rr.len;
+        if (t < n) {
+            out[base + t] = row[u];
+            out_len[base + t] = rr.len;
+        }
+    }
+    // this part's pairs in block-count order, longest first (as fill_claim's sort)
+    const uint32_t blk = q.hash_kind >= DSY_SHA384 ? 128u : 64u, lenb = q.hash_kind >= DSY_SHA384 ? 16u : 8u;
+    auto bin_of = [&](uint32_t len) {
+        return (uint32_t)kSortBins - 1u - min(n_blocks(q.prefix_len + len, blk, lenb), (uint32_t)kSortBins - 1);
+    };
+    for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads) hist[i] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+        if (threadIdx.x + (uint64_t)kFillThreads * u < n) atomicAdd(&hist[bin_of(reg_len[u])], 1u);
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const uint32_t per = kSortBins / 64, lane = threadIdx.x;
+        uint32_t sum = 0;
+        for (uint32_t i = 0; i < per; ++i) sum += hist[lane * per + i];
+        uint32_t incl = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t o = __shfl_up(incl, d, 64);
+            if ((int)lane >= d) incl += o;
+        }
+        uint32_t run = incl - sum;
+        for (uint32_t i = 0; i < per; ++i) {
+            const uint32_t h = hist[lane * per + i];
+            hist[lane * per + i] = run;
+            run += h;
+        }
+    }
+    __syncthreads();
+    PairTask* task = L.task + (uint64_t)a_slot * W + base;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        const uint64_t t = threadIdx.x + (uint64_t)kFillThreads * u;
+        if (t < n) {
+            PairTask tk;
+            tk.off = ((uint64_t)reg_off[u] << 7) + kLineBias;
+            tk.len = reg_len[u];
+            tk.slot = (uint32_t)(base + t);
+            task[atomicAdd(&hist[bin_of(tk.len)], 1u)] = tk;
+        }
+    }
+    if (part == 0 && threadIdx.x == 0) {
+        S->n_window = W;
+        S->cand_next = c + W;
+        S->commit = 1;
+        atomicMax(&L.flags[kFlagChunks], (uint32_t)(W / 64));
+    }
+}
+
 __global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) k_fill(RespondLaunch L) {
-    const uint32_t a_slot = blockIdx.x;
+    const uint32_t a_slot = blockIdx.x, part = blockIdx.y;
     const uint64_t clk0 = L.fill_clock ? __builtin_amdgcn_s_memtime() : 0;
     const uint32_t r = L.act[a_slot];
     ReqState* S = &L.state[r];
     if (S->done) {
-        if (threadIdx.x == 0) S->n_window = 0;
+        if (part == 0 && threadIdx.x == 0) S->n_window = 0;
         return;
     }
     const Plan* plans = L.plans + (uint64_t)r * L.J;
+    if (gridDim.y > 1) {  // a split window when the claim allows one (every part decides alike: S is not written here)
+        const ReqState st = *S;
+        if (st.meta < L.J) {
+            const Plan p = plans[st.meta];
+            if (bulk_window(L, L.reqs[r], st, p)) {
+                fill_bulk_part(L, a_slot, part, L.reqs[r], S, p, st.cand);
+                return;
+            }
+        }
+        if (part > 0) return;
+    }
     fill_claim(L, a_slot, r, L.reqs[r], S, S->meta, S->cand, S->sub, [&](uint32_t j) { return plans[j]; }, clk0, clk0);
 }
 
@@ -988,6 +1098,10 @@ __global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
     }
     overflow = __any(overflow) ? 1u : 0u;
     if (lane == 0) {
+        if (S->commit) {  // a split window's cursor (k_fill's parts read the old one while they ran)
+            S->cand = S->cand_next;
+            S->commit = 0;
+        }
         S->emitted = emitted;
         L.emitted_n[r] = emitted;
         S->spent = spent;
@@ -1089,7 +1203,9 @@ hipError_t launch_setup(const RespondLaunch& L, const void* h_src, void* d_dst, 
 
 hipError_t launch_fill(const RespondLaunch& L) {
     if (!L.n_act) return hipSuccess;
-    hipLaunchKernelGGL(k_fill, dim3(L.n_act), dim3(kFillThreads), 0, L.stream, L);
+    // windows of >= 2 bulk chunks may split over workgroups (k_fill's parts)
+    const uint32_t parts = L.window >= 2 * kBulkChunk ? (uint32_t)((L.window + kBulkChunk - 1) / kBulkChunk) : 1u;
+    hipLaunchKernelGGL(k_fill, dim3(L.n_act, parts), dim3(kFillThreads), 0, L.stream, L);
     return hipGetLastError();
 }
 

@@ -65,10 +65,13 @@ class DirectDistribution(object):
 
 
 class MetaMessage(object):
-    """The subset of a Message meta the sync path needs: name, database id (sync.meta_message) and distribution."""
+    """The subset of a Message meta the sync path needs: name, database id (sync.meta_message) and distribution;
+    double_signed: the meta uses DoubleMemberAuthentication (authentication.py), whose messages the reference also
+    records in the double_signed_sync table (dispersy.py:1537-1541)."""
 
-    def __init__(self, name, database_id, distribution):
+    def __init__(self, name, database_id, distribution, double_signed=False):
         self.name, self.database_id, self.distribution = name, database_id, distribution
+        self.double_signed = bool(double_signed)
 
     @property
     def syncable(self):

@@ -158,3 +158,35 @@ def test_last_sync_history_matches_reference(lazy):
     (got,) = com.respond([ClaimRequest(1, 10 ** 6, 1, 0, BloomFilter(1024, 0.01, b"\x00"))], include_inactive=True,
                          byte_limit=1 << 40)
     assert sorted(store.rowid[got].tolist()) == want
+
+
+def test_store_messages_refuses_what_it_cannot_keep_consistent():
+    """store_messages checks a batch before storing any of it: a LastSync meta without the store's member column, and
+    the history of a double-member-signed LastSync meta (double_signed_sync, dispersy.py:1567-1578), are refused with
+    both store copies unchanged (CPU: the store is not on the device)."""
+    import pytest as _pytest
+    from dispersy_amd.community import SyncCommunity
+    from dispersy_amd.distribution import LastSyncDistribution, MetaMessage
+    from dispersy_amd.store import SyncStore
+
+    class D(object):
+        def __init__(self, gt):
+            self.global_time = gt
+
+    class M(object):
+        def __init__(self, meta, gt, member):
+            self.meta, self.packet, self.distribution, self.member = meta, b"p%d" % gt, D(gt), member
+            self.database_id = meta.database_id
+
+    last = MetaMessage("last", 1, LastSyncDistribution("ASC", 128, history_size=2))
+    store = SyncStore.from_rows([(1, 5, 1, 0, b"x")], ctx=object())  # no member column
+    com = SyncCommunity(store, [last], global_time=10)
+    with _pytest.raises(ValueError):
+        com.store_messages([M(last, 7, 3)])
+    assert store.n == 1
+    dbl = MetaMessage("dbl", 2, LastSyncDistribution("ASC", 128, history_size=1), double_signed=True)
+    store2 = SyncStore.from_rows([(1, 5, 2, 0, b"x", 4)], ctx=object())
+    com2 = SyncCommunity(store2, [dbl], global_time=10)
+    with _pytest.raises(NotImplementedError):
+        com2.store_messages([M(dbl, 7, 4)])
+    assert store2.n == 1
