@@ -1840,6 +1840,11 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
     if ((rc = ws_get(w, "pair_len", pool * 4, &d_len))) return rc;
     if ((rc = ws_get(w, "miss_mask", pool / 8 + 64, &d_miss))) return rc;
     if ((rc = ws_get(w, "task", pool * sizeof(PairTask), &d_task))) return rc;
+    void* d_bulk;  // split windows' sort state: [R][kSortBins] histogram + cursors, zero between windows
+    bool bulk_fresh = false;
+    const size_t bulk_b = (size_t)std::max<uint32_t>(R, 1) * 2 * 1024 * 4;
+    if ((rc = ws_get(w, "bulk_sort", bulk_b, &d_bulk, &bulk_fresh))) return rc;
+    if (bulk_fresh) HIP_TRY(hipMemsetAsync(d_bulk, 0, bulk_b, st));
     uint8_t* h_in;
     if ((rc = stage_get(w, in_b + kHostHead + act_done_b, &h_in))) return rc;
     jb.h_in = h_in;
@@ -1937,6 +1942,8 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
     L.pair_len = (uint32_t*)d_len;
     L.miss_mask = (uint64_t*)d_miss;
     L.task = (PairTask*)d_task;
+    L.bulk_hist = (uint32_t*)d_bulk;
+    L.bulk_cur = (uint32_t*)d_bulk + (size_t)std::max<uint32_t>(R, 1) * 1024;
     L.flags = (uint32_t*)(io + cnt_b);
     L.counters = (uint64_t*)io;
     L.stream = st;

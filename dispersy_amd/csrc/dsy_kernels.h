@@ -177,6 +177,9 @@ struct RespondLaunch {
     uint64_t* pair_off;       // device [pool]: its packet's blob offset
     uint32_t* pair_len;       // device [pool]: its packet's length
     PairTask* task;           // device [R*W]: per-claim hashing order (window slots sorted by block count)
+    uint32_t* bulk_hist;      // device [R][kSortBins]: a split window's block-count histogram (k_fill's parts), zero
+                              // outside a window (k_compact clears what a window used)
+    uint32_t* bulk_cur;       // device [R][kSortBins]: the split window's sort cursors (k_fill_sort)
     uint64_t* miss_mask;      // device [n_act * W / 64]: bit t of claim slot a = window pair t is missing
     uint64_t* out;            // device [sum cap]
     uint32_t* flags;          // device [16], zeroed by k_setup: [kFlagChunks] the window's longest claim in 64-pair

@@ -627,16 +627,23 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
 // A split window: a claim that keeps every live row of a span (a scan with modulo 1, ASC or DESC) and has at least W
 // candidates left in its current meta fills its window with gridDim.y workgroups, part p taking pairs
 // [p * kBulkChunk, (p + 1) * kBulkChunk) -- candidate -> row is arithmetic, so every part knows its pairs' slots without
-// the others.  Each part sorts its own pairs by block count (the hashing kernel's lanes stay balanced: its 64-pair
-// chunks lie inside one part's sorted run).  Part 0 files the window; the cursor is committed by k_compact, since the
-// other parts read it while this launch runs.  (A config 5 claim whose filter covers its 10^5-10^6 rows walks them in
-// 2^18-pair windows: one workgroup per claim left the chip idle, 1-2 ms per window.)
+// the others.  The block-count sort stays one sort over the whole window (a heavy-tailed window sorted part by part
+// spreads its few 64 KB packets over many hashing waves): the parts add their histograms into the claim's
+// bulk_hist, and k_fill_sort places every part's pairs from the scanned totals.  Part 0 files the window; the cursor
+// is committed by k_compact, since the other parts read it while this launch runs.  (A config 5 claim whose filter
+// covers its 10^5-10^6 rows walks them in 2^18-pair windows: one workgroup per claim left the chip idle, 1-2 ms per
+// window.)
 static constexpr uint64_t kBulkChunk = (uint64_t)kFillThreads * 8;
 
 __device__ __forceinline__ bool bulk_window(const RespondLaunch& L, const DevRequest& q, const ReqState& S,
                                             const Plan& p) {
     return S.meta < L.J && S.sub == 0 && p.mode == 0 && q.modulo <= 1 && p.dir != DSY_RANDOM && S.cand < p.ncand &&
            p.ncand - S.cand >= L.window;
+}
+
+__device__ __forceinline__ uint32_t sort_bin(const DevRequest& q, uint32_t len) {
+    const uint32_t blk = q.hash_kind >= DSY_SHA384 ? 128u : 64u, lenb = q.hash_kind >= DSY_SHA384 ? 16u : 8u;
+    return (uint32_t)kSortBins - 1u - min(n_blocks(q.prefix_len + len, blk, lenb), (uint32_t)kSortBins - 1);
 }
 
 __device__ __forceinline__ void fill_bulk_part(const RespondLaunch& L, uint32_t a_slot, uint32_t part,
@@ -648,12 +655,13 @@ __device__ __forceinline__ void fill_bulk_part(const RespondLaunch& L, uint32_t 
     const uint64_t n = W - base < kBulkChunk ? W - base : kBulkChunk;  // W is a multiple of 64
     uint64_t* mask = L.miss_mask + (uint64_t)a_slot * (W / 64) + base / 64;
     for (uint64_t w = threadIdx.x; w < n / 64; w += kFillThreads) mask[w] = 0;
+    for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads) hist[i] = 0;
     uint64_t* out = L.pair_row + (uint64_t)a_slot * W;
+    uint64_t* out_off = L.pair_off + (uint64_t)a_slot * W;
     uint32_t* out_len = L.pair_len + (uint64_t)a_slot * W;
     const RowRec* __restrict__ rec = L.st.rec;
     constexpr int kU = (int)(kBulkChunk / kFillThreads);
     uint64_t row[kU];
-    uint32_t reg_off[kU], reg_len[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
         const uint64_t t = threadIdx.x + (uint64_t)kFillThreads * u;
@@ -661,32 +669,54 @@ __device__ __forceinline__ void fill_bulk_part(const RespondLaunch& L, uint32_t 
         const uint64_t lr = p.a + (p.dir == DSY_DESC ? p.ncand - 1 - ci : ci);
         row[u] = L.st.live_row ? L.st.live_row[lr] : lr;
     }
+    __syncthreads();  // hist cleared
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
         const uint64_t t = threadIdx.x + (uint64_t)kFillThreads * u;
-        const RowRec rr = t < n ? rec[row[u]] : RowRec{};
-        reg_off[u] = (uint32_t)(rr.off >> 7);
-        reg_len[u] = rr.len;
         if (t < n) {
+            const RowRec rr = rec[row[u]];
             out[base + t] = row[u];
+            out_off[base + t] = rr.off;
             out_len[base + t] = rr.len;
+            atomicAdd(&hist[sort_bin(q, rr.len)], 1u);
         }
     }
-    // this part's pairs in block-count order, longest first (as fill_claim's sort)
-    const uint32_t blk = q.hash_kind >= DSY_SHA384 ? 128u : 64u, lenb = q.hash_kind >= DSY_SHA384 ? 16u : 8u;
-    auto bin_of = [&](uint32_t len) {
-        return (uint32_t)kSortBins - 1u - min(n_blocks(q.prefix_len + len, blk, lenb), (uint32_t)kSortBins - 1);
-    };
-    for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads) hist[i] = 0;
     __syncthreads();
-#pragma unroll
-    for (int u = 0; u < kU; ++u)
-        if (threadIdx.x + (uint64_t)kFillThreads * u < n) atomicAdd(&hist[bin_of(reg_len[u])], 1u);
+    uint32_t* gh = L.bulk_hist + (uint64_t)a_slot * kSortBins;
+    for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads)
+        if (hist[i]) atomicAdd(&gh[i], hist[i]);
+    if (part == 0 && threadIdx.x == 0) {
+        S->n_window = W;
+        S->cand_next = c + W;
+        S->commit = 1;
+        atomicMax(&L.flags[kFlagChunks], (uint32_t)(W / 64));
+    }
+}
+
+// The split windows' sort: every part places its pairs at the claim's bin starts (scan of bulk_hist) plus the ranges
+// it reserves per bin in bulk_cur (one atomic per part and bin); slots inside a bin come in no particular order.
+__global__ void __launch_bounds__(kFillThreads) k_fill_sort(RespondLaunch L) {
+    __shared__ uint32_t start[kSortBins];
+    __shared__ uint32_t hist[kSortBins];
+    const uint32_t a_slot = blockIdx.x, part = blockIdx.y;
+    const uint32_t r = L.act[a_slot];
+    const ReqState* S = &L.state[r];
+    if (S->done || !S->commit) return;  // not a split window (k_fill sorted it whole)
+    const uint64_t W = L.window;
+    const uint64_t base = (uint64_t)part * kBulkChunk;
+    if (base >= W) return;
+    const uint64_t n = W - base < kBulkChunk ? W - base : kBulkChunk;
+    const DevRequest& q = L.reqs[r];
+    const uint32_t* gh = L.bulk_hist + (uint64_t)a_slot * kSortBins;
+    for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads) {
+        start[i] = gh[i];
+        hist[i] = 0;
+    }
     __syncthreads();
-    if (threadIdx.x < 64) {
+    if (threadIdx.x < 64) {  // exclusive scan of the claim's totals by one wave
         const uint32_t per = kSortBins / 64, lane = threadIdx.x;
         uint32_t sum = 0;
-        for (uint32_t i = 0; i < per; ++i) sum += hist[lane * per + i];
+        for (uint32_t i = 0; i < per; ++i) sum += start[lane * per + i];
         uint32_t incl = sum;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -695,29 +725,40 @@ __device__ __forceinline__ void fill_bulk_part(const RespondLaunch& L, uint32_t 
         }
         uint32_t run = incl - sum;
         for (uint32_t i = 0; i < per; ++i) {
-            const uint32_t h = hist[lane * per + i];
-            hist[lane * per + i] = run;
+            const uint32_t h = start[lane * per + i];
+            start[lane * per + i] = run;
             run += h;
         }
     }
+    const uint32_t* len_w = L.pair_len + (uint64_t)a_slot * W + base;
+    const uint64_t* off_w = L.pair_off + (uint64_t)a_slot * W + base;
+    constexpr int kU = (int)(kBulkChunk / kFillThreads);
+    uint32_t len[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+        const uint64_t t = threadIdx.x + (uint64_t)kFillThreads * u;
+        len[u] = t < n ? len_w[t] : 0u;
+    }
+    __syncthreads();  // starts scanned
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+        if (threadIdx.x + (uint64_t)kFillThreads * u < n) atomicAdd(&hist[sort_bin(q, len[u])], 1u);
     __syncthreads();
-    PairTask* task = L.task + (uint64_t)a_slot * W + base;
+    uint32_t* gc = L.bulk_cur + (uint64_t)a_slot * kSortBins;
+    for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads)
+        if (hist[i]) hist[i] = start[i] + atomicAdd(&gc[i], hist[i]);  // this part's range in bin i
+    __syncthreads();
+    PairTask* task = L.task + (uint64_t)a_slot * W;
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
         const uint64_t t = threadIdx.x + (uint64_t)kFillThreads * u;
         if (t < n) {
             PairTask tk;
-            tk.off = ((uint64_t)reg_off[u] << 7) + kLineBias;
-            tk.len = reg_len[u];
+            tk.off = off_w[t];
+            tk.len = len[u];
             tk.slot = (uint32_t)(base + t);
-            task[atomicAdd(&hist[bin_of(tk.len)], 1u)] = tk;
+            task[atomicAdd(&hist[sort_bin(q, len[u])], 1u)] = tk;
         }
-    }
-    if (part == 0 && threadIdx.x == 0) {
-        S->n_window = W;
-        S->cand_next = c + W;
-        S->commit = 1;
-        atomicMax(&L.flags[kFlagChunks], (uint32_t)(W / 64));
     }
 }
 
@@ -1097,11 +1138,17 @@ __global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
         }
     }
     overflow = __any(overflow) ? 1u : 0u;
-    if (lane == 0) {
-        if (S->commit) {  // a split window's cursor (k_fill's parts read the old one while they ran)
+    if (S->commit) {  // a split window: its sort state cleared, its cursor (k_fill's parts read the old one) committed
+        uint32_t* gh = L.bulk_hist + (uint64_t)a_slot * kSortBins;
+        uint32_t* gc = L.bulk_cur + (uint64_t)a_slot * kSortBins;
+        for (uint32_t i = lane; i < kSortBins; i += 64) gh[i] = gc[i] = 0;
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {
             S->cand = S->cand_next;
             S->commit = 0;
         }
+    }
+    if (lane == 0) {
         S->emitted = emitted;
         L.emitted_n[r] = emitted;
         S->spent = spent;
@@ -1203,9 +1250,10 @@ hipError_t launch_setup(const RespondLaunch& L, const void* h_src, void* d_dst, 
 
 hipError_t launch_fill(const RespondLaunch& L) {
     if (!L.n_act) return hipSuccess;
-    // windows of >= 2 bulk chunks may split over workgroups (k_fill's parts)
+    // windows of >= 2 bulk chunks may split over workgroups (k_fill's parts, then k_fill_sort)
     const uint32_t parts = L.window >= 2 * kBulkChunk ? (uint32_t)((L.window + kBulkChunk - 1) / kBulkChunk) : 1u;
     hipLaunchKernelGGL(k_fill, dim3(L.n_act, parts), dim3(kFillThreads), 0, L.stream, L);
+    if (parts > 1) hipLaunchKernelGGL(k_fill_sort, dim3(L.n_act, parts), dim3(kFillThreads), 0, L.stream, L);
     return hipGetLastError();
 }
 
