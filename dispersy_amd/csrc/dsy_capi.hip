@@ -123,6 +123,12 @@ struct dsy_ctx {
     uint32_t bloom_grid = 0; // DSY_BLOOM_GRID at creation: k_bloom grid cap (0: 2 x max_grid)
     uint32_t pair_grid = 0;  // DSY_PAIR_GRID at creation: k_pair_test grid cap (0: max_grid, 8 workgroups per CU)
     int or_mode = 1;     // DSY_OR_MODE at creation: filter-build atomics (filter_set_all OR_MODE, dsy_message.h)
+    // DSY_POOL at creation: bit k = hash kind k's responder pairs are pooled across claims (k_pool_scatter) -- MD5,
+    // SHA-1 and SHA-256 only; DSY_POOL_QUEUE: the pooled hashing takes its wave-tasks from a queue
+    uint32_t pool_kinds = (1u << DSY_SHA1) | (1u << DSY_SHA256);
+    int pool_queue = 0;
+    int pool_deal = 0;   // DSY_POOL_DEAL: the pooled hashing's resident-grid deal (k_pair_test<POOL>)
+    uint32_t direct_kinds = 0;  // DSY_PAIR_DIRECT: bit k = hash kind k's responder hashing uses direct loads
     uint32_t timing = 0;  // bit i: bracket class i with events
     std::vector<PendingTimer> pending;
     std::vector<hipEvent_t> event_pool;
@@ -486,6 +492,11 @@ int dsy_ctx_create(int device, dsy_ctx** out) {
     if (const char* v = getenv("DSY_OR_MODE")) c->or_mode = atoi(v);
     if (const char* v = getenv("DSY_PAIR_GRID")) c->pair_grid = (uint32_t)atoi(v);
     if (const char* v = getenv("DSY_BLOOM_GRID")) c->bloom_grid = (uint32_t)atoi(v);
+    if (const char* v = getenv("DSY_POOL")) c->pool_kinds = (uint32_t)strtoul(v, nullptr, 0);
+    if (const char* v = getenv("DSY_POOL_QUEUE")) c->pool_queue = atoi(v);
+    if (const char* v = getenv("DSY_POOL_DEAL")) c->pool_deal = atoi(v);
+    if (const char* v = getenv("DSY_PAIR_DIRECT")) c->direct_kinds = (uint32_t)strtoul(v, nullptr, 0);
+    c->pool_kinds &= (1u << DSY_MD5) | (1u << DSY_SHA1) | (1u << DSY_SHA256);
     hipHostMalloc(&c->pinned, 4096, hipHostMallocDefault);
     *out = c;
     return DSY_OK;
@@ -1736,15 +1747,49 @@ static int job_window(dsy_ctx* c, RespondSlot& sl) {
                        (unsigned long long)mx_sel, (unsigned long long)(srt / n), (unsigned long long)mx_srt);
         L.fill_clock = nullptr;
     }
+    // DSY_PAIR_TRACE=<path>: every window's wave-task records are appended to <path> (WaveTrace, 32 B each, after a
+    // 16-byte header {records, window, kernel start/end unknown}); diagnostics only, the window waits for them
+    static const char* trace_path = getenv("DSY_PAIR_TRACE");
+    void* d_tr = nullptr;
+    const uint32_t trace_cap = 1u << 20;
+    if (trace_path) {
+        if ((rc = ws_get(sl.w, "pair_trace", (size_t)trace_cap * sizeof(WaveTrace) + 64, &d_tr))) return rc;
+        HIP_TRY(hipMemsetAsync(d_tr, 0, 64, st));
+        L.trace_n = (uint32_t*)d_tr;
+        L.trace = (WaveTrace*)((uint8_t*)d_tr + 64);
+        L.trace_cap = trace_cap;
+    }
     for (size_t f = 0; f < jb.fam_active.size(); ++f) {
         if (!runs[f].second) continue;
         const int fid = jb.fam_id[f];
         timer_dispatch(c, &t, kTimePairTest, &L.ev_start, &L.ev_stop);
         const int kc = fid / 2;
-        HIP_TRY(launch_pair_test_list(L, kc / 3, kc % 3 == 0 ? 2 : kc % 3 == 1 ? 4 : 8, fid % 2 == 1,
-                                      jb.d_slots + runs[f].first, (uint32_t)runs[f].second));
+        const uint32_t chunk = kc % 3 == 0 ? 2 : kc % 3 == 1 ? 4 : 8;
+        if ((L.pool_mask >> fid) & 1u)
+            HIP_TRY(launch_pair_test_pooled(L, kc / 3, chunk, fid % 2 == 1, (uint32_t)fid, jb.d_slots + runs[f].first,
+                                            (uint32_t)runs[f].second));
+        else
+            HIP_TRY(launch_pair_test_list(L, kc / 3, chunk, fid % 2 == 1, jb.d_slots + runs[f].first,
+                                          (uint32_t)runs[f].second));
         timer_dispatched(c, &t);
         L.ev_start = L.ev_stop = nullptr;
+    }
+    if (trace_path) {
+        uint32_t n = 0;
+        HIP_TRY(hipMemcpyAsync(&n, d_tr, 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        n = std::min(n, trace_cap);
+        std::vector<WaveTrace> rec(n);
+        if (n) HIP_TRY(hipMemcpyAsync(rec.data(), L.trace, (size_t)n * sizeof(WaveTrace), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (FILE* fp = fopen(trace_path, "ab")) {
+            const uint64_t head[2] = {n, L.window};
+            fwrite(head, 8, 2, fp);
+            if (n) fwrite(rec.data(), sizeof(WaveTrace), n, fp);
+            fclose(fp);
+        }
+        L.trace = nullptr;
+        L.trace_n = nullptr;
     }
     timer_begin(c, &t, kTimeCompact, st);
     HIP_TRY(launch_compact(L));
@@ -1769,7 +1814,6 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
     // ---- validate claims (payload.py:89-101, conversion.py:772-789) and their filters; group them by hash family
     // (kind x chunk width: one pair-test launch per family)
     // family id = (kind * 3 + chunk class) * 2 + long prefix (> 4 bytes: the byte-wise hashing path)
-    constexpr int kFamilies = 5 * 3 * 2;
     std::vector<uint32_t> fam_members[kFamilies];
     uint64_t memo_m = 0;  // check_family of the previous claim's (m, k): a batch's claims share one filter shape
     uint32_t memo_k = 0, memo_chunk = 0;
@@ -1845,6 +1889,18 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
     const size_t bulk_b = (size_t)std::max<uint32_t>(R, 1) * 2 * 1024 * 4;
     if ((rc = ws_get(w, "bulk_sort", bulk_b, &d_bulk, &bulk_fresh))) return rc;
     if (bulk_fresh) HIP_TRY(hipMemsetAsync(d_bulk, 0, bulk_b, st));
+    // pooled families (c->pool_kinds): the pooled order and the families' counts (zero outside a window)
+    uint32_t pool_mask = 0;
+    if (!c->pair_diag && pool <= 0xffffffffull)
+        for (int f = 0; f < kFamilies; ++f)
+            if (!fam_members[f].empty() && ((c->pool_kinds >> (f / 6)) & 1u)) pool_mask |= 1u << f;
+    void *d_pool = nullptr, *d_pool_counts = nullptr;
+    if (pool_mask) {
+        bool pc_fresh = false;
+        if ((rc = ws_get(w, "pool_task", pool * sizeof(PoolTask), &d_pool))) return rc;
+        if ((rc = ws_get(w, "pool_counts", sizeof(PoolCounts), &d_pool_counts, &pc_fresh))) return rc;
+        if (pc_fresh) HIP_TRY(hipMemsetAsync(d_pool_counts, 0, sizeof(PoolCounts), st));
+    }
     uint8_t* h_in;
     if ((rc = stage_get(w, in_b + kHostHead + act_done_b, &h_in))) return rc;
     jb.h_in = h_in;
@@ -1948,7 +2004,13 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
     L.counters = (uint64_t*)io;
     L.stream = st;
     L.diag = c->pair_diag;
+    L.direct_kinds = c->direct_kinds;
     L.grid_cap = c->pair_grid ? c->pair_grid : c->max_grid;
+    L.pool_mask = pool_mask;
+    L.pool_queue = c->pool_queue;
+    L.pool_deal = c->pool_deal;
+    L.pool_counts = (PoolCounts*)d_pool_counts;
+    L.pool = (PoolTask*)d_pool;
 
     // ---- per-claim output capacity: every emitted packet but the last costs >= min_len bytes of budget, so a
     // claim sends at most byte_limit / min_len + 2 packets.  When that bound is small the capacities and output

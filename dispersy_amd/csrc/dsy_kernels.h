@@ -28,6 +28,26 @@ struct __attribute__((aligned(16))) PairTask {
     uint32_t slot;
 };
 
+// One (claim, packet) pair of a pooled family (k_pool_scatter -> k_pair_test<POOL>): the family's pairs of every
+// active claim in one block-count order, so a hashing wave mixes claims and its 64 lanes run the same number of
+// blocks.  The packet is line `line` of the store's line copy (+ kLineBias); a_slot / slot name the claim's window
+// slot and the pair's place in its window.
+struct __attribute__((aligned(16))) PoolTask {
+    uint32_t line;
+    uint32_t len;
+    uint32_t a_slot;
+    uint32_t slot;
+};
+// per hash family: block-count histogram of the window's pooled pairs (k_fill) and the scatter's cursors
+static constexpr uint32_t kPoolBins = 1024;
+static constexpr uint32_t kFamilies = 5 * 3 * 2;  // (hash kind x chunk class) x long-prefix flag, as respond_core
+struct PoolCounts {
+    uint32_t hist[kFamilies][kPoolBins];
+    uint32_t cur[kFamilies][kPoolBins];
+    uint32_t total[kFamilies];  // the family's pooled pairs in this window (k_pool_scatter)
+    uint32_t next[kFamilies];   // wave-task queue head (k_pair_test<POOL> with pool_queue)
+};
+
 // A store row's packet in the line copy: starts kLineBias (dsy_message.h) bytes into a 128-byte line of
 // StoreView::lines.
 struct RowRec {
@@ -82,6 +102,14 @@ hipError_t launch_len_sort(const LenSort& s, const uint64_t* offsets, const uint
                            uint32_t* d_bins /* 1024 */, PairTask* d_tasks, uint32_t max_grid, hipStream_t stream);
 
 // ------------------------------------------------------------------------------------------ responder
+// One hashing wave-task as DSY_PAIR_TRACE records it: where it ran (HW_ID, XCC_ID), when (s_memrealtime, 100 MHz)
+// and how long its longest lane was (blocks).
+struct WaveTrace {
+    uint32_t hw_id, xcc_id;
+    uint64_t t0, t1;
+    uint32_t blocks, task;
+};
+
 // Store view the responder kernels read.  `live` rows are the rows with undone == 0, in index order.
 
 struct StoreView {
@@ -185,13 +213,27 @@ struct RespondLaunch {
     uint32_t* flags;          // device [16], zeroed by k_setup: [kFlagChunks] the window's longest claim in 64-pair
                               // chunks (k_fill atomicMax, read by k_pair_test, reset by k_compact)
     uint64_t* fill_clock;     // optional [n_act][4] s_memtime stamps of k_fill phases (DSY_FILL_PROFILE)
+    WaveTrace* trace;         // optional (DSY_PAIR_TRACE): one record per k_pair_test wave-task, trace_n[0] counts them
+    uint32_t* trace_n;
+    uint32_t trace_cap;
     int diag;                 // k_pair_test DIAG (MD5 / SHA-1, 2-byte chunks): 0 product, 1 no loads, 2 loads only
+    uint32_t direct_kinds;    // bit k: hash kind k hashes with direct loads, not the LDS-DMA line staging
     uint32_t grid_cap;        // k_pair_test workgroups at most (0: 2048)
     hipEvent_t ev_start, ev_stop;  // when set: recorded by k_pair_test's own dispatch (launch_timed)
     uint64_t* counters;       // device [kCntSpread][kCntN]: pairs hashed, compression blocks, packet bytes, pairs the reference
                               // would have hashed (it stops at the byte limit), lane-block slots of the hashing waves
+    uint32_t pool_mask;       // bit f: family f's pairs are pooled across claims (k_fill counts, k_pool_scatter orders)
+    int pool_queue;           // k_pair_test<POOL>: waves take wave-tasks from a queue instead of a grid stride
+    int pool_deal;            // k_pair_test<POOL>: resident grid, wave-tasks dealt so each SIMD's waves sum to the mean
+    PoolCounts* pool_counts;  // device, zero outside a window (k_pair_test<POOL> clears its family's)
+    PoolTask* pool;           // device [pool]: the pooled order of the family being hashed
     hipStream_t stream;
 };
+
+// the family id respond_core groups claims by
+__device__ __host__ __forceinline__ uint32_t family_id(uint32_t kind, uint32_t chunk, uint32_t prefix_len) {
+    return (kind * 3 + (chunk == 2 ? 0u : chunk == 4 ? 1u : 2u)) * 2 + (prefix_len > 4 || prefix_len == 0 ? 1u : 0u);
+}
 
 // copy the staged claims (pinned host h_src -> d_dst), zero d_zero, plans, upper bounds, and (per_claim_cap != 0)
 // the per-claim capacities and states
@@ -207,6 +249,10 @@ hipError_t launch_fill_first(const RespondLaunch& L, const void* h_src, void* d_
 // long_prefix: the listed claims' prefixes are longer than 4 bytes (hashed without the LDS-DMA staging)
 hipError_t launch_pair_test_list(const RespondLaunch& L, int kind, uint32_t chunk, bool long_prefix,
                                  const uint32_t* d_list, uint32_t n);
+// a pooled family (bit fam of L.pool_mask): its listed claims' window pairs into L.pool in block-count order
+// (k_pool_scatter), then one hashing launch over the pool (k_pair_test<POOL>)
+hipError_t launch_pair_test_pooled(const RespondLaunch& L, int kind, uint32_t chunk, bool long_prefix, uint32_t fam,
+                                   const uint32_t* d_list, uint32_t n);
 hipError_t launch_compact(const RespondLaunch& L);
 hipError_t launch_pack(const RespondLaunch& L, uint64_t* packed, uint64_t* packed_offsets, uint64_t* d_scan_tmp);
 // copy each row's packet from (blob, offsets) to its line-aligned place rec[i].off in lines

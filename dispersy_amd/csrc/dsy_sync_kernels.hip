@@ -275,6 +275,29 @@ __device__ __forceinline__ void enum_range(const uint64_t* __restrict__ gt, cons
     *y = ly;
 }
 static constexpr uint32_t kSortBins = 1024;
+static_assert(kSortBins == kPoolBins, "a pooled family's histogram has k_fill's bins");
+
+// exclusive scan of kSortBins LDS counters in place, by the first wave of the workgroup (the others idle); the sum
+// of the counters goes to *total when given
+__device__ __forceinline__ void bins_exclusive_scan(uint32_t* bins, uint32_t* total = nullptr) {
+    if (threadIdx.x >= 64) return;
+    const uint32_t per = kSortBins / 64, lane = threadIdx.x;
+    uint32_t sum = 0;
+    for (uint32_t i = 0; i < per; ++i) sum += bins[lane * per + i];
+    uint32_t incl = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d, 64);
+        if ((int)lane >= d) incl += o;
+    }
+    uint32_t run = incl - sum;
+    for (uint32_t i = 0; i < per; ++i) {
+        const uint32_t h = bins[lane * per + i];
+        bins[lane * per + i] = run;
+        run += h;
+    }
+    if (total && lane == 63) *total = incl;
+}
 
 __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* lds, uint64_t* total) {
     // lds: kFillWaves + 1 words.  Wave-level inclusive scans (no barrier), one LDS round for the wave totals.
@@ -308,6 +331,9 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
                                            uint64_t clk_start, uint64_t clk0) {
     __shared__ uint64_t scan[kFillWaves + 2];
     __shared__ uint32_t first_cross;
+    constexpr int kCandRuns = kFillThreads * 2;  // kBatch below: a round's candidates
+    __shared__ uint32_t run_pos[kCandRuns];       // a round's candidates: first output position (round-relative)
+    __shared__ uint64_t run_x[kCandRuns];         // and first live row
     const uint64_t W = L.window;
     // this window's missing-pair bits of the claim start clear (k_pair_test sets them)
     for (uint64_t w = threadIdx.x; w < W / 64; w += kFillThreads) L.miss_mask[(uint64_t)a_slot * (W / 64) + w] = 0;
@@ -326,6 +352,7 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
     // kFillThreads * kCand candidates (the fill is latency-bound: fewer, wider rounds)
     constexpr int kCand = 2;
     constexpr uint64_t kBatch = (uint64_t)kFillThreads * kCand;
+    static_assert(kBatch == kCandRuns, "one LDS run slot per candidate of a round");
     while (j < L.J && filled < W) {
         const Plan p = plan_at(j);
         if (c >= p.ncand) { ++j; c = 0; s = 0; continue; }
@@ -473,20 +500,41 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
             }
             at += cnts[u];
         }
-        at = pos;
+        // the extra rows of shared global times: when a candidate of this round holds more than one row, the
+        // workgroup emits them together -- thread i takes the round's output positions i, i + 256, ..., its
+        // candidate found by binary search over the candidates' starts in LDS -- so a global time shared by 10^5
+        // rows (config 5's Zipf global times) is not walked by one thread
+        bool many = false;
 #pragma unroll
-        for (int u = 0; u < kCand; ++u) {
-            for (uint64_t e = 1; e < cnts[u]; ++e) {
-                const uint64_t dst = filled + at + e;
-                if (dst >= W) break;
-                const uint64_t lr = p.dir == DSY_DESC ? xs[u] - e : xs[u] + e;
+        for (int u = 0; u < kCand; ++u) many |= cnts[u] > 1;
+        if (__syncthreads_or(many)) {
+            at = pos;
+#pragma unroll
+            for (int u = 0; u < kCand; ++u) {
+                run_pos[threadIdx.x * kCand + u] = (uint32_t)(at < W ? at : W);
+                run_x[threadIdx.x * kCand + u] = xs[u];
+                at += cnts[u];
+            }
+            __syncthreads();
+            const uint64_t lim = total < W - filled ? total : W - filled;
+            for (uint64_t jj = threadIdx.x; jj < lim; jj += kFillThreads) {
+                const uint32_t j = (uint32_t)jj;
+                uint32_t lo = 0, hi = (uint32_t)kBatch;  // the last candidate starting at or before j
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (run_pos[mid] <= j) lo = mid;
+                    else hi = mid;
+                }
+                const uint64_t e = j - run_pos[lo];
+                if (e == 0) continue;  // a candidate's first row: emitted above
+                const uint64_t lr = p.dir == DSY_DESC ? run_x[lo] - e : run_x[lo] + e;
                 const uint64_t row = L.st.live_row ? L.st.live_row[lr] : lr;
                 const RowRec rw = rec[row];
-                out[dst] = row;
-                out_off[dst] = rw.off;
-                out_len[dst] = rw.len;
+                out[filled + jj] = row;
+                out_off[filled + jj] = rw.off;
+                out_len[filled + jj] = rw.len;
             }
-            at += cnts[u];
+            __syncthreads();  // run_pos / run_x are rewritten by the next round
         }
         const uint64_t batch = (p.ncand - c) < kBatch ? (p.ncand - c) : kBatch;
         if (filled + total <= W) {
@@ -575,6 +623,13 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
         for (uint64_t t = threadIdx.x; t < filled; t += kFillThreads) atomicAdd(&hist[bin_of(out_len[t])], 1u);
     }
     __syncthreads();
+    const uint32_t fam = family_id(q.hash_kind, q.chunk_bytes, q.prefix_len);
+    if ((L.pool_mask >> fam) & 1u) {  // a pooled family: the window's counts go into the family's histogram too
+        uint32_t* ph = L.pool_counts->hist[fam];
+        for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads)
+            if (hist[i]) atomicAdd(&ph[i], hist[i]);
+        __syncthreads();
+    }
     if (threadIdx.x < 64) {  // exclusive scan of the kSortBins counters by one wave
         const uint32_t per = kSortBins / 64, lane = threadIdx.x;
         uint32_t sum = 0;
@@ -683,8 +738,13 @@ __device__ __forceinline__ void fill_bulk_part(const RespondLaunch& L, uint32_t 
     }
     __syncthreads();
     uint32_t* gh = L.bulk_hist + (uint64_t)a_slot * kSortBins;
+    const uint32_t fam = family_id(q.hash_kind, q.chunk_bytes, q.prefix_len);
+    uint32_t* ph = ((L.pool_mask >> fam) & 1u) ? L.pool_counts->hist[fam] : nullptr;
     for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads)
-        if (hist[i]) atomicAdd(&gh[i], hist[i]);
+        if (hist[i]) {
+            atomicAdd(&gh[i], hist[i]);
+            if (ph) atomicAdd(&ph[i], hist[i]);
+        }
     if (part == 0 && threadIdx.x == 0) {
         S->n_window = W;
         S->cand_next = c + W;
@@ -759,6 +819,75 @@ __global__ void __launch_bounds__(kFillThreads) k_fill_sort(RespondLaunch L) {
             tk.slot = (uint32_t)(base + t);
             task[atomicAdd(&hist[sort_bin(q, len[u])], 1u)] = tk;
         }
+    }
+}
+
+// ------------------------------------------------------------------------------------ k_pool_scatter
+// A pooled family's window pairs -- its listed claims' task records, each claim's sorted by block count on its own --
+// into one block-count order over all of them, L.pool[0 .. total), longest first.  With ~300 pairs per claim
+// (the SHA-1 test filters of node.py:617 hold 284 keys) a claim's 64-pair chunks each span several block counts, and
+// a claim's last chunk is partly empty; pooled, every hashing wave but the last runs 64 lanes of one block count.
+// Workgroup (x, y) takes parts y, y + gridDim.y, ... (kPoolPart pairs each) of claim list[x]'s window: the family's
+// histogram (k_fill) scanned in LDS gives every bin's start, one atomic per (workgroup, part, bin) its range in the
+// bin.  Workgroup (0, 0) also publishes the total and resets the wave-task queue.
+static constexpr uint64_t kPoolPart = 1024;
+
+__global__ void __launch_bounds__(256) k_pool_scatter(RespondLaunch L, const uint32_t* __restrict__ list, uint32_t fam) {
+    __shared__ uint32_t start[kSortBins];
+    __shared__ uint32_t lh[kSortBins];
+    const uint32_t a_slot = list[blockIdx.x];
+    const uint32_t r = L.act[a_slot];
+    const uint64_t W = L.window;
+    const uint64_t n = L.state[r].n_window;
+    PoolCounts* pc = L.pool_counts;
+    const bool first = blockIdx.x == 0 && blockIdx.y == 0;
+    const uint64_t base0 = (uint64_t)blockIdx.y * kPoolPart;
+    if (base0 >= n && !first) return;
+    for (uint32_t i = threadIdx.x; i < kSortBins; i += 256) {
+        start[i] = pc->hist[fam][i];
+        lh[i] = 0;
+    }
+    __syncthreads();
+    bins_exclusive_scan(start, first ? &pc->total[fam] : nullptr);
+    if (first && threadIdx.x == 0) pc->next[fam] = 0;
+    __syncthreads();
+    const DevRequest& q = L.reqs[r];
+    const PairTask* task = L.task + (uint64_t)a_slot * W;
+    for (uint64_t base = base0; base < n; base += (uint64_t)gridDim.y * kPoolPart) {
+        const uint64_t cnt = n - base < kPoolPart ? n - base : kPoolPart;
+        constexpr int kU = (int)(kPoolPart / 256);
+        PairTask tk[kU];
+        uint32_t bin[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const uint64_t t = threadIdx.x + 256ull * u;
+            if (t < cnt) {
+                tk[u] = task[base + t];
+                bin[u] = sort_bin(q, tk[u].len);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+            if (threadIdx.x + 256ull * u < cnt) atomicAdd(&lh[bin[u]], 1u);
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < kSortBins; i += 256)
+            if (lh[i]) lh[i] = start[i] + atomicAdd(&pc->cur[fam][i], lh[i]);
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            if (threadIdx.x + 256ull * u < cnt) {
+                PoolTask p;
+                p.line = (uint32_t)(tk[u].off >> 7);  // off = line * 128 + kLineBias
+                p.len = tk[u].len;
+                p.a_slot = a_slot;
+                p.slot = tk[u].slot;
+                const uint32_t pos = atomicAdd(&lh[bin[u]], 1u);
+                if (pos < (uint64_t)L.n_act * W) L.pool[pos] = p;  // (always: the counts are this window's pairs)
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < kSortBins; i += 256) lh[i] = 0;
+        __syncthreads();
     }
 }
 
@@ -846,39 +975,93 @@ __global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_waves_per_
 // per task and measured 234 -> 338 us per headline launch.
 // Measured and dropped: half-line staging (two 4 KiB buffers, one block's words live, 95 VGPRs, 5 waves per SIMD)
 // ran the headline launch in the same 234 us (compute ceiling 175 us, gather ceiling 191 us vs 176 for full lines).
-template <class H, int CHUNK, bool DMA, int DIAG = 0>
+// POOL: the wave-tasks are 64 consecutive pairs of the family's pooled order (k_pool_scatter): the claim -- filter,
+// prefix, m, k -- is per lane.  pool_queue: waves take wave-tasks from a queue (longest first) instead of the grid
+// stride.
+template <class H, int CHUNK, bool DMA, int DIAG = 0, bool POOL = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_pair_test(RespondLaunch L, const uint32_t* __restrict__ req_list,
-                                                   uint32_t n_list) {
+                                                   uint32_t n_list, uint32_t fam) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dma_lds[];
     const uint64_t W = L.window;
-    // chunks per claim: the window's longest claim (k_fill), not W / 64 -- a claim of ~1000 pairs in a 4096-pair
-    // window would otherwise leave 3/4 of the wave-tasks empty, each costing a dependent load chain to skip
-    const uint64_t waves_per_req = min((uint64_t)L.flags[kFlagChunks], W / 64);
-    const uint64_t total_waves = (uint64_t)n_list * waves_per_req;
+    uint64_t total_waves;
+    uint32_t n_pool = 0;
+    if constexpr (POOL) {
+        n_pool = (uint32_t)min((uint64_t)L.pool_counts->total[fam], (uint64_t)L.n_act * W);
+        total_waves = (n_pool + 63) / 64;
+        if (blockIdx.x == 0) {  // the family's histogram and cursors start the next window at zero (k_fill adds)
+            for (uint32_t i = threadIdx.x; i < kSortBins; i += blockDim.x)
+                L.pool_counts->hist[fam][i] = L.pool_counts->cur[fam][i] = 0;
+        }
+    } else {
+        // chunks per claim: the window's longest claim (k_fill), not W / 64 -- a claim of ~1000 pairs in a 4096-pair
+        // window would otherwise leave 3/4 of the wave-tasks empty, each costing a dependent load chain to skip
+        const uint64_t waves_per_req = min((uint64_t)L.flags[kFlagChunks], W / 64);
+        total_waves = (uint64_t)n_list * waves_per_req;
+    }
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t wave0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const bool queue = POOL && L.pool_queue;
+    auto next_task = [&]() -> uint64_t {
+        uint32_t v = 0;
+        if (lane == 0) v = atomicAdd(&L.pool_counts->next[fam], 1u);
+        return (uint64_t)(uint32_t)__shfl((int)v, 0, 64);
+    };
     uint8_t* my_lds = dma_lds + (threadIdx.x >> 6) * DmaGeometry<2, 1>::kWaveBytes;
     unsigned long long acc_blocks = 0, acc_bytes = 0, acc_slots = 0;  // this lane's work, reduced once per block
-    // chunk-major task order: wave-task v hashes 64-pair chunk (v / n_list) of claim (v % n_list), so the
-    // non-empty chunks of every claim come first and spread evenly over the grid
-    for (uint64_t wv = wave0; wv < total_waves; wv += wstride) {
-        const uint32_t a_slot = req_list[wv % n_list];
-        const uint32_t r = L.act[a_slot];
-        const uint64_t i0 = (wv / n_list) * 64;
-        const uint64_t n = L.state[r].n_window;
-        if (i0 >= n) continue;  // wave-uniform: past this claim's window
-        const uint64_t i = i0 + lane;
-        const bool active = i < n;
-        const DevRequest& q = L.reqs[r];
-        uint32_t t = 0;
-        KeyView kv{L.st.lines + DSY_BLOB_GUARD, 0u, q.prefix, q.prefix_len};  // idle lanes: an empty key past the guard
-        if (active) {
-            const PairTask tk = L.task[(uint64_t)a_slot * W + i];
-            t = tk.slot;
-            kv.key = L.st.lines + tk.off;
-            kv.len = tk.len;
+    // deal: the resident grid (4 workgroups per CU) visits whole rounds of its waves, the wave-tasks permuted within
+    // a round.  Workgroups i, i + G/4, i + G/2, i + 3G/4 share a CU (observed: tools/trace_summary.py over
+    // DSY_PAIR_TRACE), and each SIMD holds one wave of each, in no fixed order.  A workgroup's four waves take four
+    // consecutive wave-tasks (about equal), and the workgroups of a CU take positions c, G/2 - 1 - c, G/2 + c,
+    // G - 1 - c of the G workgroup positions (snaking over the quarters), so every SIMD's four waves sum to about the
+    // mean when the wave-tasks come longest first.  Later rounds snake back.
+    const bool deal = L.pool_deal && gridDim.x % 4 == 0;
+    const uint64_t wend = deal ? (total_waves + wstride - 1) / wstride * wstride : total_waves;
+    for (uint64_t wv = queue ? next_task() : wave0; wv < wend; wv = queue ? next_task() : wv + wstride) {
+        uint32_t a_slot, r, t = 0;
+        bool active;
+        const uint8_t* key = L.st.lines + DSY_BLOB_GUARD;  // idle lanes: an empty key past the guard
+        uint32_t len = 0;
+        uint64_t v = wv;
+        if (deal) {
+            const uint64_t R = wstride, G = gridDim.x, k = wv / R, x = wv % R;
+            const uint64_t i = x / 4, q = i / (G / 4), c = i % (G / 4);
+            const uint64_t pos = q * (G / 4) + ((q & 1) ? G / 4 - 1 - c : c);
+            const uint64_t rank = 4 * pos + x % 4;
+            v = k * R + ((k & 1) ? R - 1 - rank : rank);
+            if (v >= total_waves) continue;  // wave-uniform
         }
+        if constexpr (POOL) {
+            const uint64_t i = v * 64 + lane;
+            active = i < n_pool;
+            const PoolTask pt = L.pool[active ? i : n_pool - 1];
+            a_slot = pt.a_slot;
+            r = L.act[a_slot];
+            if (active) {
+                t = pt.slot;
+                key = L.st.lines + ((uint64_t)pt.line << 7) + kLineBias;
+                len = pt.len;
+            }
+        } else {
+            // chunk-major task order: wave-task v hashes 64-pair chunk (v / n_list) of claim (v % n_list), so the
+            // non-empty chunks of every claim come first (the longest packets of each) and spread over the grid
+            a_slot = req_list[v % n_list];
+            r = L.act[a_slot];
+            const uint64_t i0 = (v / n_list) * 64;
+            const uint64_t n = L.state[r].n_window;
+            if (i0 >= n) continue;  // wave-uniform: past this claim's window
+            const uint64_t i = i0 + lane;
+            active = i < n;
+            if (active) {
+                const PairTask tk = L.task[(uint64_t)a_slot * W + i];
+                t = tk.slot;
+                key = L.st.lines + tk.off;
+                len = tk.len;
+            }
+        }
+        const DevRequest& q = L.reqs[r];
+        KeyView kv{key, len, q.prefix, q.prefix_len};
+        const uint64_t trace_t0 = L.trace ? __builtin_amdgcn_s_memrealtime() : 0;
         H st;
         if constexpr (DMA) {
             // prefixes of 0 or > 4 bytes go to DMA = false
@@ -902,6 +1085,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, d, 64));
         if (lane == 0) acc_slots += 64ull * nbmax;
+        if (L.trace && lane == 0) {  // diagnostics: the wave-task's place and time
+            const uint32_t at = atomicAdd(L.trace_n, 1u);
+            if (at < L.trace_cap) {
+                WaveTrace w;
+                w.hw_id = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+                w.xcc_id = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+                w.t0 = trace_t0;
+                w.t1 = __builtin_amdgcn_s_memrealtime();
+                w.blocks = nbmax;
+                w.task = (uint32_t)wv;
+                L.trace[at] = w;
+            }
+        }
     }
     // one set of atomics per workgroup (a contended atomic per wave-task would stall the next vmcnt wait of
     // every wave behind it)
@@ -927,8 +1123,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
     }
 }
 
+// pooled (fam: the family id): k_pool_scatter orders the listed claims' pairs into L.pool first; MD5, SHA-1 and
+// SHA-256 only (the larger SHA-2 families take the per-claim order)
 template <class H, int CHUNK>
-static hipError_t pair_test_family(const RespondLaunch& L, bool long_prefix, const uint32_t* list, uint32_t n_list) {
+static hipError_t pair_test_family(const RespondLaunch& L, bool long_prefix, const uint32_t* list, uint32_t n_list,
+                                   bool pooled = false, uint32_t fam = 0) {
     const uint64_t waves = (uint64_t)n_list * (L.window / 64);
     uint64_t blocks = (waves + 3) / 4;
     // 8 workgroups per CU (respond_core: the ctx's max_grid, DSY_PAIR_GRID overrides): the grid-stride then deals
@@ -937,47 +1136,73 @@ static hipError_t pair_test_family(const RespondLaunch& L, bool long_prefix, con
     const uint64_t cap = L.grid_cap ? L.grid_cap : 2048;
     if (blocks > cap) blocks = cap;
     if (blocks == 0) return hipSuccess;
+    if (L.pool_deal) blocks = cap / 2 / 4 * 4;  // the resident grid: 4 workgroups per CU (128 VGPRs)
+    constexpr bool poolable = H::kind == DSY_MD5 || H::kind == DSY_SHA1 || H::kind == DSY_SHA256;
+    if constexpr (poolable) {
+        if (pooled) {
+            // one workgroup per claim for windows of <= 16 parts (the common 4096-pair window: 1024 claims, 1024
+            // workgroups), more for the big windows of a few long claims
+            const uint32_t parts = (uint32_t)std::max<uint64_t>(1, L.window / (16 * kPoolPart));
+            hipLaunchKernelGGL(k_pool_scatter, dim3(n_list, parts), dim3(256), 0, L.stream, L, list, fam);
+        }
+    } else {
+        pooled = false;
+    }
     // MD5 and SHA-1 stage their 64-byte blocks through LDS with DMA (8 keys x 128 contiguous bytes per wave
     // instruction, single LDS buffer, next stage in flight while the current one is compressed from registers:
     // tools/hashbench, profiles/hashbench_r1_dmareg.txt); SHA-2 is compute-bound enough that direct loads match it
     constexpr bool dma = H::kind == DSY_MD5 || H::kind == DSY_SHA1;
     if constexpr (dma) {
-        if (!long_prefix) {
+        if (!long_prefix && !((L.direct_kinds >> H::kind) & 1u)) {
             const size_t lds = 4 * DmaGeometry<2, 1>::kWaveBytes;
-            auto kern = k_pair_test<H, CHUNK, true>;
-            if constexpr (CHUNK == 2) {
+            auto kern = pooled ? k_pair_test<H, CHUNK, true, 0, true> : k_pair_test<H, CHUNK, true>;
+            if constexpr (CHUNK == 2) {  // (respond_core pools no family while a diagnostic build is asked for)
                 if (L.diag == 1) kern = k_pair_test<H, CHUNK, true, 1>;
                 if (L.diag == 2) kern = k_pair_test<H, CHUNK, true, 2>;
             }
-            launch_timed(kern, dim3((uint32_t)blocks), dim3(256), lds, L.stream, L.ev_start, L.ev_stop, L, list, n_list);
+            launch_timed(kern, dim3((uint32_t)blocks), dim3(256), lds, L.stream, L.ev_start, L.ev_stop, L, list, n_list,
+                         fam);
             return hipGetLastError();
         }
     }
-    launch_timed(k_pair_test<H, CHUNK, false>, dim3((uint32_t)blocks), dim3(256), 0, L.stream, L.ev_start, L.ev_stop, L,
-                 list, n_list);
+    auto kern = k_pair_test<H, CHUNK, false>;
+    if constexpr (poolable)
+        if (pooled) kern = k_pair_test<H, CHUNK, false, 0, true>;
+    launch_timed(kern, dim3((uint32_t)blocks), dim3(256), 0, L.stream, L.ev_start, L.ev_stop, L, list, n_list, fam);
     return hipGetLastError();
 }
 
 template <class H>
-static hipError_t pair_test_chunk(const RespondLaunch& L, uint32_t chunk, bool lp, const uint32_t* list, uint32_t n) {
+static hipError_t pair_test_chunk(const RespondLaunch& L, uint32_t chunk, bool lp, const uint32_t* list, uint32_t n,
+                                  bool pooled, uint32_t fam) {
     switch (chunk) {
-        case 2: return pair_test_family<H, 2>(L, lp, list, n);
-        case 4: return pair_test_family<H, 4>(L, lp, list, n);
-        default: return pair_test_family<H, 8>(L, lp, list, n);
+        case 2: return pair_test_family<H, 2>(L, lp, list, n, pooled, fam);
+        case 4: return pair_test_family<H, 4>(L, lp, list, n, pooled, fam);
+        default: return pair_test_family<H, 8>(L, lp, list, n, pooled, fam);
+    }
+}
+
+static hipError_t pair_test_kind(const RespondLaunch& L, int kind, uint32_t chunk, bool long_prefix, const uint32_t* list,
+                                 uint32_t n, bool pooled, uint32_t fam) {
+    switch (kind) {
+        case DSY_MD5: return pair_test_chunk<Md5>(L, chunk, long_prefix, list, n, pooled, fam);
+        case DSY_SHA1:
+            return chunk == 2 ? pair_test_family<Sha1, 2>(L, long_prefix, list, n, pooled, fam)
+                              : pair_test_family<Sha1, 4>(L, long_prefix, list, n, pooled, fam);
+        case DSY_SHA256: return pair_test_chunk<Sha256>(L, chunk, long_prefix, list, n, pooled, fam);
+        case DSY_SHA384: return pair_test_chunk<Sha384>(L, chunk, long_prefix, list, n, false, fam);
+        default: return pair_test_chunk<Sha512>(L, chunk, long_prefix, list, n, false, fam);
     }
 }
 
 hipError_t launch_pair_test_list(const RespondLaunch& L, int kind, uint32_t chunk, bool long_prefix, const uint32_t* list,
                                  uint32_t n) {
-    switch (kind) {
-        case DSY_MD5: return pair_test_chunk<Md5>(L, chunk, long_prefix, list, n);
-        case DSY_SHA1:
-            return chunk == 2 ? pair_test_family<Sha1, 2>(L, long_prefix, list, n)
-                              : pair_test_family<Sha1, 4>(L, long_prefix, list, n);
-        case DSY_SHA256: return pair_test_chunk<Sha256>(L, chunk, long_prefix, list, n);
-        case DSY_SHA384: return pair_test_chunk<Sha384>(L, chunk, long_prefix, list, n);
-        default: return pair_test_chunk<Sha512>(L, chunk, long_prefix, list, n);
-    }
+    return pair_test_kind(L, kind, chunk, long_prefix, list, n, false, 0);
+}
+
+hipError_t launch_pair_test_pooled(const RespondLaunch& L, int kind, uint32_t chunk, bool long_prefix, uint32_t fam,
+                                   const uint32_t* list, uint32_t n) {
+    return pair_test_kind(L, kind, chunk, long_prefix, list, n, true, fam);
 }
 
 // ----------------------------------------------------------------------------------------- k_compact
