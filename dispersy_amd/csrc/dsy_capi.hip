@@ -124,8 +124,10 @@ struct dsy_ctx {
     uint32_t pair_grid = 0;  // DSY_PAIR_GRID at creation: k_pair_test grid cap (0: max_grid, 8 workgroups per CU)
     int or_mode = 1;     // DSY_OR_MODE at creation: filter-build atomics (filter_set_all OR_MODE, dsy_message.h)
     // DSY_POOL at creation: bit k = hash kind k's responder pairs are pooled across claims (k_pool_scatter) -- MD5,
-    // SHA-1 and SHA-256 only; DSY_POOL_QUEUE: the pooled hashing takes its wave-tasks from a queue
-    uint32_t pool_kinds = (1u << DSY_SHA1) | (1u << DSY_SHA256);
+    // SHA-1 and SHA-256 only; DSY_POOL_QUEUE: the pooled hashing takes its wave-tasks from a queue.  Off by default:
+    // on the SHA-1 leg pooling takes k_pair_test 104 -> 95 us (lane use 0.82 -> 1.00) but k_pool_scatter costs 18 us
+    // (1024 workgroups' atomics on the same ~20 bin cursors), 0.149 -> 0.157 ms per step; MD5 headline 0.28 -> 0.30
+    uint32_t pool_kinds = 0;
     int pool_queue = 0;
     int pool_deal = 0;   // DSY_POOL_DEAL: the pooled hashing's resident-grid deal (k_pair_test<POOL>)
     uint32_t direct_kinds = 0;  // DSY_PAIR_DIRECT: bit k = hash kind k's responder hashing uses direct loads
