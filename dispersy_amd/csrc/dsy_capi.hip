@@ -1798,8 +1798,9 @@ static int job_window(dsy_ctx* c, RespondSlot& sl) {
     timer_end(c, &t, st);
     // speculatively pack the output now (it is redone if another window follows): the GPU packs while the host wakes
     // up and reads the status
-    HIP_TRY(launch_pack(L, (uint64_t*)jb.d_packed, (uint64_t*)jb.d_packed_off, nullptr));
-    HIP_TRY(hipEventRecord(sl.ev_done, st));
+    static const bool ev_marker = getenv("DSY_EVENT_MARKER") != nullptr;  // A/B: the event as a separate record
+    HIP_TRY(launch_pack(L, (uint64_t*)jb.d_packed, (uint64_t*)jb.d_packed_off, nullptr, ev_marker ? nullptr : sl.ev_done));
+    if (ev_marker) HIP_TRY(hipEventRecord(sl.ev_done, st));
     if (g_host_profile && !jb.hp[2]) jb.hp[2] = host_us();  // first window enqueued
     return DSY_OK;
 }
@@ -1811,7 +1812,7 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
     sl.job = RespondJob{};
     RespondJob& jb = sl.job;
     const hipStream_t st = c->stream;
-    if (!sl.ev_done) HIP_TRY(hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming));
+    if (!sl.ev_done) HIP_TRY(hipEventCreate(&sl.ev_done));  // (recorded by a dispatch: hipExtLaunchKernelGGL)
     if (g_host_profile) jb.hp[0] = host_us();
     // ---- validate claims (payload.py:89-101, conversion.py:772-789) and their filters; group them by hash family
     // (kind x chunk width: one pair-test launch per family)

@@ -254,7 +254,9 @@ hipError_t launch_pair_test_list(const RespondLaunch& L, int kind, uint32_t chun
 hipError_t launch_pair_test_pooled(const RespondLaunch& L, int kind, uint32_t chunk, bool long_prefix, uint32_t fam,
                                    const uint32_t* d_list, uint32_t n);
 hipError_t launch_compact(const RespondLaunch& L);
-hipError_t launch_pack(const RespondLaunch& L, uint64_t* packed, uint64_t* packed_offsets, uint64_t* d_scan_tmp);
+// done (optional): an event the last pack kernel's dispatch records when it completes
+hipError_t launch_pack(const RespondLaunch& L, uint64_t* packed, uint64_t* packed_offsets, uint64_t* d_scan_tmp,
+                       hipEvent_t done = nullptr);
 // copy each row's packet from (blob, offsets) to its line-aligned place rec[i].off in lines
 hipError_t launch_store_lines(const uint8_t* blob, const uint64_t* offsets, const RowRec* rec, uint64_t n,
                               uint8_t* lines, hipStream_t stream);

@@ -1497,13 +1497,25 @@ hipError_t launch_compact(const RespondLaunch& L) {
     return hipGetLastError();
 }
 
-hipError_t launch_pack(const RespondLaunch& L, uint64_t* packed, uint64_t* packed_offsets, uint64_t*) {
+hipError_t launch_pack(const RespondLaunch& L, uint64_t* packed, uint64_t* packed_offsets, uint64_t*, hipEvent_t done) {
+    // done: recorded by the last kernel's own dispatch (an event record between two dispatches leaves a ~6 us gap on
+    // the queue, in front of the next batch's selection)
     if (L.R && L.R <= kPackFusedMax) {
-        hipLaunchKernelGGL(k_pack_fused, dim3(L.R), dim3(256), 0, L.stream, L, packed_offsets, packed);
+        if (done) hipExtLaunchKernelGGL(k_pack_fused, dim3(L.R), dim3(256), 0, L.stream, nullptr, done, 0, L,
+                                        packed_offsets, packed);
+        else hipLaunchKernelGGL(k_pack_fused, dim3(L.R), dim3(256), 0, L.stream, L, packed_offsets, packed);
+        return hipGetLastError();
+    }
+    if (!L.R) {
+        if (done) hipExtLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, L.stream, nullptr, done, 0, L,
+                                        packed_offsets);
+        else hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, L.stream, L, packed_offsets);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, L.stream, L, packed_offsets);
-    if (L.R) hipLaunchKernelGGL(k_copy_out, dim3(L.R), dim3(256), 0, L.stream, L, packed_offsets, packed);
+    if (done) hipExtLaunchKernelGGL(k_copy_out, dim3(L.R), dim3(256), 0, L.stream, nullptr, done, 0, L, packed_offsets,
+                                    packed);
+    else hipLaunchKernelGGL(k_copy_out, dim3(L.R), dim3(256), 0, L.stream, L, packed_offsets, packed);
     return hipGetLastError();
 }
 
