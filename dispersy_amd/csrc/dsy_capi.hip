@@ -89,6 +89,7 @@ struct RespondJob {
     void* d_packed_off = nullptr;
     size_t in_b = 0, cnt_b = 0;
     uint64_t per_claim = 0;
+    uint64_t cap_pairs = 0;    // pairs the bound per-pair buffers hold (job_pair_buffers)
     bool fused_first = false, first = true, ran = false, first_fill = true;
     double hp[4] = {0, 0, 0, 0};
     double hp_wait = 0;
@@ -1672,6 +1673,40 @@ int dsy_claim_largest(dsy_ctx* c, const dsy_bloom_params* p, const dsy_store* s,
 static const uint64_t kWindow = 4096;
 static const uint64_t kMaxWindow = 1 << 18;
 static const uint64_t kMinSlots = 4096;
+// DSY_BIG_POOL (experiments; 0 by default): windows after the first share a pool of that many pairs, allocated the
+// first time a call needs it, and W may reach 2^20.  Measured on config 5 (2^27 pairs): 9 -> 3 windows per step but
+// the same 11.9 ms of hashing (3 x 3.97 ms instead of 9 x 1.32: a window is not bounded by its longest packet's serial
+// digest) and a slower step, 16.8 -> 19.5 ms (one k_compact wave walks a 2^20-pair window's miss words).
+static uint64_t big_pool_pairs() {
+    static const uint64_t v = getenv("DSY_BIG_POOL") ? strtoull(getenv("DSY_BIG_POOL"), nullptr, 0) : 0;
+    return v;
+}
+
+// (Re)bind a job's per-pair buffers for `pairs` pairs (window slots x W); grows the slot's workspace when needed.
+static int job_pair_buffers(RespondSlot& sl, uint64_t pairs) {
+    RespondJob& jb = sl.job;
+    RespondLaunch& L = jb.L;
+    Workspace& w = sl.w;
+    void *d_pairs, *d_off, *d_len, *d_miss, *d_task;
+    int rc;
+    if ((rc = ws_get(w, "pairs", pairs * 8, &d_pairs))) return rc;
+    if ((rc = ws_get(w, "pair_off", pairs * 8, &d_off))) return rc;
+    if ((rc = ws_get(w, "pair_len", pairs * 4, &d_len))) return rc;
+    if ((rc = ws_get(w, "miss_mask", pairs / 8 + 64, &d_miss))) return rc;
+    if ((rc = ws_get(w, "task", pairs * sizeof(PairTask), &d_task))) return rc;
+    L.pair_row = (uint64_t*)d_pairs;
+    L.pair_off = (uint64_t*)d_off;
+    L.pair_len = (uint32_t*)d_len;
+    L.miss_mask = (uint64_t*)d_miss;
+    L.task = (PairTask*)d_task;
+    if (L.pool_mask) {
+        void* d_pool;
+        if ((rc = ws_get(w, "pool_task", pairs * sizeof(PoolTask), &d_pool))) return rc;
+        L.pool = (PoolTask*)d_pool;
+    }
+    jb.cap_pairs = pairs;
+    return DSY_OK;
+}
 
 // DSY_HOST_PROFILE: one stderr line per call with the host-side phases of respond_core (microseconds)
 static double host_us() {
@@ -1694,10 +1729,16 @@ static int job_window(dsy_ctx* c, RespondSlot& sl) {
         runs.push_back({n_act, fa.size()});
         n_act += fa.size();
     }
-    uint64_t W = jb.pool / n_act / 64 * 64;
-    W = std::min<uint64_t>(std::max<uint64_t>(W, kWindow), kMaxWindow);
+    const uint64_t pool_now = jb.first ? jb.pool : std::max<uint64_t>(jb.pool, std::min<uint64_t>(big_pool_pairs(),
+                                                                                                 0xffffffffull));
+    uint64_t W = pool_now / n_act / 64 * 64;
+    W = std::min<uint64_t>(std::max<uint64_t>(W, kWindow), big_pool_pairs() ? kMaxWindow * 4 : kMaxWindow);
     if (c->window_cap) W = std::min<uint64_t>(W, c->window_cap);
     L.window = W;
+    int rc;
+    if (W * n_act > jb.cap_pairs) {  // a later window's bigger pool (this slot's earlier windows have completed)
+        if ((rc = job_pair_buffers(sl, W * n_act))) return rc;
+    }
     L.n_act = (uint32_t)n_act;
     if (!jb.first) {  // the first window's list went up with the claims
         uint32_t* h_act = (uint32_t*)jb.h_in;  // the staged claims are on the device already: reuse the space
@@ -1708,7 +1749,6 @@ static int job_window(dsy_ctx* c, RespondSlot& sl) {
     }
     jb.first = false;
     jb.ran = true;
-    int rc;
     static const bool fill_profile = getenv("DSY_FILL_PROFILE") != nullptr;
     void* d_fc = nullptr;
     if (fill_profile) {
@@ -1870,7 +1910,7 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
     jb.in_b = in_b;
     jb.cnt_b = cnt_b;
     int rc;
-    void *d_in, *d_io, *d_plans, *d_state, *d_pairs, *d_off, *d_len, *d_miss, *d_task, *d_emit, *d_ticket;
+    void *d_in, *d_io, *d_plans, *d_state, *d_emit, *d_ticket;
     Workspace& w = sl.w;
     if ((rc = ws_get(w, "resp_in", in_b, &d_in))) return rc;
     if ((rc = ws_get(w, "emitted_n", std::max<size_t>(R, 1) * 8, &d_emit))) return rc;
@@ -1882,11 +1922,6 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
     if (io_fresh) HIP_TRY(hipMemsetAsync(d_io, 0, io_b, st));  // flags start (and stay, k_compact) at zero
     if ((rc = ws_get(w, "plans", std::max<size_t>((size_t)R * J, 1) * sizeof(Plan), &d_plans))) return rc;
     if ((rc = ws_get(w, "state", std::max<size_t>(R, 1) * sizeof(ReqState), &d_state))) return rc;
-    if ((rc = ws_get(w, "pairs", pool * 8, &d_pairs))) return rc;
-    if ((rc = ws_get(w, "pair_off", pool * 8, &d_off))) return rc;
-    if ((rc = ws_get(w, "pair_len", pool * 4, &d_len))) return rc;
-    if ((rc = ws_get(w, "miss_mask", pool / 8 + 64, &d_miss))) return rc;
-    if ((rc = ws_get(w, "task", pool * sizeof(PairTask), &d_task))) return rc;
     void* d_bulk;  // split windows' sort state: [R][kSortBins] histogram + cursors, zero between windows
     bool bulk_fresh = false;
     const size_t bulk_b = (size_t)std::max<uint32_t>(R, 1) * 2 * 1024 * 4;
@@ -1897,10 +1932,9 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
     if (!c->pair_diag && pool <= 0xffffffffull)
         for (int f = 0; f < kFamilies; ++f)
             if (!fam_members[f].empty() && ((c->pool_kinds >> (f / 6)) & 1u)) pool_mask |= 1u << f;
-    void *d_pool = nullptr, *d_pool_counts = nullptr;
+    void* d_pool_counts = nullptr;
     if (pool_mask) {
         bool pc_fresh = false;
-        if ((rc = ws_get(w, "pool_task", pool * sizeof(PoolTask), &d_pool))) return rc;
         if ((rc = ws_get(w, "pool_counts", sizeof(PoolCounts), &d_pool_counts, &pc_fresh))) return rc;
         if (pc_fresh) HIP_TRY(hipMemsetAsync(d_pool_counts, 0, sizeof(PoolCounts), st));
     }
@@ -1996,11 +2030,6 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
     L.upper = (uint64_t*)(io + head_b);
     L.emitted_n = (uint64_t*)d_emit;
     L.ticket = (uint32_t*)d_ticket;
-    L.pair_row = (uint64_t*)d_pairs;
-    L.pair_off = (uint64_t*)d_off;
-    L.pair_len = (uint32_t*)d_len;
-    L.miss_mask = (uint64_t*)d_miss;
-    L.task = (PairTask*)d_task;
     L.bulk_hist = (uint32_t*)d_bulk;
     L.bulk_cur = (uint32_t*)d_bulk + (size_t)std::max<uint32_t>(R, 1) * 1024;
     L.flags = (uint32_t*)(io + cnt_b);
@@ -2013,7 +2042,7 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
     L.pool_queue = c->pool_queue;
     L.pool_deal = c->pool_deal;
     L.pool_counts = (PoolCounts*)d_pool_counts;
-    L.pool = (PoolTask*)d_pool;
+    if ((rc = job_pair_buffers(sl, pool))) return rc;
 
     // ---- per-claim output capacity: every emitted packet but the last costs >= min_len bytes of budget, so a
     // claim sends at most byte_limit / min_len + 2 packets.  When that bound is small the capacities and output
