@@ -461,33 +461,48 @@ class SyncCommunity(object):
         double_signed_sync table) is outside this path.  Returns the new store rows."""
         if not messages:
             return np.zeros(0, dtype=np.int64)
-        # what this batch needs is checked before anything is stored, so a refused batch changes neither copy
+        # one pass over the messages; what a meta needs (history, sequence numbers, its checks) is worked out once
+        # per meta object, and everything is checked before anything is stored, so a refused batch changes neither
+        # copy
+        has_member = self._store.member is not None
+        per_meta = {}
+        metas, gts, seqs, packets = [], [], [], []
+        members = [] if has_member else None
         for m in messages:
             meta = getattr(m, "meta", None)
-            dist = getattr(meta, "distribution", None)
-            history = isinstance(dist, LastSyncDistribution)
-            if history and getattr(meta, "double_signed", False) and not dist.custom_callback:
-                # the reference's history of a double-signed meta is per member pair, through double_signed_sync
-                # (dispersy.py:1567-1578, :1593-1594); pruning it per single member would delete the wrong rows
-                raise NotImplementedError("LastSyncDistribution history of a double-member-signed meta (%s): the "
-                                          "double_signed_sync table is outside this path" % getattr(meta, "name", "?"))
-            if self._store.member is None and (history or (isinstance(dist, FullSyncDistribution) and
-                                                           dist.enable_sequence_number)):
-                raise ValueError("store_messages: meta %s keeps per-member history; the store needs its member column"
-                                 % getattr(meta, "name", "?"))
-        metas = [_meta_id(m) for m in messages]
-        gts = [m.distribution.global_time for m in messages]
-        members = [_member_id(m) for m in messages] if self._store.member is not None else None
-        seqs = []
-        for m in messages:
-            d = getattr(getattr(m, "meta", None), "distribution", None)
-            seqs.append(m.distribution.sequence_number if isinstance(d, FullSyncDistribution) and
-                        d.enable_sequence_number else 0)
-        rows = self._store.append([m.packet for m in messages], gts, metas, member=members, sequence=seqs)
-        self._last_sync_history(messages)
+            info = per_meta.get(id(meta))
+            if info is None:
+                info = per_meta[id(meta)] = self._meta_store_info(meta)
+            dist = m.distribution
+            metas.append(m.database_id if hasattr(m, "database_id") else meta.database_id)
+            gts.append(dist.global_time)
+            seqs.append(dist.sequence_number if info[0] else 0)
+            packets.append(m.packet)
+            if has_member:
+                members.append(_member_id(m))
+        rows = self._store.append(packets, gts, metas, member=members, sequence=seqs)
+        if any(h for _, h in per_meta.values()):
+            self._last_sync_history(messages)
         self.update_global_time(max(gts))
         self.dispersy_store(messages)
         return rows
+
+    def _meta_store_info(self, meta):
+        """(sequence, history): whether messages of `meta` store a sequence number (a sequence-numbered
+        FullSyncDistribution, dispersy.py:1529-1531) and keep a LastSyncDistribution history; raises for what this path does not store: the LastSyncDistribution history of a
+        double-member-signed meta (the reference keeps it per member pair in double_signed_sync, dispersy.py:1567-1578,
+        :1593-1594 -- pruning it per single member would delete the wrong rows), and per-member history or sequence
+        numbers in a store without its member column."""
+        dist = getattr(meta, "distribution", None)
+        history = isinstance(dist, LastSyncDistribution)
+        seq = isinstance(dist, FullSyncDistribution) and bool(dist.enable_sequence_number)
+        if history and getattr(meta, "double_signed", False) and not dist.custom_callback:
+            raise NotImplementedError("LastSyncDistribution history of a double-member-signed meta (%s): the "
+                                      "double_signed_sync table is outside this path" % getattr(meta, "name", "?"))
+        if self._store.member is None and (history or seq):
+            raise ValueError("store_messages: meta %s keeps per-member history; the store needs its member column"
+                             % getattr(meta, "name", "?"))
+        return seq, history
 
     def _last_sync_history(self, messages):
         st = self._store

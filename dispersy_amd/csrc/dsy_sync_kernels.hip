@@ -103,14 +103,59 @@ __device__ __forceinline__ uint64_t plan_one(const RespondLaunch& L, const DevRe
     Plan p{};
     p.dir = mt.dir;
     p.a = p.b = mt.seg_a;
+    bool have_ends = false;  // p.g_lo / p.g_hi known from the searches' probes
     if (lo <= hi && mt.seg_a < mt.seg_b) {
-        p.a = lower_bound_interp(L.st.live_gt, mt.seg_a, mt.seg_b, lo);
-        p.b = hi >= kMaxGt ? mt.seg_b : lower_bound_interp(L.st.live_gt, p.a, mt.seg_b, hi + 1);
+        // Both ends of the span in two dependent rounds of loads when the segment's global times are dense or evenly
+        // spread: the segment's end values (shared by both searches), then both interpolated positions and their
+        // predecessors together -- whose values are also g_lo and g_hi.  Anything else falls back to
+        // lower_bound_interp's rounds and binary search.
+        const uint64_t* gt = L.st.live_gt;
+        const uint64_t a = mt.seg_a, b = mt.seg_b;
+        const uint64_t g0 = gt[a], g1 = gt[b - 1];
+        const bool open_hi = hi >= kMaxGt;
+        const uint64_t v0 = lo, v1 = open_hi ? 0 : hi + 1;
+        auto guess = [&](uint64_t v) -> uint64_t {  // a position in [a + 1, b - 1] for g0 < v <= g1 (b - a >= 2)
+            const double f = (double)(v - g0) / (double)(g1 - g0);
+            uint64_t q = a + 1 + (uint64_t)(f * (double)(b - 2 - a));
+            return q > b - 1 ? b - 1 : q;
+        };
+        // search 0: lower_bound(lo); search 1: lower_bound(hi + 1) (open_hi: the segment's end)
+        bool done0 = false, done1 = open_hi;
+        uint64_t r0 = 0, r1 = b, q0 = 0, q1 = 0;
+        if (v0 <= g0) { r0 = a; done0 = true; }
+        else if (v0 > g1) { r0 = b; done0 = true; }
+        else q0 = guess(v0);
+        if (!done1) {
+            if (v1 <= g0) { r1 = a; done1 = true; }
+            else if (v1 > g1) { r1 = b; done1 = true; }
+            else q1 = guess(v1);
+        }
+        uint64_t gp0 = 0, gq0 = 0, gp1 = 0, gq1 = 0;
+        if (!done0) { gp0 = gt[q0]; gq0 = gt[q0 - 1]; }
+        if (!done1) { gp1 = gt[q1]; gq1 = gt[q1 - 1]; }
+        if (!done0 && gq0 < v0 && v0 <= gp0) { r0 = q0; done0 = true; }
+        if (!done1 && gq1 < v1 && v1 <= gp1) { r1 = q1; done1 = true; }
+        if (!done0) r0 = lower_bound_interp(gt, a, b, v0);
+        if (!done1) r1 = lower_bound_interp(gt, r0, b, v1);
+        p.a = r0;
+        p.b = r1 < r0 ? r0 : r1;
+        if (p.b > p.a) {
+            // g_lo = gt[p.a]: the found position's value, or the segment's first; g_hi = gt[p.b - 1] likewise
+            const bool lo_known = p.a == a || (p.a == q0 && gq0 < v0 && v0 <= gp0);
+            const bool hi_known = p.b == b || (!open_hi && p.b == q1 && gq1 < v1 && v1 <= gp1);
+            if (lo_known && hi_known) {
+                p.g_lo = p.a == a ? g0 : gp0;
+                p.g_hi = p.b == b ? g1 : gq1;
+                have_ends = true;
+            }
+        }
     }
     const uint64_t span = p.b - p.a;
     if (span) {
-        p.g_lo = L.st.live_gt[p.a];
-        p.g_hi = L.st.live_gt[p.b - 1];
+        if (!have_ends) {
+            p.g_lo = L.st.live_gt[p.a];
+            p.g_hi = L.st.live_gt[p.b - 1];
+        }
         p.dense = p.g_hi - p.g_lo == span - 1;
     }
     const uint64_t mod = q.modulo;

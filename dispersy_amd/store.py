@@ -258,10 +258,10 @@ class SyncStore(object):
         rows = np.arange(n0, n0 + a, dtype=np.int64)
         if a == 0:
             return rows
-        lens = np.fromiter((len(p) for p in packets), dtype=np.uint64, count=a)
+        lens = np.fromiter(map(len, packets), dtype=np.uint64, count=a)
         new_off = np.zeros(a + 1, dtype=np.uint64)
         np.cumsum(lens, out=new_off[1:])
-        data = b"".join(bytes(p) for p in packets)
+        data = b"".join(packets)  # bytes-like items join as they are
         if self._handle is not None:
             lib = self.ctx.lib
             _native.check(lib.dsy_store_append(self.ctx.handle, self._handle, data, len(data), new_off.ctypes.data, a,
@@ -271,8 +271,13 @@ class SyncStore(object):
         b = self._buf
         b["offsets"] = _room(b["offsets"], n0 + 1, n0 + a + 1)
         b["offsets"][n0 + 1:n0 + a + 1] = b["offsets"][n0] + new_off[1:]
-        seqs = (np.zeros(a, dtype=np.int64) if sequence is None
-                else np.asarray([x or 0 for x in sequence], dtype=np.int64))
+        if sequence is None:
+            seqs = np.zeros(a, dtype=np.int64)
+        else:
+            try:
+                seqs = np.asarray(sequence, dtype=np.int64)  # ints (0: NULL)
+            except TypeError:  # None entries
+                seqs = np.asarray([x or 0 for x in sequence], dtype=np.int64)
         for name, vals in (("global_time", gts), ("meta", metas), ("undone", np.zeros(a, dtype=np.int64)),
                            ("rowid", ids), ("sequence", seqs), ("deleted", np.zeros(a, dtype=bool))):
             b[name] = _room(b[name], n0, n0 + a)
