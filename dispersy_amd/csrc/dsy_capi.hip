@@ -131,6 +131,7 @@ struct dsy_ctx {
     uint32_t pool_kinds = 0;
     int pool_queue = 0;
     int pool_deal = 0;   // DSY_POOL_DEAL: the pooled hashing's resident-grid deal (k_pair_test<POOL>)
+    int pair_prio = 0;   // DSY_PAIR_PRIO: k_pair_test raises the wave priority of long wave-tasks
     uint32_t direct_kinds = 0;  // DSY_PAIR_DIRECT: bit k = hash kind k's responder hashing uses direct loads
     uint32_t timing = 0;  // bit i: bracket class i with events
     std::vector<PendingTimer> pending;
@@ -498,6 +499,7 @@ int dsy_ctx_create(int device, dsy_ctx** out) {
     if (const char* v = getenv("DSY_POOL")) c->pool_kinds = (uint32_t)strtoul(v, nullptr, 0);
     if (const char* v = getenv("DSY_POOL_QUEUE")) c->pool_queue = atoi(v);
     if (const char* v = getenv("DSY_POOL_DEAL")) c->pool_deal = atoi(v);
+    if (const char* v = getenv("DSY_PAIR_PRIO")) c->pair_prio = atoi(v);
     if (const char* v = getenv("DSY_PAIR_DIRECT")) c->direct_kinds = (uint32_t)strtoul(v, nullptr, 0);
     c->pool_kinds &= (1u << DSY_MD5) | (1u << DSY_SHA1) | (1u << DSY_SHA256);
     hipHostMalloc(&c->pinned, 4096, hipHostMallocDefault);
@@ -2041,6 +2043,7 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
     L.pool_mask = pool_mask;
     L.pool_queue = c->pool_queue;
     L.pool_deal = c->pool_deal;
+    L.pair_prio = c->pair_prio;
     L.pool_counts = (PoolCounts*)d_pool_counts;
     if ((rc = job_pair_buffers(sl, pool))) return rc;
 

@@ -225,6 +225,7 @@ struct RespondLaunch {
     uint32_t pool_mask;       // bit f: family f's pairs are pooled across claims (k_fill counts, k_pool_scatter orders)
     int pool_queue;           // k_pair_test<POOL>: waves take wave-tasks from a queue instead of a grid stride
     int pool_deal;            // k_pair_test<POOL>: resident grid, wave-tasks dealt so each SIMD's waves sum to the mean
+    int pair_prio;            // k_pair_test: wave priority by the wave-task's length (s_setprio)
     PoolCounts* pool_counts;  // device, zero outside a window (k_pair_test<POOL> clears its family's)
     PoolTask* pool;           // device [pool]: the pooled order of the family being hashed
     hipStream_t stream;

@@ -1107,6 +1107,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         const DevRequest& q = L.reqs[r];
         KeyView kv{key, len, q.prefix, q.prefix_len};
         const uint64_t trace_t0 = L.trace ? __builtin_amdgcn_s_memrealtime() : 0;
+        const uint32_t nb = active ? n_blocks(kv.plen + kv.len, H::block_bytes, H::len_bytes) : 0u;
+        // lane-block slots this wave-task occupies: 64 x the longest lane (load-balance denominator)
+        uint32_t nbmax = nb;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, d, 64));
+        if (L.pair_prio) {
+            // the SIMD's arbiter issues for the longest wave-tasks first: a heavy-tailed window's few 64 KB packets
+            // (1024 blocks of serial digest) set its end.  pair_prio 1: tasks of >= 32 blocks (2 KB packets);
+            // 2: every task by length (packets of 100-1500 B too)
+            const uint32_t b = L.pair_prio == 2 ? nbmax * 16 : nbmax;
+            if (b >= 256) __builtin_amdgcn_s_setprio(3);
+            else if (b >= 64) __builtin_amdgcn_s_setprio(2);
+            else if (b >= 32) __builtin_amdgcn_s_setprio(1);
+        }
         H st;
         if constexpr (DMA) {
             // prefixes of 0 or > 4 bytes go to DMA = false
@@ -1114,10 +1128,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         } else {
             hash_key<H>(kv, st);
         }
+        if (L.pair_prio) __builtin_amdgcn_s_setprio(0);
         const uint32_t* filt = (const uint32_t*)(L.filters + q.filter_offset);
         const uint64_t m = q.m_bits;
         const uint32_t ok = filter_has_all<H, CHUNK>(filt, st, q.k, m);
-        const uint32_t nb = active ? n_blocks(kv.plen + kv.len, H::block_bytes, H::len_bytes) : 0u;
         if (active) {
             // misses are rare (the requester holds most of its range): one atomic bit per missing pair
             if (!ok && DIAG == 0)  // (the diagnostics' digests are garbage: their misses would be mostly atomics)
@@ -1125,10 +1139,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
             acc_blocks += nb;
             acc_bytes += kv.len;
         }
-        // lane-block slots this wave-task occupied: 64 x the longest lane (load-balance denominator)
-        uint32_t nbmax = nb;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, d, 64));
         if (lane == 0) acc_slots += 64ull * nbmax;
         if (L.trace && lane == 0) {  // diagnostics: the wave-task's place and time
             const uint32_t at = atomicAdd(L.trace_n, 1u);
