@@ -131,7 +131,7 @@ struct dsy_ctx {
     uint32_t pool_kinds = 0;
     int pool_queue = 0;
     int pool_deal = 0;   // DSY_POOL_DEAL: the pooled hashing's resident-grid deal (k_pair_test<POOL>)
-    int pair_prio = 0;   // DSY_PAIR_PRIO: k_pair_test raises the wave priority of long wave-tasks
+    int pair_prio = 1;   // DSY_PAIR_PRIO: k_pair_test raises the wave priority of long wave-tasks (0 off)
     uint32_t direct_kinds = 0;  // DSY_PAIR_DIRECT: bit k = hash kind k's responder hashing uses direct loads
     uint32_t timing = 0;  // bit i: bracket class i with events
     std::vector<PendingTimer> pending;

@@ -1112,14 +1112,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         uint32_t nbmax = nb;
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, d, 64));
-        if (L.pair_prio) {
-            // the SIMD's arbiter issues for the longest wave-tasks first: a heavy-tailed window's few 64 KB packets
-            // (1024 blocks of serial digest) set its end.  pair_prio 1: tasks of >= 32 blocks (2 KB packets);
-            // 2: every task by length (packets of 100-1500 B too)
-            const uint32_t b = L.pair_prio == 2 ? nbmax * 16 : nbmax;
-            if (b >= 256) __builtin_amdgcn_s_setprio(3);
-            else if (b >= 64) __builtin_amdgcn_s_setprio(2);
-            else if (b >= 32) __builtin_amdgcn_s_setprio(1);
+        // the SIMD's arbiter issues for the longest wave-tasks first: a heavy-tailed window's few 64 KB packets (1024
+        // blocks of serial digest) set its end.  pair_prio 1 (default): tasks of >= 32 blocks (2 KB packets; config
+        // 5: k_pair_test -4 %, the headline's packets never qualify); 2: every task by length (packets of 100-1500 B
+        // too: headline and SHA-1 leg +1-4 %)
+        const uint32_t prio_b = L.pair_prio == 2 ? nbmax * 16 : L.pair_prio == 1 ? nbmax : 0u;
+        const bool raised = prio_b >= 32;  // wave-uniform
+        if (raised) {
+            if (prio_b >= 256) __builtin_amdgcn_s_setprio(3);
+            else if (prio_b >= 64) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(1);
         }
         H st;
         if constexpr (DMA) {
@@ -1128,7 +1130,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         } else {
             hash_key<H>(kv, st);
         }
-        if (L.pair_prio) __builtin_amdgcn_s_setprio(0);
+        if (raised) __builtin_amdgcn_s_setprio(0);
         const uint32_t* filt = (const uint32_t*)(L.filters + q.filter_offset);
         const uint64_t m = q.m_bits;
         const uint32_t ok = filter_has_all<H, CHUNK>(filt, st, q.k, m);
