@@ -562,22 +562,50 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
             }
             __syncthreads();
             const uint64_t lim = total < W - filled ? total : W - filled;
-            for (uint64_t jj = threadIdx.x; jj < lim; jj += kFillThreads) {
-                const uint32_t j = (uint32_t)jj;
-                uint32_t lo = 0, hi = (uint32_t)kBatch;  // the last candidate starting at or before j
-                while (hi - lo > 1) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (run_pos[mid] <= j) lo = mid;
-                    else hi = mid;
+            // kRowU positions per thread per pass, their record loads issued together; a thread's positions only
+            // grow, so its candidate index is kept and searched forward only when the position leaves it (a global
+            // time of 10^5 rows is one candidate for every position)
+            constexpr int kRowU = 4;
+            uint32_t cur = 0;
+            for (uint64_t j0 = threadIdx.x; j0 < lim; j0 += (uint64_t)kFillThreads * kRowU) {
+                uint64_t lr[kRowU];
+                bool take[kRowU];
+#pragma unroll
+                for (int u = 0; u < kRowU; ++u) {
+                    const uint64_t jj = j0 + (uint64_t)kFillThreads * u;
+                    const uint32_t j = (uint32_t)jj;
+                    take[u] = false;
+                    lr[u] = 0;
+                    if (jj < lim) {
+                        if (cur + 1 < (uint32_t)kBatch && run_pos[cur + 1] <= j) {
+                            uint32_t lo = cur + 1, hi = (uint32_t)kBatch;  // the last candidate starting <= j
+                            while (hi - lo > 1) {
+                                const uint32_t mid = (lo + hi) >> 1;
+                                if (run_pos[mid] <= j) lo = mid;
+                                else hi = mid;
+                            }
+                            cur = lo;
+                        }
+                        const uint64_t e = j - run_pos[cur];
+                        take[u] = e != 0;  // a candidate's first row was emitted above
+                        lr[u] = p.dir == DSY_DESC ? run_x[cur] - e : run_x[cur] + e;
+                    }
                 }
-                const uint64_t e = j - run_pos[lo];
-                if (e == 0) continue;  // a candidate's first row: emitted above
-                const uint64_t lr = p.dir == DSY_DESC ? run_x[lo] - e : run_x[lo] + e;
-                const uint64_t row = L.st.live_row ? L.st.live_row[lr] : lr;
-                const RowRec rw = rec[row];
-                out[filled + jj] = row;
-                out_off[filled + jj] = rw.off;
-                out_len[filled + jj] = rw.len;
+                uint64_t row[kRowU];
+#pragma unroll
+                for (int u = 0; u < kRowU; ++u) row[u] = (take[u] && L.st.live_row) ? L.st.live_row[lr[u]] : lr[u];
+                RowRec rw[kRowU];
+#pragma unroll
+                for (int u = 0; u < kRowU; ++u) rw[u] = take[u] ? rec[row[u]] : RowRec{};
+#pragma unroll
+                for (int u = 0; u < kRowU; ++u) {
+                    if (take[u]) {
+                        const uint64_t dst = filled + j0 + (uint64_t)kFillThreads * u;
+                        out[dst] = row[u];
+                        out_off[dst] = rw[u].off;
+                        out_len[dst] = rw[u].len;
+                    }
+                }
             }
             __syncthreads();  // run_pos / run_x are rewritten by the next round
         }
