@@ -159,7 +159,13 @@ struct ReqState {
     uint32_t overflow; // output capacity exceeded (host retries with a larger capacity)
     uint64_t cand_next;// a split window's next cursor (k_fill's parts run concurrently): k_compact commits it to cand
     uint32_t commit;   // cand_next is pending
+    uint32_t sort_later; // a big window filled by one workgroup: its histogram is in bulk_hist, k_fill_sort places it
+    // the cursor at the start of the next window (written by k_compact): k_fill's workgroups decide on a split window
+    // from it, not from the cursor its part 0 advances while the other parts may still be starting
+    uint32_t win_meta;
     uint32_t pad;
+    uint64_t win_cand;
+    uint64_t win_sub;
 };
 
 // Device copy of one claim: the fields of dsy_request the kernels read, with the prefix bytes moved to a side

@@ -320,6 +320,8 @@ __device__ __forceinline__ void enum_range(const uint64_t* __restrict__ gt, cons
     *y = ly;
 }
 static constexpr uint32_t kSortBins = 1024;
+// k_fill: a window one workgroup selected with more pairs than this is sorted by k_fill_sort's workgroups
+static constexpr uint64_t kSplitSortMin = 8192;
 static_assert(kSortBins == kPoolBins, "a pooled family's histogram has k_fill's bins");
 
 // exclusive scan of kSortBins LDS counters in place, by the first wave of the workgroup (the others idle); the sum
@@ -373,7 +375,7 @@ __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* l
 template <class PlanAt>
 __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_slot, uint32_t r, const DevRequest& q,
                                            ReqState* S, uint32_t j, uint64_t c, uint64_t s, PlanAt plan_at,
-                                           uint64_t clk_start, uint64_t clk0) {
+                                           uint64_t clk_start, uint64_t clk0, bool may_split = false) {
     __shared__ uint64_t scan[kFillWaves + 2];
     __shared__ uint32_t first_cross;
     constexpr int kCandRuns = kFillThreads * 2;  // kBatch below: a round's candidates
@@ -703,6 +705,21 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
             if (hist[i]) atomicAdd(&ph[i], hist[i]);
         __syncthreads();
     }
+    if (may_split && filled > kSplitSortMin) {
+        // a big window this one workgroup selected (a claim whose global times hold 10^4-10^5 rows each, config
+        // 5's Zipf): its pairs are placed by k_fill_sort's workgroups, kBulkChunk each, from this histogram
+        uint32_t* gh = L.bulk_hist + (uint64_t)a_slot * kSortBins;
+        for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads) gh[i] = hist[i];
+        if (threadIdx.x == 0) S->sort_later = 1;
+        if (L.fill_clock && threadIdx.x == 0) {
+            uint64_t* fc = L.fill_clock + (uint64_t)a_slot * 4;
+            fc[0] = clk0;
+            fc[1] = clk1;
+            fc[2] = __builtin_amdgcn_s_memtime();
+            fc[3] = clk_start;
+        }
+        return;
+    }
     if (threadIdx.x < 64) {  // exclusive scan of the kSortBins counters by one wave
         const uint32_t per = kSortBins / 64, lane = threadIdx.x;
         uint32_t sum = 0;
@@ -834,11 +851,12 @@ __global__ void __launch_bounds__(kFillThreads) k_fill_sort(RespondLaunch L) {
     const uint32_t a_slot = blockIdx.x, part = blockIdx.y;
     const uint32_t r = L.act[a_slot];
     const ReqState* S = &L.state[r];
-    if (S->done || !S->commit) return;  // not a split window (k_fill sorted it whole)
+    if (S->done || !(S->commit || S->sort_later)) return;  // k_fill sorted it whole
     const uint64_t W = L.window;
+    const uint64_t nw = S->n_window;  // (W for a split window)
     const uint64_t base = (uint64_t)part * kBulkChunk;
-    if (base >= W) return;
-    const uint64_t n = W - base < kBulkChunk ? W - base : kBulkChunk;
+    if (base >= nw) return;
+    const uint64_t n = nw - base < kBulkChunk ? nw - base : kBulkChunk;
     const DevRequest& q = L.reqs[r];
     const uint32_t* gh = L.bulk_hist + (uint64_t)a_slot * kSortBins;
     for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads) {
@@ -974,8 +992,11 @@ __global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_waves_per_
         return;
     }
     const Plan* plans = L.plans + (uint64_t)r * L.J;
-    if (gridDim.y > 1) {  // a split window when the claim allows one (every part decides alike: S is not written here)
-        const ReqState st = *S;
+    if (gridDim.y > 1) {  // a split window when the claim allows one: every part decides from the window's start cursor
+        ReqState st = *S;
+        st.meta = S->win_meta;
+        st.cand = S->win_cand;
+        st.sub = S->win_sub;
         if (st.meta < L.J) {
             const Plan p = plans[st.meta];
             if (bulk_window(L, L.reqs[r], st, p)) {
@@ -985,7 +1006,9 @@ __global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_waves_per_
         }
         if (part > 0) return;
     }
-    fill_claim(L, a_slot, r, L.reqs[r], S, S->meta, S->cand, S->sub, [&](uint32_t j) { return plans[j]; }, clk0, clk0);
+    // (k_fill_sort runs after this launch whenever it has parts: a big window may leave its placement to it)
+    fill_claim(L, a_slot, r, L.reqs[r], S, S->meta, S->cand, S->sub, [&](uint32_t j) { return plans[j]; }, clk0, clk0,
+               gridDim.y > 1);
 }
 
 // First window of a call whose claims all serve one meta with device-side output capacities (respond_core's common
@@ -1448,17 +1471,21 @@ __global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
         }
     }
     overflow = __any(overflow) ? 1u : 0u;
-    if (S->commit) {  // a split window: its sort state cleared, its cursor (k_fill's parts read the old one) committed
+    if (S->commit || S->sort_later) {  // a split window or sort: its sort state cleared
         uint32_t* gh = L.bulk_hist + (uint64_t)a_slot * kSortBins;
         uint32_t* gc = L.bulk_cur + (uint64_t)a_slot * kSortBins;
         for (uint32_t i = lane; i < kSortBins; i += 64) gh[i] = gc[i] = 0;
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) {
-            S->cand = S->cand_next;
+            if (S->commit) S->cand = S->cand_next;  // the split window's cursor (k_fill's parts read the old one)
             S->commit = 0;
+            S->sort_later = 0;
         }
     }
     if (lane == 0) {
+        S->win_meta = S->meta;  // the next window's start (after a split window's commit above)
+        S->win_cand = S->cand;
+        S->win_sub = S->sub;
         S->emitted = emitted;
         L.emitted_n[r] = emitted;
         S->spent = spent;
