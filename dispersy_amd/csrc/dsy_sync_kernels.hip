@@ -375,15 +375,22 @@ __device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t* l
 template <class PlanAt>
 __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_slot, uint32_t r, const DevRequest& q,
                                            ReqState* S, uint32_t j, uint64_t c, uint64_t s, PlanAt plan_at,
-                                           uint64_t clk_start, uint64_t clk0, bool may_split = false) {
+                                           uint64_t clk_start, uint64_t clk0, bool may_split = false,
+                                           bool slice = false, uint64_t s0 = 0, uint64_t s1 = 0) {
     __shared__ uint64_t scan[kFillWaves + 2];
     __shared__ uint32_t first_cross;
     constexpr int kCandRuns = kFillThreads * 2;  // kBatch below: a round's candidates
     __shared__ uint32_t run_pos[kCandRuns];       // a round's candidates: first output position (round-relative)
     __shared__ uint64_t run_x[kCandRuns];         // and first live row
     const uint64_t W = L.window;
+    // slice: this workgroup is one of the window's parts -- every part selects alike (the same candidates, counts
+    // and cursor) and writes only the pairs at window positions [s0, s1); part 0 (s0 == 0) files the cursor, the
+    // parts' histograms go to bulk_hist and k_fill_sort places the pairs
+    if (!slice) { s0 = 0; s1 = W; }
+    if (s1 > W) s1 = W;
     // this window's missing-pair bits of the claim start clear (k_pair_test sets them)
-    for (uint64_t w = threadIdx.x; w < W / 64; w += kFillThreads) L.miss_mask[(uint64_t)a_slot * (W / 64) + w] = 0;
+    for (uint64_t w = s0 / 64 + threadIdx.x; w < s1 / 64; w += kFillThreads)
+        L.miss_mask[(uint64_t)a_slot * (W / 64) + w] = 0;
     uint64_t* out = L.pair_row + (uint64_t)a_slot * W;
     uint64_t* out_off = L.pair_off + (uint64_t)a_slot * W;
     uint32_t* out_len = L.pair_len + (uint64_t)a_slot * W;
@@ -423,27 +430,30 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
             const RowRec* __restrict__ rec = L.st.rec;
             // kDenseU rows per thread per round, every load of the round issued before the first is consumed
             constexpr int kDenseU = kSortReg;
-            const bool to_regs = filled == 0 && take <= (uint64_t)kFillThreads * kDenseU;
-            for (uint64_t i0 = 0; i0 < take; i0 += (uint64_t)kFillThreads * kDenseU) {
+            const bool to_regs = !slice && filled == 0 && take <= (uint64_t)kFillThreads * kDenseU;
+            // the positions this workgroup writes: i in [ib, ie)
+            const uint64_t ib = s0 > filled ? s0 - filled : 0;
+            const uint64_t ie = s1 > filled ? (take < s1 - filled ? take : s1 - filled) : 0;
+            for (uint64_t i0 = ib; i0 < ie; i0 += (uint64_t)kFillThreads * kDenseU) {
                 uint64_t row[kDenseU];
                 RowRec rr[kDenseU];
 #pragma unroll
                 for (int u = 0; u < kDenseU; ++u) {
                     const uint64_t i = i0 + threadIdx.x + (uint64_t)kFillThreads * u;
-                    const uint64_t ci = cs + (i < take ? i : 0);
+                    const uint64_t ci = cs + (i < ie ? i : ib);
                     const uint64_t cd = p.dir == DSY_DESC ? p.ncand - 1 - ci : ci;
                     const uint64_t lr = p.a + (p.mode == 1 ? p.g0 + cd * mod - p.g_lo : cd);
-                    row[u] = (L.st.live_row && i < take) ? L.st.live_row[lr] : lr;
+                    row[u] = (L.st.live_row && i < ie) ? L.st.live_row[lr] : lr;
                 }
 #pragma unroll
                 for (int u = 0; u < kDenseU; ++u) {
-                    const bool in = i0 + threadIdx.x + (uint64_t)kFillThreads * u < take;
+                    const bool in = i0 + threadIdx.x + (uint64_t)kFillThreads * u < ie;
                     rr[u] = in ? rec[row[u]] : RowRec{};
                 }
 #pragma unroll
                 for (int u = 0; u < kDenseU; ++u) {
                     const uint64_t i = i0 + threadIdx.x + (uint64_t)kFillThreads * u;
-                    if (i < take) {
+                    if (i < ie) {
                         out[filled + i] = row[u];
                         if (!to_regs) out_off[filled + i] = rr[u].off;  // read back only by the sort
                         out_len[filled + i] = rr[u].len;
@@ -540,7 +550,7 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
 #pragma unroll
         for (int u = 0; u < kCand; ++u) {
             const uint64_t dst = filled + at;
-            if (cnts[u] && dst < W) {
+            if (cnts[u] && dst >= s0 && dst < s1) {
                 out[dst] = row0[u];
                 out_off[dst] = r0[u].off;
                 out_len[dst] = r0[u].len;
@@ -563,13 +573,16 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
                 at += cnts[u];
             }
             __syncthreads();
-            const uint64_t lim = total < W - filled ? total : W - filled;
+            uint64_t lim = total < W - filled ? total : W - filled;  // positions j of this round: [jb, lim)
+            const uint64_t lim_s = s1 > filled ? s1 - filled : 0;
+            if (lim_s < lim) lim = lim_s;
+            const uint64_t jb = s0 > filled ? s0 - filled : 0;
             // kRowU positions per thread per pass, their record loads issued together; a thread's positions only
             // grow, so its candidate index is kept and searched forward only when the position leaves it (a global
             // time of 10^5 rows is one candidate for every position)
             constexpr int kRowU = 4;
             uint32_t cur = 0;
-            for (uint64_t j0 = threadIdx.x; j0 < lim; j0 += (uint64_t)kFillThreads * kRowU) {
+            for (uint64_t j0 = jb + threadIdx.x; j0 < lim; j0 += (uint64_t)kFillThreads * kRowU) {
                 uint64_t lr[kRowU];
                 bool take[kRowU];
 #pragma unroll
@@ -647,7 +660,7 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
             __syncthreads();
         }
     }
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && s0 == 0) {
         S->meta = j;
         S->cand = c;
         S->sub = s;
@@ -657,6 +670,34 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
         if (filled) atomicMax(&L.flags[kFlagChunks], (uint32_t)((filled + 63) / 64));
     }
     const uint64_t clk1 = L.fill_clock ? __builtin_amdgcn_s_memtime() : 0;
+    if (slice) {
+        // this part's pairs into the claim's histogram (and its pooled family's); k_fill_sort places them
+        __shared__ uint32_t sh[kSortBins];
+        for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads) sh[i] = 0;
+        __syncthreads();  // every thread's writes of this part's pairs are complete, sh cleared
+        const uint64_t e = filled < s1 ? filled : s1;
+        const uint32_t blk_s = q.hash_kind >= DSY_SHA384 ? 128u : 64u, lenb_s = q.hash_kind >= DSY_SHA384 ? 16u : 8u;
+        for (uint64_t t = s0 + threadIdx.x; t < e; t += kFillThreads)
+            atomicAdd(&sh[kSortBins - 1u - min(n_blocks(q.prefix_len + out_len[t], blk_s, lenb_s), kSortBins - 1)], 1u);
+        __syncthreads();
+        uint32_t* gh = L.bulk_hist + (uint64_t)a_slot * kSortBins;
+        const uint32_t fam_s = family_id(q.hash_kind, q.chunk_bytes, q.prefix_len);
+        uint32_t* ph = ((L.pool_mask >> fam_s) & 1u) ? L.pool_counts->hist[fam_s] : nullptr;
+        for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads)
+            if (sh[i]) {
+                atomicAdd(&gh[i], sh[i]);
+                if (ph) atomicAdd(&ph[i], sh[i]);
+            }
+        if (threadIdx.x == 0 && s0 == 0) S->sort_later = 1;
+        if (L.fill_clock && threadIdx.x == 0 && s0 == 0) {
+            uint64_t* fc = L.fill_clock + (uint64_t)a_slot * 4;
+            fc[0] = clk0;
+            fc[1] = clk1;
+            fc[2] = __builtin_amdgcn_s_memtime();
+            fc[3] = clk_start;
+        }
+        return;
+    }
     // Load balance: order this window's pairs by compression-block count (counting sort in LDS) so the 64
     // lanes of a hashing wave run the same number of blocks.  task[i] = the pair hashed by lane-slot i (blob
     // offset, length, window slot), so the hashing kernel reads 16 contiguous bytes per lane and then the packet;
@@ -779,6 +820,8 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
 // covers its 10^5-10^6 rows walks them in 2^18-pair windows: one workgroup per claim left the chip idle, 1-2 ms per
 // window.)
 static constexpr uint64_t kBulkChunk = (uint64_t)kFillThreads * 8;
+// k_fill: an enumerating claim with at most this many candidates left fills a window of >= 2 parts part by part
+static constexpr uint64_t kSliceCands = 2048;
 
 __device__ __forceinline__ bool bulk_window(const RespondLaunch& L, const DevRequest& q, const ReqState& S,
                                             const Plan& p) {
@@ -1001,6 +1044,15 @@ __global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_waves_per_
             const Plan p = plans[st.meta];
             if (bulk_window(L, L.reqs[r], st, p)) {
                 fill_bulk_part(L, a_slot, part, L.reqs[r], S, p, st.cand);
+                return;
+            }
+            // an enumeration with few candidates left, each global time possibly holding 10^4-10^5 rows (config 5's
+            // Zipf global times): every part selects alike from the window-start cursor and writes its slice
+            if (p.mode == 1 && st.cand <= p.ncand && p.ncand - st.cand <= kSliceCands) {
+                const uint64_t s0 = (uint64_t)part * kBulkChunk;
+                if (s0 >= L.window) return;
+                fill_claim(L, a_slot, r, L.reqs[r], S, st.meta, st.cand, st.sub, [&](uint32_t j) { return plans[j]; },
+                           clk0, clk0, false, true, s0, s0 + kBulkChunk);
                 return;
             }
         }
