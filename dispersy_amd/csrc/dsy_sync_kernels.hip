@@ -825,8 +825,9 @@ static constexpr uint64_t kSliceCands = 2048;
 
 __device__ __forceinline__ bool bulk_window(const RespondLaunch& L, const DevRequest& q, const ReqState& S,
                                             const Plan& p) {
+    // (a claim's last, partial window of such a span splits too: one workgroup walking 2^18 rows took ~0.4 ms)
     return S.meta < L.J && S.sub == 0 && p.mode == 0 && q.modulo <= 1 && p.dir != DSY_RANDOM && S.cand < p.ncand &&
-           p.ncand - S.cand >= L.window;
+           p.ncand - S.cand >= 2 * kBulkChunk;
 }
 
 __device__ __forceinline__ uint32_t sort_bin(const DevRequest& q, uint32_t len) {
@@ -838,11 +839,12 @@ __device__ __forceinline__ void fill_bulk_part(const RespondLaunch& L, uint32_t 
                                                const DevRequest& q, ReqState* S, const Plan& p, uint64_t c) {
     __shared__ uint32_t hist[kSortBins];
     const uint64_t W = L.window;
+    const uint64_t nw = p.ncand - c < W ? p.ncand - c : W;  // this window's pairs: the span's rest, at most W
     const uint64_t base = (uint64_t)part * kBulkChunk;
-    if (base >= W) return;
-    const uint64_t n = W - base < kBulkChunk ? W - base : kBulkChunk;  // W is a multiple of 64
+    if (base >= nw) return;
+    const uint64_t n = nw - base < kBulkChunk ? nw - base : kBulkChunk;
     uint64_t* mask = L.miss_mask + (uint64_t)a_slot * (W / 64) + base / 64;
-    for (uint64_t w = threadIdx.x; w < n / 64; w += kFillThreads) mask[w] = 0;
+    for (uint64_t w = threadIdx.x; w < (n + 63) / 64; w += kFillThreads) mask[w] = 0;
     for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads) hist[i] = 0;
     uint64_t* out = L.pair_row + (uint64_t)a_slot * W;
     uint64_t* out_off = L.pair_off + (uint64_t)a_slot * W;
@@ -879,10 +881,12 @@ __device__ __forceinline__ void fill_bulk_part(const RespondLaunch& L, uint32_t 
             if (ph) atomicAdd(&ph[i], hist[i]);
         }
     if (part == 0 && threadIdx.x == 0) {
-        S->n_window = W;
-        S->cand_next = c + W;
+        S->n_window = nw;
+        S->cand_next = c + nw;
         S->commit = 1;
-        atomicMax(&L.flags[kFlagChunks], (uint32_t)(W / 64));
+        // the span's rest in the last meta: every candidate visited (the next meta, if any, starts next window)
+        if (c + nw >= p.ncand && S->win_meta + 1 >= L.J) S->exhausted = 1;
+        atomicMax(&L.flags[kFlagChunks], (uint32_t)((nw + 63) / 64));
     }
 }
 
