@@ -299,12 +299,18 @@ __global__ void k_sim_resp_counts(dsy_sim_config c, const uint8_t* __restrict__ 
 __host__ __device__ constexpr uint32_t sim_respond_wave_lds(uint32_t nwords, bool dma) {
     return (2 * kSimListCap + nwords * 4 + 16 + 2 * kSimRespMax + 15) / 16 * 16 + (dma ? 4096u : 0u);
 }
-// shared by the workgroup's four claims: one round's pooled candidates (id, owner, position) in block-count order,
+// shared by the workgroup's NW claims: one round's pooled candidates (id, owner, position) in block-count order,
 // their miss flags per owner, a 64-bin histogram, per-wave counts and the active flags
-static constexpr uint32_t kSimRespPoolLds = 256 * 2 + 256 + 256 + 4 * 64 + 64 * 4 + 4 * 4 + 16;
-__host__ __device__ constexpr uint32_t sim_respond_lds(uint32_t nwords, bool dma) {
-    return 4 * sim_respond_wave_lds(nwords, dma) + kSimRespPoolLds;
+__host__ __device__ constexpr uint32_t sim_resp_pool_lds(uint32_t nw) {
+    return (64 * nw * 2 + 64 * nw + 64 * nw + nw * 64 + 64 * 4 + nw * 4 + 16 + 15) / 16 * 16;
 }
+__host__ __device__ constexpr uint32_t sim_respond_lds(uint32_t nwords, bool dma, uint32_t nw = 4) {
+    return nw * sim_respond_wave_lds(nwords, dma) + sim_resp_pool_lds(nw);
+}
+// claims (waves) per k_sim_respond workgroup.  DSY_SIM_WAVES=8 pools twice the candidates per round at the same 16
+// waves per CU (two 8-wave workgroups): lane utilisation 0.84 -> 0.91 but the launch 13.2 -> 14.2 ms (a round waits
+// for the slowest of eight claims at its barriers), so four stay the default
+static constexpr uint32_t kSimRespWaves = 8;
 
 // One wave per incoming claim answers it: the responder's packets in global-time order, 64 candidates per round,
 // hash + probe, then the missing ones are sent until the byte budget is spent (the crossing packet is sent) and the
@@ -313,8 +319,8 @@ __host__ __device__ constexpr uint32_t sim_respond_lds(uint32_t nwords, bool dma
 // the pool in chunks of 64 equal-length lanes (the filter and prefix of each lane's own claim); then each claim's
 // wave applies the budget rule to its candidates in order.  Without the pool a chunk runs as long as its longest
 // random-length packet (lane utilisation 0.56).
-template <class H, int CHUNK>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(H::kind == DSY_SHA256 ? 3 : 4, 8)))
+template <class H, int CHUNK, int NW>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(H::kind == DSY_SHA256 ? 3 : 4, 8)))
 k_sim_respond(dsy_sim_config c, const uint8_t* __restrict__ ublob, const uint64_t* __restrict__ uoff,
               const uint32_t* __restrict__ bits, const uint8_t* __restrict__ claims, uint64_t n_claims,
               uint8_t* __restrict__ out, const uint32_t* __restrict__ slots, unsigned long long* __restrict__ tested,
@@ -323,7 +329,7 @@ k_sim_respond(dsy_sim_config c, const uint8_t* __restrict__ ublob, const uint64_
     // MD5 / SHA-1 stage the packets through LDS with DMA (hash_key_dma_reg, one block per stage), as the claim build
     constexpr bool kDma = H::kind == DSY_MD5 || H::kind == DSY_SHA1;
     const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint64_t ci = (uint64_t)blockIdx.x * 4 + wv;
+    const uint64_t ci = (uint64_t)blockIdx.x * NW + wv;
     const bool live = ci < n_claims;  // wave-uniform; idle waves still meet the barriers
     const uint32_t nwords = (uint32_t)((c.m_bits + 31) / 32);
     const uint32_t wave_b = sim_respond_wave_lds(nwords, kDma);
@@ -334,13 +340,13 @@ k_sim_respond(dsy_sim_config c, const uint8_t* __restrict__ ublob, const uint64_
     uint32_t* filt = filt_of(wv);
     uint8_t* pre = (uint8_t*)(filt + nwords);
     uint16_t* outl = (uint16_t*)(pre + 16);
-    uint8_t* pool = sim_lds + 4 * wave_b;
-    uint16_t* pool_id = (uint16_t*)pool;         // [256]
-    uint8_t* pool_own = pool + 512;              // [256] owner wave
-    uint8_t* pool_pos = pool + 768;              // [256] position in the owner's chunk
-    uint8_t* flags = pool + 1024;                // [4][64] miss flags of the round
-    uint32_t* phist = (uint32_t*)(pool + 1280);  // [64]
-    uint32_t* pcnt = phist + 64;                 // [4] candidates per wave this round
+    uint8_t* pool = sim_lds + NW * wave_b;
+    uint16_t* pool_id = (uint16_t*)pool;                 // [64 NW]
+    uint8_t* pool_own = pool + 128 * NW;                 // [64 NW] owner wave
+    uint8_t* pool_pos = pool + 192 * NW;                 // [64 NW] position in the owner's chunk
+    uint8_t* flags = pool + 256 * NW;                    // [NW][64] miss flags of the round
+    uint32_t* phist = (uint32_t*)(pool + 320 * NW);      // [64]
+    uint32_t* pcnt = phist + 64;                         // [NW] candidates per wave this round
     dsy_sim_claim_header h{};
     uint32_t n_sel = 0;
     if (live) {
@@ -368,10 +374,10 @@ k_sim_respond(dsy_sim_config c, const uint8_t* __restrict__ ublob, const uint64_
         if (lane == 0) pcnt[wv] = cnt;
         if (threadIdx.x < 64) phist[threadIdx.x] = 0;
         __syncthreads();
-        const uint32_t c0 = pcnt[0], c1 = pcnt[1], c2 = pcnt[2], c3 = pcnt[3];
-        const uint32_t pn = c0 + c1 + c2 + c3;
+        uint32_t pn = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) pn += pcnt[w];
         if (!pn) break;  // workgroup-uniform
-        const uint32_t at = wv == 0 ? 0 : wv == 1 ? c0 : wv == 2 ? c0 + c1 : c0 + c1 + c2;
         // pool this wave's candidates, then rank them by block count over the workgroup
         uint32_t my_id = 0, my_bin = 0;
         if (lane < cnt) {
@@ -397,7 +403,6 @@ k_sim_respond(dsy_sim_config c, const uint8_t* __restrict__ ublob, const uint64_
             pool_own[slot] = (uint8_t)wv;
             pool_pos[slot] = (uint8_t)lane;
         }
-        (void)at;
         __syncthreads();
         if (wv * 64 < pn) {  // wave wv hashes pooled chunk wv (workgroup-uniform per wave)
             const uint32_t i = wv * 64 + lane;
@@ -497,9 +502,16 @@ static hipError_t sim_family(int op, const SimLaunch& L) {
     } else {
         if (!L.n_in) return hipSuccess;
         constexpr bool dma = H::kind == DSY_MD5 || H::kind == DSY_SHA1;
-        const size_t lds = sim_respond_lds((uint32_t)((L.cfg.m_bits + 31) / 32), dma);
-        hipLaunchKernelGGL((k_sim_respond<H, CHUNK>), dim3((uint32_t)((L.n_in + 3) / 4)), dim3(256), lds, L.stream, L.cfg,
-                           L.ublob, L.uoff, L.bits, L.in, L.n_in, L.out, L.slots, L.tested, L.work);
+        static const uint32_t nw = getenv("DSY_SIM_WAVES") && atoi(getenv("DSY_SIM_WAVES")) == 8 ? kSimRespWaves : 4;
+        const uint32_t nwords = (uint32_t)((L.cfg.m_bits + 31) / 32);
+        if (nw == 4)
+            hipLaunchKernelGGL((k_sim_respond<H, CHUNK, 4>), dim3((uint32_t)((L.n_in + 3) / 4)), dim3(256),
+                               sim_respond_lds(nwords, dma, 4), L.stream, L.cfg, L.ublob, L.uoff, L.bits, L.in, L.n_in,
+                               L.out, L.slots, L.tested, L.work);
+        else
+            hipLaunchKernelGGL((k_sim_respond<H, CHUNK, kSimRespWaves>), dim3((uint32_t)((L.n_in + kSimRespWaves - 1) / kSimRespWaves)),
+                               dim3(64 * kSimRespWaves), sim_respond_lds(nwords, dma, kSimRespWaves), L.stream, L.cfg,
+                               L.ublob, L.uoff, L.bits, L.in, L.n_in, L.out, L.slots, L.tested, L.work);
     }
     return hipGetLastError();
 }
