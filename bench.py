@@ -433,11 +433,41 @@ def run(args, rank, world, local):
             "dropin": dropin,
             "sha1_respond": sha1,
         }
+        line.update(tail_keys(gossip, sha1, heavy, single, large))
         print(json.dumps(line))
     if store is not None:
         lib.dsy_store_free(store)
     if dist:
         dist.destroy_process_group()
+
+
+def _get(d, *path):
+    for k in path:
+        if not isinstance(d, dict) or k not in d:
+            return None
+        d = d[k]
+    return d
+
+
+def tail_keys(gossip, sha1=None, heavy=None, single=None, large=None):
+    """Compact top-level keys printed LAST on the JSON line, so a driver that keeps only the tail of stdout still
+    sees BASELINE's second metric (gossip sync rounds/s at N GPUs, config 3) and each leg's headline number.  The
+    nested legs above hold the same values with their rooflines and CPU baselines."""
+    out = {
+        "gossip_n_gpus": _get(gossip, "n_gpus") if gossip else None,
+        "gossip_rounds_per_s": _get(gossip, "value"),
+        "gossip_ms_per_round": _get(gossip, "ms_per_round"),
+        "gossip_store_checksum": _get(gossip, "store_checksum"),
+        "gossip_scaling": _get(gossip, "scaling"),
+        "sha1_respond_int32_frac": _get(sha1, "roofline", "frac"),
+        "sha1_respond_ms_per_step": _get(sha1, "ms_per_step"),
+        "cfg5_ms_per_step": _get(heavy, "ms_per_step"),
+        "cfg5_hbm_frac": _get(heavy, "roofline", "hbm", "frac"),
+        "cfg1_sha1_int32_frac": _get(single, "sha1", "roofline_test", "valu_int32", "frac"),
+        "cfg4_sha256_add_int32_frac": {k: v.get("add_valu_frac") for k, v in (_get(large, "filters") or {}).items()}
+        or None,
+    }
+    return out
 
 
 class Batches(object):

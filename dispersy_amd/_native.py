@@ -13,7 +13,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("DSY_LIB", os.path.join(_HERE, "libdsybloom.so"))
 
-DSY_OK, DSY_EINVAL, DSY_EHIP, DSY_ENOMEM, DSY_ECAPACITY, DSY_EUNSORTED, DSY_EEMPTY = 0, -1, -2, -3, -4, -5, -6
+DSY_OK, DSY_EINVAL, DSY_EHIP, DSY_ENOMEM, DSY_ECAPACITY, DSY_EUNSORTED, DSY_EEMPTY, DSY_EINTERNAL = 0, -1, -2, -3, -4, -5, -6, -7
 DSY_MD5, DSY_SHA1, DSY_SHA256, DSY_SHA384, DSY_SHA512 = range(5)
 HASH_KINDS = {"md5": DSY_MD5, "sha1": DSY_SHA1, "sha256": DSY_SHA256, "sha384": DSY_SHA384, "sha512": DSY_SHA512}
 DSY_ASC, DSY_DESC, DSY_RANDOM = 0, 1, 2
@@ -21,6 +21,7 @@ DSY_ASC, DSY_DESC, DSY_RANDOM = 0, 1, 2
 DSY_DUP_NEW, DSY_DUP_EXACT, DSY_DUP_KEEP, DSY_DUP_REPLACE, DSY_DUP_TRIPLET = range(5)
 DIRECTIONS = {"ASC": DSY_ASC, "DESC": DSY_DESC, "RANDOM": DSY_RANDOM}
 BLOB_GUARD = 256
+SIM_RESP_MAX = 64  # DSY_SIM_RESP_MAX: packets per simulator response record
 SYNC_HEADER = 24  # DSY_SYNC_HEADER: '>QQHHBH' + the 1-byte prefix (conversion.py:727-728)
 
 # the ctx timer classes of dsy_ctx_kernel_time

@@ -107,6 +107,7 @@ struct RespondSlot {
     hipEvent_t ev_done = nullptr;
     bool busy = false;       // submitted, not yet waited for
     uint64_t ticket = 0;
+    uint64_t last_use = 0;   // when a job last started here: submit takes the least recently used free slot
     RespondJob job;
 };
 
@@ -118,6 +119,7 @@ struct dsy_ctx {
     static constexpr int kSlots = 3;  // responder batches in flight at most (dsy_sync_respond_submit)
     RespondSlot rs[kSlots];
     uint64_t next_ticket = 1;
+    uint64_t use_clock = 0;  // RespondSlot::last_use
     uint32_t max_grid = 2048;
     int bloom_diag = 0;  // DSY_BLOOM_DIAG at creation: single-filter ceiling diagnostics (k_bloom DIAG)
     int pair_diag = 0;   // DSY_PAIR_DIAG at creation: responder ceiling diagnostics (k_pair_test DIAG)
@@ -132,6 +134,7 @@ struct dsy_ctx {
     int pool_queue = 0;
     int pool_deal = 0;   // DSY_POOL_DEAL: the pooled hashing's resident-grid deal (k_pair_test<POOL>)
     int pair_prio = 1;   // DSY_PAIR_PRIO: k_pair_test raises the wave priority of long wave-tasks (0 off)
+    int bulk_zero = 1;   // DSY_BULK_ZERO=0: the calls do not zero their split-window sort state (diagnostic)
     uint32_t direct_kinds = 0;  // DSY_PAIR_DIRECT: bit k = hash kind k's responder hashing uses direct loads
     uint32_t timing = 0;  // bit i: bracket class i with events
     std::vector<PendingTimer> pending;
@@ -500,6 +503,7 @@ int dsy_ctx_create(int device, dsy_ctx** out) {
     if (const char* v = getenv("DSY_POOL_QUEUE")) c->pool_queue = atoi(v);
     if (const char* v = getenv("DSY_POOL_DEAL")) c->pool_deal = atoi(v);
     if (const char* v = getenv("DSY_PAIR_PRIO")) c->pair_prio = atoi(v);
+    if (const char* v = getenv("DSY_BULK_ZERO")) c->bulk_zero = atoi(v);
     if (const char* v = getenv("DSY_PAIR_DIRECT")) c->direct_kinds = (uint32_t)strtoul(v, nullptr, 0);
     c->pool_kinds &= (1u << DSY_MD5) | (1u << DSY_SHA1) | (1u << DSY_SHA256);
     hipHostMalloc(&c->pinned, 4096, hipHostMallocDefault);
@@ -1924,11 +1928,11 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
     if (io_fresh) HIP_TRY(hipMemsetAsync(d_io, 0, io_b, st));  // flags start (and stay, k_compact) at zero
     if ((rc = ws_get(w, "plans", std::max<size_t>((size_t)R * J, 1) * sizeof(Plan), &d_plans))) return rc;
     if ((rc = ws_get(w, "state", std::max<size_t>(R, 1) * sizeof(ReqState), &d_state))) return rc;
-    void* d_bulk;  // split windows' sort state: [R][kSortBins] histogram + cursors, zero between windows
-    bool bulk_fresh = false;
+    // split windows' sort state: [R][kSortBins] histogram + cursors, zeroed by the call's first kernel (k_setup or
+    // k_fill_first) and kept zero between windows by k_compact
+    void* d_bulk;
     const size_t bulk_b = (size_t)std::max<uint32_t>(R, 1) * 2 * 1024 * 4;
-    if ((rc = ws_get(w, "bulk_sort", bulk_b, &d_bulk, &bulk_fresh))) return rc;
-    if (bulk_fresh) HIP_TRY(hipMemsetAsync(d_bulk, 0, bulk_b, st));
+    if ((rc = ws_get(w, "bulk_sort", bulk_b, &d_bulk))) return rc;
     // pooled families (c->pool_kinds): the pooled order and the families' counts (zero outside a window)
     uint32_t pool_mask = 0;
     if (!c->pair_diag && pool <= 0xffffffffull)
@@ -1936,9 +1940,10 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
             if (!fam_members[f].empty() && ((c->pool_kinds >> (f / 6)) & 1u)) pool_mask |= 1u << f;
     void* d_pool_counts = nullptr;
     if (pool_mask) {
-        bool pc_fresh = false;
-        if ((rc = ws_get(w, "pool_counts", sizeof(PoolCounts), &d_pool_counts, &pc_fresh))) return rc;
-        if (pc_fresh) HIP_TRY(hipMemsetAsync(d_pool_counts, 0, sizeof(PoolCounts), st));
+        if ((rc = ws_get(w, "pool_counts", sizeof(PoolCounts), &d_pool_counts))) return rc;
+        // every call starts from zero counts (k_pair_test<POOL> keeps them zero between windows; a call that ended
+        // early may have left some)
+        HIP_TRY(hipMemsetAsync(d_pool_counts, 0, sizeof(PoolCounts), st));
     }
     uint8_t* h_in;
     if ((rc = stage_get(w, in_b + kHostHead + act_done_b, &h_in))) return rc;
@@ -2012,6 +2017,7 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
     L.st.live_gt = s->d_live_gt;
     L.st.live_row = s->d_live_row;
     L.st.n_live = s->n_live;
+    L.st.lines_bytes = s->lines_cap;
     L.reqs = (const DevRequest*)d_in;
     L.metas = (const SegMeta*)((uint8_t*)d_in + reqs_b);
     jb.d_slots = (const uint32_t*)((uint8_t*)d_in + reqs_b + metas_b);
@@ -2044,6 +2050,7 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
     L.pool_queue = c->pool_queue;
     L.pool_deal = c->pool_deal;
     L.pair_prio = c->pair_prio;
+    L.bulk_zero = c->bulk_zero;
     L.pool_counts = (PoolCounts*)d_pool_counts;
     if ((rc = job_pair_buffers(sl, pool))) return rc;
 
@@ -2090,10 +2097,27 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
         }
     }
     if ((rc = ws_get(w, "packed", std::max<uint64_t>(cap_total, 1) * 8, &jb.d_packed))) return rc;
+    L.packed_cap = cap_total;
     if ((rc = ws_get(w, "packed_off", ((size_t)R + 1) * 8, &jb.d_packed_off))) return rc;
     size_t n_act = 0;
     for (auto& fa : jb.fam_active) n_act += fa.size();
     if (n_act) return job_window(c, sl);
+    return DSY_OK;
+}
+
+// The host-mapped status a window's kernels leave: the output-capacity overflow flag (k_compact) and the bounds
+// checks (kStatusGuard: an index the responder computed fell outside its buffer; the access was skipped).
+static int job_status(const RespondJob& jb) {
+    const volatile uint64_t* h = (const volatile uint64_t*)jb.h_io;
+    if (h[kStatusOverflow]) return fail(DSY_ECAPACITY, "internal: a claim overflowed its output capacity");
+    if (const uint64_t g = h[kStatusGuard]) {
+        static const char* what[] = {"k_fill_sort placed a pair past its window", "k_pair_test read a task record "
+                                     "naming a packet outside the line copy", "k_pack's output overflowed the "
+                                     "packed buffer", "a window held more pairs than W"};
+        for (int b = 0; b < 4; ++b)
+            if ((g >> (8 * b)) & 0xff) return fail(DSY_EINTERNAL, "internal: bounds check tripped: %s", what[b]);
+        return fail(DSY_EINTERNAL, "internal: bounds check tripped (0x%llx)", (unsigned long long)g);
+    }
     return DSY_OK;
 }
 
@@ -2111,7 +2135,7 @@ static int job_finish(dsy_ctx* c, RespondSlot& sl, uint64_t** d_packed, uint64_t
         HIP_TRY(hipEventSynchronize(sl.ev_done));  // this job's window, not what later batches queued behind it
         if (g_host_profile) jb.hp_wait += host_us() - w0;
         // capacity overflow can only come from a wrong min_len bound; report it loudly
-        if (((const volatile uint64_t*)jb.h_io)[kCntN]) return fail(DSY_ECAPACITY, "internal: a claim overflowed its output capacity");
+        if (int rc = job_status(jb)) return rc;
         const volatile uint8_t* done = jb.h_io + kHostHead;
         size_t a = 0, left = 0;
         for (auto& fa : jb.fam_active) {
@@ -2129,6 +2153,7 @@ static int job_finish(dsy_ctx* c, RespondSlot& sl, uint64_t** d_packed, uint64_t
     if (!jb.ran) {
         HIP_TRY(launch_pack(L, (uint64_t*)jb.d_packed, (uint64_t*)jb.d_packed_off, nullptr));
         HIP_TRY(hipStreamSynchronize(st));
+        if (int rc = job_status(jb)) return rc;
     }
     for (uint32_t k = 0; k < kCntN; ++k) h_tot[k] = ((const volatile uint64_t*)jb.h_io)[k];
     timers_collect_lazy(c);
@@ -2155,6 +2180,7 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
                         uint64_t** d_packed_off, uint64_t* total_pairs) {
     if (c->inflight()) return fail(DSY_EINVAL, "submitted responder batches are in flight: dsy_sync_respond_wait them first");
     RespondSlot& sl = sync_slot(c);
+    sl.last_use = ++c->use_clock;
     int rc = job_start(c, sl, s, reqs, R, d_filters, filters_len, metas, J, responder_gt, include_inactive, byte_limit,
                        seed);
     if (rc) return rc;
@@ -2210,11 +2236,13 @@ int dsy_sync_respond_submit(dsy_ctx* c, const dsy_store* s, const dsy_request* r
     if (!c || !s || (R && (!reqs || !d_filters)) || (nmeta && !metas) || !out_ticket)
         return fail(DSY_EINVAL, "NULL argument");
     Guard g(c);
+    // the least recently used free slot: a waited-for batch's output stays valid until two more submits at least
     int k = -1;
-    for (int i = 0; i < dsy_ctx::kSlots && k < 0; ++i)
-        if (!c->rs[i].busy) k = i;
+    for (int i = 0; i < dsy_ctx::kSlots; ++i)
+        if (!c->rs[i].busy && (k < 0 || c->rs[i].last_use < c->rs[k].last_use)) k = i;
     if (k < 0) return fail(DSY_EINVAL, "%d responder batches are in flight: dsy_sync_respond_wait one first", dsy_ctx::kSlots);
     RespondSlot& sl = c->rs[k];
+    sl.last_use = ++c->use_clock;
     int rc = job_start(c, sl, s, reqs, R, d_filters, 0, metas, nmeta, responder_global_time, include_inactive,
                        byte_limit, random_seed);
     if (rc) {

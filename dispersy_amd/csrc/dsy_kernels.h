@@ -120,6 +120,7 @@ struct StoreView {
     const uint64_t* live_gt;  // [n_live] global_time of live row i
     const uint64_t* live_row; // [n_live] store row of live row i (nullptr: identity)
     uint64_t n_live;
+    uint64_t lines_bytes;     // bytes of `lines` (both DSY_BLOB_GUARD guards included): the hashing's bounds check
 };
 
 // Per (claim, meta) selection plan.
@@ -139,6 +140,14 @@ struct Plan {
 // Spread over kCntSpread copies (a workgroup adds into copy blockIdx % kCntSpread): thousands of same-address
 // atomics at the end of a launch serialise into its tail; the host sums the copies.
 enum { kCntPairs = 0, kCntBlocks = 1, kCntBytes = 2, kCntUseful = 3, kCntSlots = 4, kCntN = 8 };
+// host-mapped status words after the kCntN totals: [kStatusOverflow] a claim overflowed its output capacity
+// (k_compact); [kStatusGuard] one byte per device-side bounds check that tripped (kGuard*): an index the responder
+// computed fell outside the buffer it addresses -- the access is skipped and the call fails with DSY_EINTERNAL
+enum { kStatusOverflow = kCntN, kStatusGuard = kCntN + 1 };
+enum { kGuardSortPos = 0, kGuardTask = 1, kGuardPack = 2, kGuardWindow = 3 };
+__device__ __forceinline__ void guard_trip(uint64_t* h_status, int which) {
+    ((volatile uint8_t*)&h_status[kStatusGuard])[which] = 1;
+}
 static constexpr uint32_t kCntSpread = 64;
 __device__ __forceinline__ unsigned long long* counter(uint64_t* counters, uint32_t which) {
     return (unsigned long long*)&counters[(blockIdx.x % kCntSpread) * kCntN + which];
@@ -200,8 +209,8 @@ struct RespondLaunch {
     const uint32_t* act;      // device [n_act]: window slot a serves claim act[a]
     uint32_t n_act;
     uint8_t* act_done;        // host-mapped [n_act]: written by k_compact, 1 once claim act[a] is done
-    uint64_t* h_status;       // host-mapped [kCntN + 1]: counter totals (folded by the pack kernels) and the
-                              // overflow flag (k_compact)
+    uint64_t* h_status;       // host-mapped [kCntN + 2]: counter totals (folded by the pack kernels), the
+                              // overflow flag (k_compact) and the bounds-check bytes (kStatusGuard)
     Plan* plans;              // device [R*J]
     ReqState* state;          // device [R]
     uint64_t* upper;          // device [R]: upper bound of selected rows per claim
@@ -216,6 +225,7 @@ struct RespondLaunch {
     uint32_t* bulk_cur;       // device [R][kSortBins]: the split window's sort cursors (k_fill_sort)
     uint64_t* miss_mask;      // device [n_act * W / 64]: bit t of claim slot a = window pair t is missing
     uint64_t* out;            // device [sum cap]
+    uint64_t packed_cap;      // rows the packed output holds (k_pack's bounds check)
     uint32_t* flags;          // device [16], zeroed by k_setup: [kFlagChunks] the window's longest claim in 64-pair
                               // chunks (k_fill atomicMax, read by k_pair_test, reset by k_compact)
     uint64_t* fill_clock;     // optional [n_act][4] s_memtime stamps of k_fill phases (DSY_FILL_PROFILE)
@@ -232,6 +242,8 @@ struct RespondLaunch {
     int pool_queue;           // k_pair_test<POOL>: waves take wave-tasks from a queue instead of a grid stride
     int pool_deal;            // k_pair_test<POOL>: resident grid, wave-tasks dealt so each SIMD's waves sum to the mean
     int pair_prio;            // k_pair_test: wave priority by the wave-task's length (s_setprio)
+    int bulk_zero;            // k_setup / k_fill_first zero the call's bulk_hist / bulk_cur rows (DSY_BULK_ZERO=0: not,
+                              // a diagnostic of the state k_compact leaves between calls)
     PoolCounts* pool_counts;  // device, zero outside a window (k_pair_test<POOL> clears its family's)
     PoolTask* pool;           // device [pool]: the pooled order of the family being hashed
     hipStream_t stream;

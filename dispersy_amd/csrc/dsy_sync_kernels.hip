@@ -27,6 +27,7 @@
 namespace dsy {
 
 static constexpr uint64_t kMaxGt = 0x7fffffffffffffffull;  // 2^63 - 1 (community.py:2547-2548, :2806)
+static constexpr uint32_t kBulkBins = 1024;  // == kSortBins: bulk_hist / bulk_cur entries per window slot
 
 __device__ __forceinline__ uint64_t lower_bound_gt(const uint64_t* gt, uint64_t a, uint64_t b, uint64_t v) {
     while (a < b) {
@@ -222,6 +223,10 @@ __global__ void __launch_bounds__(256) k_setup(RespondLaunch L, const uint4* __r
     if (tid < in_words) dst[tid] = cw;
     for (uint32_t i = tid + nthr; i < in_words; i += nthr) dst[i] = src[i];
     for (uint32_t i = tid; i < zero_words; i += nthr) zero[i] = make_uint4(0, 0, 0, 0);
+    // the split windows' sort state starts every call at zero in this call's layout (k_compact keeps it zero between
+    // windows; a call that ended early, or one with another R, may have left counts where this call's slots are)
+    if (L.bulk_zero)
+        for (uint64_t i = tid; i < (uint64_t)L.R * kBulkBins; i += nthr) L.bulk_hist[i] = L.bulk_cur[i] = 0;
     if (planner) {
         DevRequest q;
         SegMeta mt;
@@ -319,7 +324,7 @@ __device__ __forceinline__ void enum_range(const uint64_t* __restrict__ gt, cons
     *x = lx;
     *y = ly;
 }
-static constexpr uint32_t kSortBins = 1024;
+static constexpr uint32_t kSortBins = kBulkBins;
 // k_fill: a window one workgroup selected with more pairs than this is sorted by k_fill_sort's workgroups
 static constexpr uint64_t kSplitSortMin = 8192;
 static_assert(kSortBins == kPoolBins, "a pooled family's histogram has k_fill's bins");
@@ -901,6 +906,10 @@ __global__ void __launch_bounds__(kFillThreads) k_fill_sort(RespondLaunch L) {
     if (S->done || !(S->commit || S->sort_later)) return;  // k_fill sorted it whole
     const uint64_t W = L.window;
     const uint64_t nw = S->n_window;  // (W for a split window)
+    if (nw > W) {  // (cannot happen: the fill never places more than W pairs)
+        if (threadIdx.x == 0) guard_trip(L.h_status, kGuardWindow);
+        return;
+    }
     const uint64_t base = (uint64_t)part * kBulkChunk;
     if (base >= nw) return;
     const uint64_t n = nw - base < kBulkChunk ? nw - base : kBulkChunk;
@@ -955,7 +964,11 @@ __global__ void __launch_bounds__(kFillThreads) k_fill_sort(RespondLaunch L) {
             tk.off = off_w[t];
             tk.len = len[u];
             tk.slot = (uint32_t)(base + t);
-            task[atomicAdd(&hist[sort_bin(q, len[u])], 1u)] = tk;
+            // the position lies in [0, nw) when bulk_hist holds exactly this window's counts; a stale count (state a
+            // window left behind) would place past the claim's slot: refuse the write and fail the call loudly
+            const uint32_t pos = atomicAdd(&hist[sort_bin(q, len[u])], 1u);
+            if (pos < nw) task[pos] = tk;
+            else guard_trip(L.h_status, kGuardSortPos);
         }
     }
 }
@@ -1095,6 +1108,10 @@ __global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_waves_per_
     for (uint32_t i = tid + nthr; i < in_words; i += nthr) dst[i] = src[i];
     if (blockIdx.x == 0)
         for (uint32_t i = threadIdx.x; i < counter_words; i += kFillThreads) counters[i] = make_uint4(0, 0, 0, 0);
+    // this window slot's split-window sort state starts the call at zero (as k_setup's loop does)
+    if (L.bulk_zero)
+        for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads)
+            L.bulk_hist[(uint64_t)a_slot * kSortBins + i] = L.bulk_cur[(uint64_t)a_slot * kSortBins + i] = 0;
     if (threadIdx.x < kQw) ((uint4*)&sq)[threadIdx.x] = w;
     else if (threadIdx.x < kQw + kMw) ((uint4*)&sp)[threadIdx.x - kQw] = w;  // the SegMeta, parked in sp
     __syncthreads();
@@ -1190,9 +1207,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
             a_slot = pt.a_slot;
             r = L.act[a_slot];
             if (active) {
-                t = pt.slot;
-                key = L.st.lines + ((uint64_t)pt.line << 7) + kLineBias;
-                len = pt.len;
+                const uint64_t off = ((uint64_t)pt.line << 7) + kLineBias;
+                if (off < DSY_BLOB_GUARD || off + pt.len + DSY_BLOB_GUARD > L.st.lines_bytes || pt.slot >= W) {
+                    guard_trip(L.h_status, kGuardTask);
+                    active = false;
+                } else {
+                    t = pt.slot;
+                    key = L.st.lines + off;
+                    len = pt.len;
+                }
             }
         } else {
             // chunk-major task order: wave-task v hashes 64-pair chunk (v / n_list) of claim (v % n_list), so the
@@ -1202,13 +1225,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
             const uint64_t i0 = (v / n_list) * 64;
             const uint64_t n = L.state[r].n_window;
             if (i0 >= n) continue;  // wave-uniform: past this claim's window
+            if (n > W) {  // wave-uniform (cannot happen: the fill never places more than W pairs)
+                if (lane == 0) guard_trip(L.h_status, kGuardWindow);
+                continue;
+            }
             const uint64_t i = i0 + lane;
             active = i < n;
             if (active) {
                 const PairTask tk = L.task[(uint64_t)a_slot * W + i];
-                t = tk.slot;
-                key = L.st.lines + tk.off;
-                len = tk.len;
+                // bounds check of the packet the record names (a record the fill did not write this window would
+                // address another store's line copy): skipped and reported, never dereferenced
+                if (tk.off < DSY_BLOB_GUARD || tk.off + tk.len + DSY_BLOB_GUARD > L.st.lines_bytes ||
+                    tk.slot >= n) {
+                    guard_trip(L.h_status, kGuardTask);
+                    active = false;
+                } else {
+                    t = tk.slot;
+                    key = L.st.lines + tk.off;
+                    len = tk.len;
+                }
             }
         }
         const DevRequest& q = L.reqs[r];
@@ -1546,7 +1581,7 @@ __global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
         L.emitted_n[r] = emitted;
         S->spent = spent;
         S->overflow = overflow;
-        if (overflow) L.h_status[kCntN] = 1;  // host-mapped: read after the window's sync
+        if (overflow) L.h_status[kStatusOverflow] = 1;  // host-mapped: read after the window's sync
         if (done || S->exhausted) S->done = 1;
         L.act_done[a_slot] = (uint8_t)S->done;
         atomicAdd(counter(L.counters, kCntPairs), (unsigned long long)n);
@@ -1589,6 +1624,10 @@ __global__ void __launch_bounds__(256) k_copy_out(RespondLaunch L, const uint64_
     const uint32_t r = blockIdx.x;
     const ReqState& S = L.state[r];
     const uint64_t n = S.emitted < S.cap ? S.emitted : S.cap;
+    if (packed_offsets[r] + n > L.packed_cap) {
+        if (threadIdx.x == 0) guard_trip(L.h_status, kGuardPack);
+        return;
+    }
     for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) packed[packed_offsets[r] + i] = L.out[S.out_base + i];
 }
 
@@ -1602,7 +1641,10 @@ __global__ void __launch_bounds__(256) k_pack_fused(RespondLaunch L, uint64_t* p
     const uint64_t off = block_sum_256(s, red);
     const ReqState& S = L.state[r];
     const uint64_t n = S.emitted < S.cap ? S.emitted : S.cap;
-    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) packed[off + i] = L.out[S.out_base + i];
+    const bool fits = off + n <= L.packed_cap;  // (an overflowed claim's emitted exceeds its cap: k_compact flags it)
+    if (!fits && threadIdx.x == 0) guard_trip(L.h_status, kGuardPack);
+    if (fits)
+        for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) packed[off + i] = L.out[S.out_base + i];
     if (threadIdx.x == 0) {
         packed_offsets[r] = off;
         if (r + 1 == L.R) packed_offsets[L.R] = off + S.emitted;

@@ -78,6 +78,16 @@ class GpuEngine(object):
         self.ctx = ctx or _native.Context(device.index if device.index is not None else 0)
         self.lib = self.ctx.lib
         _native.check(self.lib.dsy_sim_setup(ctypes.byref(cfg)))
+        # a response holds at most DSY_SIM_RESP_MAX packets: every packet but the budget-crossing last one costs at
+        # least the universe's shortest packet, so refuse a configuration that could overflow it (the merge's sticky
+        # overflow flag, reported by dsy_sim_stats, stays as the backstop)
+        lens = np.diff(np.asarray(offsets, dtype=np.int64))
+        if len(lens) and cfg.byte_limit > 0:
+            most = cfg.byte_limit // max(int(lens.min()), 1) + 1
+            if most > _native.SIM_RESP_MAX:
+                raise ValueError("byte_limit %d over packets of >= %d bytes allows %d packets per response; the "
+                                 "simulator's responses hold %d" % (cfg.byte_limit, int(lens.min()), most,
+                                                                     _native.SIM_RESP_MAX))
         G = _native.BLOB_GUARD
         full = bytearray(G) + bytearray(blob) + bytearray(G)
         self.ublob_t = torch.frombuffer(full, dtype=torch.uint8).to(device)
@@ -88,6 +98,7 @@ class GpuEngine(object):
         torch.cuda.current_stream(device).synchronize()  # the uploads above ran on torch's stream
         self._bufs = {}
         self._matrix = {}
+        self._tested_base = self._tested_ctx()
 
     def buffer(self, name, nbytes):
         """The engine's grow-only device buffer `name`, at least nbytes long (a view of exactly nbytes)."""
@@ -143,9 +154,17 @@ class GpuEngine(object):
                                                buf.data_ptr(), offs, len(offsets), None))
         return buf, None
 
-    def tested_total(self):
-        """(claim, packet) pairs tested since the ctx's timing counters were last reset."""
+    def _tested_ctx(self):
         return int(self.ctx.work(_native.TIME_SIM_RESPOND)["useful_pairs"])
+
+    def tested_total(self):
+        """(claim, packet) pairs tested since this engine was built -- or since the ctx's counters were last reset
+        (dsy_ctx_reset_timing), whichever is later.  The counter is the ctx's: give each engine its own ctx when
+        several run at once."""
+        now = self._tested_ctx()
+        if now < self._tested_base:  # the ctx's counters were reset since
+            self._tested_base = 0
+        return now - self._tested_base
 
     def merge(self, resps, n):
         _native.check(self.lib.dsy_sim_merge(self.ctx.handle, ctypes.byref(self.cfg), self.bits.data_ptr(),

@@ -182,6 +182,10 @@ class SyncStore(object):
         community = ? AND member = ? AND global_time = ?` (community.py:3479-3480)."""
         if self.member is None:
             raise ValueError("rows_of_keys needs the store's member column")
+        if self.communities is not None and len(self.communities) > 1:
+            raise ValueError("rows_of_keys: the store spans communities %s; the (member, global_time) key is unique "
+                             "only within one community (UNIQUE(community, member, global_time))"
+                             % sorted(self.communities))
         if self._keys is None:
             keep = np.flatnonzero(~self.deleted)
             self._keys = dict(zip(zip(self.member[keep].tolist(), self.global_time[keep].tolist()), keep.tolist()))
@@ -327,11 +331,9 @@ class SyncStore(object):
         k = int(np.searchsorted(self.global_time[seg], np.uint64(max_global_time), side="right")) if len(seg) else 0
         gone = np.flatnonzero((self.meta == m) & (self.undone != 0) & ~self.deleted &
                               (self.global_time <= np.uint64(max_global_time)))
+        # the device first: a refused call (e.g. DSY_EINVAL while responder batches are in flight) leaves the host
+        # bookkeeping untouched, so host and device never drift apart
         if k:
-            self._mark_deleted(seg[:k])
-            self._live[m] = seg[k:]
-            self._nlive[m] -= k
-            self._ops.append(("prune", m, int(max_global_time), self.n))
             if self._handle is not None:
                 out = ctypes.c_uint64()
                 _native.check(self.ctx.lib.dsy_store_prune(self.ctx.handle, self._handle, m, int(max_global_time),
@@ -339,14 +341,18 @@ class SyncStore(object):
                 if out.value != k:
                     raise RuntimeError("device and host stores disagree: the device pruned %d rows, the host %d"
                                        % (out.value, k))
+            self._mark_deleted(seg[:k])
+            self._live[m] = seg[k:]
+            self._nlive[m] -= k
+            self._ops.append(("prune", m, int(max_global_time), self.n))
         if len(gone):  # undone rows are outside the index: only their duplicate-table slots go
-            self._mark_deleted(gone)
-            self._ops.append(("delete", gone, self.n))
             if self._handle is not None:
                 out = ctypes.c_uint64()
                 rws = gone.astype(np.uint64)
                 _native.check(self.ctx.lib.dsy_store_delete(self.ctx.handle, self._handle, rws.ctypes.data, len(rws),
                                                             ctypes.byref(out)))
+            self._mark_deleted(gone)
+            self._ops.append(("delete", gone, self.n))
         return k + len(gone)
 
     def delete_rows(self, rows):
@@ -362,14 +368,7 @@ class SyncStore(object):
         if not len(rows):
             return 0
         live = rows[self.undone[rows] == 0]
-        for m in np.unique(self.meta[live]).tolist():
-            seg = self.live_rows(m)
-            drop = live[self.meta[live] == m]
-            self._live[m] = seg[~np.isin(seg, drop, assume_unique=True)]
-            self._nlive[m] -= len(drop)
-        self._mark_deleted(rows)
-        self._ops.append(("delete", rows, self.n))
-        if self._handle is not None:
+        if self._handle is not None:  # the device first (see prune)
             out = ctypes.c_uint64()
             rws = rows.astype(np.uint64)  # keep the array alive across the call
             _native.check(self.ctx.lib.dsy_store_delete(self.ctx.handle, self._handle, rws.ctypes.data, len(rws),
@@ -377,6 +376,13 @@ class SyncStore(object):
             if out.value != len(live):
                 raise RuntimeError("device and host stores disagree: the device removed %d index entries, the host "
                                    "counts %d live rows" % (out.value, len(live)))
+        for m in np.unique(self.meta[live]).tolist():
+            seg = self.live_rows(m)
+            drop = live[self.meta[live] == m]
+            self._live[m] = seg[~np.isin(seg, drop, assume_unique=True)]
+            self._nlive[m] -= len(drop)
+        self._mark_deleted(rows)
+        self._ops.append(("delete", rows, self.n))
         return len(rows)
 
     # ------------------------------------------------------------------------------------------ undo / redo
@@ -401,6 +407,8 @@ class SyncStore(object):
         cur = self.undone[rows]
         undo = np.sort(rows[(cur == 0) & (vals != 0)])
         redo = np.sort(rows[(cur != 0) & (vals == 0)])
+        if self._handle is not None:  # the device first (see prune)
+            self._set_undone_device(undo, redo)
         self._buf["undone"][rows] = vals
         for m in np.unique(self.meta[undo]).tolist():
             seg = self.live_rows(m)
@@ -411,8 +419,6 @@ class SyncStore(object):
             seg = np.concatenate([self.live_rows(m), redo[self.meta[redo] == m]])
             self._live[m] = seg[np.lexsort((seg, self.global_time[seg]))]
             self._nlive[m] = self._nlive.get(m, 0) + int((self.meta[redo] == m).sum())
-        if self._handle is not None:
-            self._set_undone_device(undo, redo)
         return len(undo) + len(redo)
 
     def _set_undone_device(self, undo, redo):

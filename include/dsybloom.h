@@ -39,6 +39,7 @@ extern "C" {
 #define DSY_ECAPACITY -4 /* output capacity too small; the required size is returned through the count pointer */
 #define DSY_EUNSORTED -5 /* store rows are not in (meta, global_time) order */
 #define DSY_EEMPTY -6    /* the reference raises IndexError: a claim range over no rows (community.py:857) */
+#define DSY_EINTERNAL -7 /* a device-side bounds check tripped (an internal invariant broke): the call's results are void */
 
 /* hash families, selected exactly as bloomfilter.py:134-156 does from (m, k) */
 #define DSY_MD5 0
@@ -288,7 +289,8 @@ int dsy_sync_respond_dev(dsy_ctx* ctx, const dsy_store* store, const dsy_request
  * batches are in flight per ctx, each with its own workspace; they run back to back on the ctx stream, so the GPU
  * goes from one batch's packing straight into the next one's selection while the host stages batches and collects
  * results.  Results are the same as the synchronous call's; a batch's
- * output buffers stay valid until its slot is reused by a later submit (after two more submits at the earliest).
+ * output buffers stay valid until its slot is reused: submit takes the least recently used free slot, so two more
+ * submits at the earliest -- or any synchronous responder call (dsy_sync_respond / _dev always run in slot 0).
  * While a batch is in flight the store must not change (append, prune, delete, replace and free return DSY_EINVAL)
  * and the synchronous responder calls return DSY_EINVAL; d_filters must stay valid until wait returns.  A fourth
  * submit returns DSY_EINVAL. */

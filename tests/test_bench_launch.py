@@ -45,6 +45,35 @@ def test_world_mismatch_is_refused():
     assert "--gpus 4" in r.stderr
 
 
+def test_tail_keys_close_the_line():
+    """The gossip rounds/s (BASELINE's second metric) and each leg's headline number are the LAST keys of the JSON
+    line, read from the legs' nested records (shapes of a real run: profiles/bench_r3_n1_v4.json), so a driver that
+    stores only the tail of stdout still holds them."""
+    sys.path.insert(0, ROOT)
+    import bench
+    with open(os.path.join(ROOT, "profiles", "bench_r3_n1_v4.json")) as f:
+        rec = json.load(f)
+    rec = rec.get("parsed", rec)
+    line = {"metric": "x", "value": 1.0, "gossip_sim": rec["gossip_sim"]}
+    tail = bench.tail_keys(rec["gossip_sim"], rec["sha1_respond"], rec["heavy_tail"], rec["single_filter"],
+                           rec["large_filter"])
+    line.update(tail)
+    text = json.dumps(line)
+    keys = list(line)
+    assert keys[-len(tail):] == list(tail)
+    for k in ("gossip_rounds_per_s", "gossip_ms_per_round", "gossip_store_checksum", "gossip_n_gpus"):
+        assert k in tail and tail[k] is not None, k
+        assert '"%s"' % k in text[-600:], k
+    assert tail["gossip_rounds_per_s"] == rec["gossip_sim"]["value"]
+    assert tail["gossip_store_checksum"] == rec["gossip_sim"]["store_checksum"]
+    assert tail["sha1_respond_int32_frac"] == rec["sha1_respond"]["roofline"]["frac"]
+    assert tail["cfg5_ms_per_step"] == rec["heavy_tail"]["ms_per_step"]
+    assert tail["cfg1_sha1_int32_frac"] == rec["single_filter"]["sha1"]["roofline_test"]["valu_int32"]["frac"]
+    assert set(tail["cfg4_sha256_add_int32_frac"]) == {"2^20", "2^22", "2^24"}
+    # legs that did not run leave None, never a KeyError
+    assert set(bench.tail_keys(None).values()) == {None}
+
+
 def test_cpu_pool_runs_closures_over_shared_arrays():
     sys.path.insert(0, ROOT)
     import bench

@@ -54,3 +54,16 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_native.BloomParams) == 8 + 4 * 4 + 256
     assert ctypes.sizeof(_native.Request) == 8 * 2 + 4 * 2 + 8 * 2 + 4 * 4 + 256
     assert ctypes.sizeof(_native.Meta) == 24
+
+
+def test_constants_match_header():
+    text = open(HEADER).read()
+    defs = dict(re.findall(r"^#define\s+(DSY_\w+)\s+(\d+)\b", text, flags=re.M))
+    assert int(defs["DSY_BLOB_GUARD"]) == _native.BLOB_GUARD
+    assert int(defs["DSY_SIM_RESP_MAX"]) == _native.SIM_RESP_MAX
+
+
+def test_status_codes_match_header():
+    defs = dict(re.findall(r"^#define\s+(DSY_E\w+|DSY_OK)\s+(-?\d+)\b", open(HEADER).read(), flags=re.M))
+    for name, val in defs.items():
+        assert getattr(_native, name) == int(val), name
