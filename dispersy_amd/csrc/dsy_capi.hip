@@ -2169,6 +2169,33 @@ static int job_finish(dsy_ctx* c, RespondSlot& sl, uint64_t** d_packed, uint64_t
         fprintf(stderr, "host_profile R=%u stage=%.1f enqueue=%.1f wait=%.1f total=%.1f\n", jb.R, jb.hp[1] - jb.hp[0],
                 jb.hp[2] ? jb.hp[2] - jb.hp[1] : 0.0, jb.hp_wait, jb.hp[3] - jb.hp[0]);
     }
+    // DSY_BULK_AUDIT (diagnostic): the split windows' sort state must be zero once a call's windows are done
+    // (k_compact clears what each window used); one stderr line per call that leaves counts behind
+    static const bool bulk_audit = getenv("DSY_BULK_AUDIT") != nullptr;
+    if (bulk_audit && jb.R) {
+        const size_t n = (size_t)jb.R * 1024;
+        std::vector<uint32_t> h(2 * n);
+        HIP_TRY(hipMemcpyAsync(h.data(), L.bulk_hist, n * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(h.data() + n, L.bulk_cur, n * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        std::string msg;
+        size_t dirty = 0;
+        for (size_t part = 0; part < 2; ++part)
+            for (uint32_t a = 0; a < jb.R; ++a) {
+                uint64_t sum = 0, nz = 0;
+                for (uint32_t i = 0; i < 1024; ++i) {
+                    sum += h[part * n + (size_t)a * 1024 + i];
+                    nz += h[part * n + (size_t)a * 1024 + i] != 0;
+                }
+                if (!nz) continue;
+                if (++dirty <= 16)
+                    msg += std::string(part ? " cur" : " hist") + "[" + std::to_string(a) + "]=" + std::to_string(sum) +
+                           "/" + std::to_string(nz);
+            }
+        if (dirty)
+            fprintf(stderr, "bulk_audit R=%u J=%u W_last=%llu dirty_rows=%zu:%s\n", jb.R, jb.J,
+                    (unsigned long long)L.window, dirty, msg.c_str());
+    }
     return DSY_OK;
 }
 
