@@ -102,6 +102,10 @@ class BloomFilter(object):
         self._m_size, self._k_functions, self._prefix = m_size, k_functions, prefix
         self._hash_name, self._chunk = hash_family(m_size, k_functions)
         self._raw = bytearray(raw) if raw is not None else bytearray(m_size // 8)
+        # the filter bytes' address, for dsy_sync_respond_gather: the ctypes view exports the bytearray's buffer, so
+        # it can never be reallocated under the address (every update is an equal-length slice assignment)
+        self._view = (ctypes.c_char * len(self._raw)).from_buffer(self._raw)
+        self._addr = ctypes.addressof(self._view)
         self._params = None
         self._record = None
 

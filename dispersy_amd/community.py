@@ -37,6 +37,7 @@ _RANGE_OF = operator.itemgetter(0, 1, 2, 3)  # a ClaimRequest's (time_low, time_
 _BLOOM_OF = operator.itemgetter(4)
 _RECORD_OF = operator.attrgetter("request_record")
 _RAW_OF = operator.attrgetter("_raw")
+_ADDR_OF = operator.attrgetter("_addr")
 
 # the sync part of an introduction-request payload (payload.py:31-153): time_high == 0 means "up to the
 # responder's global time"
@@ -711,22 +712,25 @@ class SyncCommunity(object):
     def respond(self, requests, include_inactive=False, byte_limit=None, random_seed=None):
         """Batched responder (community.py:2531-2572): for each ClaimRequest (time_high already resolved), the store
         rows the reference would send, in send order.  One call into the HIP library for the whole batch."""
-        reqs, R, blob = self.request_records(requests)
-        return self._respond_requests(reqs, R, blob, include_inactive, byte_limit, random_seed)
+        reqs, R, bfs = self._request_table(requests)
+        # the filters stay where the BloomFilters hold them: the library gathers them into pinned staging itself
+        # (dsy_sync_respond_gather writes each record's filter_offset)
+        ptrs = np.fromiter(map(_ADDR_OF, bfs), dtype=np.uint64, count=R) if R else np.zeros(1, dtype=np.uint64)
+        return self._respond_requests(reqs, R, None, include_inactive, byte_limit, random_seed, ptrs)
 
     @staticmethod
-    def request_records(requests):
-        """(dsy_request records, R, packed filters) of a list of ClaimRequests, as the C-ABI takes them: the filters'
-        static record parts (BloomFilter.request_record) joined into the record array in one pass, the claims'
-        (time_low, time_high, modulo, offset) filled as columns, time bounds clamped to 2^63-1 (community.py:2545-2548);
-        each filter sits 4-byte aligned in the blob at its record's filter_offset."""
+    def _request_table(requests):
+        """(dsy_request records with filter_offset unset, R, the claims' BloomFilters): the filters' static record
+        parts (BloomFilter.request_record) joined into the record array in one pass, the claims' (time_low, time_high,
+        modulo, offset) filled as columns, time bounds clamped to 2^63-1 (community.py:2545-2548)."""
         R = len(requests)
         if not R:
-            return np.zeros(1, dtype=_REQUEST_DTYPE), 0, b""
+            return np.zeros(1, dtype=_REQUEST_DTYPE), 0, []
         bfs = list(map(_BLOOM_OF, requests))
         reqs = np.frombuffer(bytearray(b"".join(map(_RECORD_OF, bfs))), dtype=_REQUEST_DTYPE)
-        try:
-            t = np.fromiter(map(_RANGE_OF, requests), dtype=_RANGE_DTYPE, count=R)
+        try:  # a flat uint64 fromiter: the structured-dtype one builds a tuple per claim
+            t = np.fromiter(itertools.chain.from_iterable(map(_RANGE_OF, requests)), dtype=np.uint64,
+                            count=4 * R).view(_RANGE_DTYPE)
         except OverflowError:  # a bound past 2^64: clamp in Python first
             t = np.fromiter(((min(q.time_low, MAX_GT), min(q.time_high, MAX_GT), q.modulo, q.offset) for q in requests),
                             dtype=_RANGE_DTYPE, count=R)
@@ -734,6 +738,15 @@ class SyncCommunity(object):
         reqs["time_high"] = np.minimum(t["time_high"], np.uint64(MAX_GT))
         reqs["modulo"] = t["modulo"]
         reqs["offset"] = t["offset"]
+        return reqs, R, bfs
+
+    @staticmethod
+    def request_records(requests):
+        """(dsy_request records, R, packed filters) of a list of ClaimRequests, as dsy_sync_respond takes them
+        (_request_table's records); each filter sits 4-byte aligned in the blob at its record's filter_offset."""
+        reqs, R, bfs = SyncCommunity._request_table(requests)
+        if not R:
+            return reqs, 0, b""
         raws = list(map(_RAW_OF, bfs))
         if len(set(map(len, raws))) == 1:
             # one filter size (the MTU claim): the padding is the join's separator (an empty last item adds the
@@ -784,8 +797,9 @@ class SyncCommunity(object):
             out[int(i)] = r
         return out
 
-    def _respond_requests(self, reqs, R, blob, include_inactive, byte_limit, random_seed):
-        """One dsy_sync_respond call for R dsy_request records whose filters sit in `blob`."""
+    def _respond_requests(self, reqs, R, blob, include_inactive, byte_limit, random_seed, ptrs=None):
+        """One dsy_sync_respond call for R dsy_request records whose filters sit in `blob` -- or, with `ptrs` (the
+        filters' addresses), one dsy_sync_respond_gather call."""
         byte_limit = self.dispersy_sync_response_limit if byte_limit is None else byte_limit
         seed = self._random.getrandbits(64) if random_seed is None else random_seed
         st = self._store
@@ -795,10 +809,15 @@ class SyncCommunity(object):
         cap = 1 << 16
         while True:
             out = np.empty(cap, dtype=np.uint64)
-            rc = ctx.lib.dsy_sync_respond(ctx.handle, st.handle, reqs.ctypes.data_as(ctypes.POINTER(_native.Request)),
-                                          R, blob, len(blob), mt, n_metas,
-                                          self.global_time, 1 if include_inactive else 0, int(byte_limit), seed,
-                                          out.ctypes.data, cap, out_off.ctypes.data)
+            if ptrs is None:
+                rc = ctx.lib.dsy_sync_respond(ctx.handle, st.handle,
+                                              reqs.ctypes.data_as(ctypes.POINTER(_native.Request)), R, blob, len(blob),
+                                              mt, n_metas, self.global_time, 1 if include_inactive else 0,
+                                              int(byte_limit), seed, out.ctypes.data, cap, out_off.ctypes.data)
+            else:
+                rc = ctx.lib.dsy_sync_respond_gather(ctx.handle, st.handle, reqs.ctypes.data, R, ptrs.ctypes.data, mt,
+                                                     n_metas, self.global_time, 1 if include_inactive else 0,
+                                                     int(byte_limit), seed, out.ctypes.data, cap, out_off.ctypes.data)
             if rc == _native.DSY_ECAPACITY and int(out_off[R]) > cap:
                 cap = int(out_off[R])
                 continue

@@ -2214,6 +2214,11 @@ static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs,
     return job_finish(c, sl, d_packed, d_packed_off, total_pairs);
 }
 
+static int respond_to_host(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, uint32_t R, const void* d_f,
+                           uint64_t filters_len, const dsy_meta* metas, uint32_t nmeta, uint64_t responder_global_time,
+                           int include_inactive, int64_t byte_limit, uint64_t random_seed, uint64_t* out_idx,
+                           uint64_t out_cap, uint64_t* out_req_offsets);
+
 int dsy_sync_respond(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, uint32_t R, const uint8_t* filters,
                      uint64_t filters_len, const dsy_meta* metas, uint32_t nmeta, uint64_t responder_global_time,
                      int include_inactive, int64_t byte_limit, uint64_t random_seed, uint64_t* out_idx,
@@ -2226,6 +2231,16 @@ int dsy_sync_respond(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, ui
     if ((rc = ws_get(c, "filters", filters_len + 64, &d_f))) return rc;
     if (filters_len) HIP_TRY(hipMemcpyAsync(d_f, filters, filters_len, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemsetAsync((uint8_t*)d_f + filters_len, 0, 64, c->stream));
+    return respond_to_host(c, s, reqs, R, d_f, filters_len, metas, nmeta, responder_global_time, include_inactive,
+                           byte_limit, random_seed, out_idx, out_cap, out_req_offsets);
+}
+
+// dsy_sync_respond's device step and result download, the filters already in the "filters" workspace
+static int respond_to_host(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, uint32_t R, const void* d_f,
+                           uint64_t filters_len, const dsy_meta* metas, uint32_t nmeta, uint64_t responder_global_time,
+                           int include_inactive, int64_t byte_limit, uint64_t random_seed, uint64_t* out_idx,
+                           uint64_t out_cap, uint64_t* out_req_offsets) {
+    int rc;
     uint64_t *d_packed, *d_off, pairs;
     if ((rc = respond_core(c, s, reqs, R, (const uint8_t*)d_f, filters_len + 64, metas, nmeta, responder_global_time,
                            include_inactive, byte_limit, random_seed, &d_packed, &d_off, &pairs)))
@@ -2237,6 +2252,39 @@ int dsy_sync_respond(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, ui
     if (total) HIP_TRY(hipMemcpyAsync(out_idx, d_packed, total * 8, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return DSY_OK;
+}
+
+int dsy_sync_respond_gather(dsy_ctx* c, const dsy_store* s, dsy_request* reqs, uint32_t R,
+                            const uint8_t* const* filters, const dsy_meta* metas, uint32_t nmeta,
+                            uint64_t responder_global_time, int include_inactive, int64_t byte_limit,
+                            uint64_t random_seed, uint64_t* out_idx, uint64_t out_cap, uint64_t* out_req_offsets) {
+    if (!c || !s || (R && (!reqs || !filters)) || (nmeta && !metas) || !out_req_offsets)
+        return fail(DSY_EINVAL, "NULL argument");
+    Guard g(c);
+    uint64_t total = 0;
+    for (uint32_t r = 0; r < R; ++r) {
+        if (!filters[r]) return fail(DSY_EINVAL, "claim %u: NULL filter", r);
+        if (reqs[r].m_bits == 0 || reqs[r].m_bits % 8) return fail(DSY_EINVAL, "claim %u: m_bits %llu is not a positive multiple of 8", r, (unsigned long long)reqs[r].m_bits);
+        reqs[r].filter_offset = total;
+        total += (reqs[r].m_bits / 8 + 3) & ~uint64_t(3);
+    }
+    // one host pass gathers the filters into pinned staging (the upload is then a plain DMA, no pageable bounce);
+    // the previous call's upload from this staging finished at its closing stream sync
+    uint8_t* h;
+    void* d_f;
+    int rc;
+    if ((rc = stage_get(c->main, total + 64, &h))) return rc;
+    if ((rc = ws_get(c, "filters", total + 64, &d_f))) return rc;
+    for (uint32_t r = 0; r < R; ++r) {
+        const uint64_t n = reqs[r].m_bits / 8;
+        uint8_t* dst = h + reqs[r].filter_offset;
+        memcpy(dst, filters[r], n);
+        memset(dst + n, 0, ((n + 3) & ~uint64_t(3)) - n);
+    }
+    memset(h + total, 0, 64);
+    HIP_TRY(hipMemcpyAsync(d_f, h, total + 64, hipMemcpyHostToDevice, c->stream));
+    return respond_to_host(c, s, reqs, R, d_f, total, metas, nmeta, responder_global_time, include_inactive,
+                           byte_limit, random_seed, out_idx, out_cap, out_req_offsets);
 }
 
 int dsy_sync_respond_dev(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, uint32_t R,

@@ -272,6 +272,15 @@ int dsy_sync_respond(dsy_ctx* ctx, const dsy_store* store, const dsy_request* re
                      uint64_t responder_global_time, int include_inactive, int64_t byte_limit, uint64_t random_seed,
                      uint64_t* out_idx, uint64_t out_cap, uint64_t* out_req_offsets);
 
+/* Gather form of dsy_sync_respond, for a caller whose filters are separate objects (one BloomFilter per claim,
+ * community.py:2531-2545): filters[r] points at claim r's m_bits/8 filter bytes.  The library lays the filters out
+ * itself -- it WRITES reqs[r].filter_offset -- gathering them in one host pass into pinned staging, so the upload
+ * is one DMA and the caller builds no packed buffer.  Output and errors as dsy_sync_respond. */
+int dsy_sync_respond_gather(dsy_ctx* ctx, const dsy_store* store, dsy_request* reqs, uint32_t R,
+                            const uint8_t* const* filters, const dsy_meta* metas, uint32_t nmeta,
+                            uint64_t responder_global_time, int include_inactive, int64_t byte_limit,
+                            uint64_t random_seed, uint64_t* out_idx, uint64_t out_cap, uint64_t* out_req_offsets);
+
 /* Device form: reqs/metas stay host structs (uploaded into the ctx workspace), filters are device memory
  * (d_filters), results stay in device memory owned by the ctx until the next call:
  *   *d_out_idx   -> uint64 rows, claim r at [d_out_offsets[r], d_out_offsets[r+1])
