@@ -341,10 +341,24 @@ def run(args, rank, world, local):
         "other_kernels_ms_per_step": {"select": round(sel["ms"] / n_side, 3),
                                       "compact": round(cmp_["ms"] / n_side, 3)},
     }
+    # HBM traffic per launch from the committed PMC passes (tools/profile_round.sh -> profiles/pmc_traffic_<hash>.json),
+    # reported only when the kernel it measured is the one this run executes: the file carries the sha256 of the
+    # kernel's machine code in the library it profiled (tools/kernel_hash.py), compared with this library's
     traffic_file = os.path.join(ROOT, "profiles", "pmc_traffic_%s.json" % hash_name)
     if os.path.isfile(traffic_file):
+        from tools.kernel_hash import HEADLINE, kernel_sha
         with open(traffic_file) as f:
-            roofline["traffic"] = json.load(f).get("hbm_bytes_per_launch")
+            rec = json.load(f)
+        now = kernel_sha(_native.LIB_PATH if not os.environ.get("DSY_LIB_PATH") else os.environ["DSY_LIB_PATH"],
+                         HEADLINE) if hash_name == "md5" else None
+        if now is not None and rec.get("kernel_sha") == now:
+            roofline["traffic"] = rec.get("hbm_bytes_per_launch")
+            roofline["traffic_source"] = "profiles/pmc_traffic_%s.json (%s; same kernel code, sha256 %s)" % (
+                hash_name, rec.get("round"), now[:16])
+        else:
+            roofline["traffic_source"] = "not reported: profiles/pmc_traffic_%s.json measured another build of the " \
+                                         "kernel (sha256 %s, this run %s)" % (hash_name, str(rec.get("kernel_sha"))[:16],
+                                                                            str(now)[:16])
 
     # `work` was read right after the timed steps (reset before them)
     useful = work["useful_pairs"]
@@ -433,7 +447,7 @@ def run(args, rank, world, local):
             "dropin": dropin,
             "sha1_respond": sha1,
         }
-        line.update(tail_keys(gossip, sha1, heavy, single, large))
+        line.update(tail_keys(gossip, sha1, heavy, single, large, cpu))
         print(json.dumps(line))
     if store is not None:
         lib.dsy_store_free(store)
@@ -449,7 +463,14 @@ def _get(d, *path):
     return d
 
 
-def tail_keys(gossip, sha1=None, heavy=None, single=None, large=None):
+def _ok(chk):
+    """True / False for a gpu_vs_oracle record (None when the check did not run)."""
+    if not isinstance(chk, dict):
+        return None
+    return bool(chk.get("filter_bytes_equal")) and bool(chk.get("membership_equal"))
+
+
+def tail_keys(gossip, sha1=None, heavy=None, single=None, large=None, cpu=None):
     """Compact top-level keys printed LAST on the JSON line, so a driver that keeps only the tail of stdout still
     sees BASELINE's second metric (gossip sync rounds/s at N GPUs, config 3) and each leg's headline number.  The
     nested legs above hold the same values with their rooflines and CPU baselines."""
@@ -466,7 +487,20 @@ def tail_keys(gossip, sha1=None, heavy=None, single=None, large=None):
         "cfg1_sha1_int32_frac": _get(single, "sha1", "roofline_test", "valu_int32", "frac"),
         "cfg4_sha256_add_int32_frac": {k: v.get("add_valu_frac") for k, v in (_get(large, "filters") or {}).items()}
         or None,
+        "cfg1_at_capacity_md5_tests_per_s": _get(single, "md5", "at_capacity", "test_keys_per_s"),
     }
+    # every in-leg GPU == CPU-oracle check that ran (None: the leg or its check did not run)
+    checks = {
+        "cfg2_responder_sample": _get(cpu, "gpu_matches_cpu_on_sample"),
+        "sha1_responder_sample": _get(sha1, "cpu_baseline", "gpu_matches_cpu_on_sample"),
+        "cfg5_responder_sample": _get(heavy, "cpu_baseline", "gpu_matches_cpu_on_sample"),
+        "cfg1_md5": _ok(_get(single, "md5", "gpu_vs_oracle")),
+        "cfg1_sha1": _ok(_get(single, "sha1", "gpu_vs_oracle")),
+        "cfg1_md5_at_capacity": _ok(_get(single, "md5", "at_capacity", "gpu_vs_oracle")),
+        "cfg1_sha1_at_capacity": _ok(_get(single, "sha1", "at_capacity", "gpu_vs_oracle")),
+        "cfg4_2^20": _ok(_get(large, "gpu_vs_oracle_2^20")),
+    }
+    out["gpu_matches_oracle"] = {k: v for k, v in checks.items() if v is not None} or None
     return out
 
 
@@ -1092,6 +1126,34 @@ def _timed_bloom(ctx, fn, reps):
     return kt["ms"] / 1e3 / max(kt["launches"], 1), wall
 
 
+def bloom_vs_oracle(ctx, lib, bf, m, f, prefix, blob, add_off, n_add, test_off, n_test, dev):
+    """In-leg parity check of the single-filter kernels: a fresh filter built on the GPU from the n_add keys at
+    add_off, then n_test keys at test_off tested; the same through oracle/bloom_ref (hashlib, bloomfilter.py:160-197)
+    on host copies.  Filter bytes and every membership verdict must be equal."""
+    import torch
+    from oracle.bloom_ref import OracleBloom
+    filt = torch.zeros(int(lib.dsy_filter_words(m)), dtype=torch.int32, device=dev)
+    present = torch.empty(max(n_test, 1), dtype=torch.uint8, device=dev)
+    ctx.wait_torch(dev)
+    _native.check(lib.dsy_bloom_add_dev(ctx.handle, ctypes.byref(bf.params), blob.data_ptr(), add_off.data_ptr(), n_add,
+                                        filt.data_ptr()))
+    _native.check(lib.dsy_bloom_test_dev(ctx.handle, ctypes.byref(bf.params), blob.data_ptr(), test_off.data_ptr(),
+                                         n_test, filt.data_ptr(), present.data_ptr()))
+    ctx.synchronize()
+    got_bytes = filt.cpu().numpy().view(np.uint8)[:m // 8].tobytes()
+    got = present[:n_test].cpu().numpy()
+    ob = OracleBloom.from_m_f(m, f, prefix)
+    def keys(off, n):  # the n keys at off as bytes (one host copy of just their span)
+        o = off[:n + 1].cpu().numpy()
+        lo = int(o[0])
+        host = blob[lo:int(o[-1])].cpu().numpy().tobytes()
+        return [host[int(o[i]) - lo:int(o[i + 1]) - lo] for i in range(n)]
+    ob.add_keys(keys(add_off, n_add))
+    want = np.fromiter((k in ob for k in keys(test_off, n_test)), dtype=np.uint8, count=n_test)
+    return {"adds": n_add, "tests": n_test, "filter_bytes_equal": got_bytes == ob.to_bytes(),
+            "membership_equal": bool(np.array_equal(got, want)), "present_fraction": round(float(got.mean()), 4)}
+
+
 def single_filter(args, ctx, lib, blob, offsets, N, dev, rank, world):
     """BASELINE config 1 at GPU scale: BloomFilter(10160, 0.01, 4-byte prefix) (MD5, k=7) and the reference's test
     filter BloomFilter(4096, 0.001, b"x") (SHA-1, k=10, tests/debugcommunity/node.py:617): add 100 k packets, then
@@ -1131,6 +1193,31 @@ def single_filter(args, ctx, lib, blob, offsets, N, dev, rank, world):
                                              "unit": "Tops/s", "frac": round(ops / k_test / 1e12 / PEAK_INT32_TOPS, 4),
                                              "ops_per_block": OPS_PER_BLOCK[name]}},
         }
+        # the leg above fills the filter far past its capacity (every bit set): a GPU == oracle check of the same
+        # kernels on 20 k adds and 50 k tests, then SURVEY §8(d) row 1's at-capacity variant -- get_capacity(f) adds
+        # (1059 for the MTU filter), 1 M tests, false positives ~f -- timed and checked against the oracle in full
+        out[name]["gpu_vs_oracle"] = bloom_vs_oracle(ctx, lib, bf, m, f, prefix, blob, offsets, 20_000, offsets,
+                                                     50_000, dev)
+        cap = bf.get_capacity(f)
+        n_t = min(1_000_000, N)
+        filt.zero_()
+        ctx.wait_torch(dev)
+        add_cap = lambda: _native.check(lib.dsy_bloom_add_dev(ctx.handle, ctypes.byref(bf.params), blob.data_ptr(),  # noqa: E731
+                                                              offsets.data_ptr(), cap, filt.data_ptr()))
+        test_cap = lambda: _native.check(lib.dsy_bloom_test_dev(ctx.handle, ctypes.byref(bf.params), blob.data_ptr(),  # noqa: E731
+                                                                offsets.data_ptr(), n_t, filt.data_ptr(),
+                                                                present.data_ptr()))
+        add_cap()
+        test_cap()
+        k_cap, wall_cap = _timed_bloom(ctx, test_cap, 5)
+        chk = bloom_vs_oracle(ctx, lib, bf, m, f, prefix, blob, offsets, cap, offsets, n_t, dev) \
+            if rank == 0 and world == 1 and args.cpu_claims > 0 else None
+        out[name]["at_capacity"] = {
+            "adds": cap, "tests": n_t, "test_keys_per_s": round(n_t / k_cap, 1),
+            "test_wall_keys_per_s": round(n_t / wall_cap, 1),
+            "present_fraction": round(float(present[:n_t].float().mean().item()), 4),
+            "expected_present_fraction": round(cap / n_t + f * (1 - cap / n_t), 4),
+            "avg_launch_us": round(k_cap * 1e6, 1), "gpu_vs_oracle": chk}
     if rank == 0 and world == 1:
         out["cpu_baseline"] = single_filter_cpu(blob, offsets)
     return out
@@ -1256,6 +1343,11 @@ def large_filter(args, ctx, lib, dev, rank, world, dist=None):
             "test_gblocks_per_s": round(test_blocks / k_test / 1e9, 2),
             "bits_set": ones, "present_fraction": round(float(present.float().mean().item()), 4),
         }
+    # the legs above saturate every filter (100 M keys): a GPU == oracle check of the HBM-resident-filter kernels at
+    # 2^20 on 20 k adds and 20 k tests (oracle/bloom_ref: hashlib SHA-256, 'L' chunks)
+    bf = BloomFilter(1 << 20, 0.01, b"\x07")
+    out["gpu_vs_oracle_2^20"] = bloom_vs_oracle(ctx, lib, bf, 1 << 20, 0.01, b"\x07", blob, offsets, 20_000, test_off,
+                                                20_000, dev)
     if rank == 0 and world == 1:
         out["cpu_baseline"] = large_filter_cpu(blob, offsets)
     del blob_full, blob, offsets, lengths

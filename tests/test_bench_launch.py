@@ -56,7 +56,7 @@ def test_tail_keys_close_the_line():
     rec = rec.get("parsed", rec)
     line = {"metric": "x", "value": 1.0, "gossip_sim": rec["gossip_sim"]}
     tail = bench.tail_keys(rec["gossip_sim"], rec["sha1_respond"], rec["heavy_tail"], rec["single_filter"],
-                           rec["large_filter"])
+                           rec["large_filter"], rec["cpu_baseline"])
     line.update(tail)
     text = json.dumps(line)
     keys = list(line)
@@ -70,6 +70,10 @@ def test_tail_keys_close_the_line():
     assert tail["cfg5_ms_per_step"] == rec["heavy_tail"]["ms_per_step"]
     assert tail["cfg1_sha1_int32_frac"] == rec["single_filter"]["sha1"]["roofline_test"]["valu_int32"]["frac"]
     assert set(tail["cfg4_sha256_add_int32_frac"]) == {"2^20", "2^22", "2^24"}
+    # the in-leg GPU == oracle checks of that run (round 3 had only the responder samples)
+    assert tail["gpu_matches_oracle"]["cfg2_responder_sample"] is True
+    assert tail["gpu_matches_oracle"]["sha1_responder_sample"] is True
+    assert tail["gpu_matches_oracle"]["cfg5_responder_sample"] is True
     # legs that did not run leave None, never a KeyError
     assert set(bench.tail_keys(None).values()) == {None}
 

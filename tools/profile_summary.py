@@ -51,7 +51,11 @@ def main():
     for k, cs in summary.items():
         if "k_pair_test" in k and "FETCH_SIZE" in cs:
             kind = "md5" if "Md5" in k else "sha1" if "Sha1" in k else "sha256" if "Sha256" in k else "sha512"
+            sys.path.insert(0, ROOT)
+            from tools.kernel_hash import HEADLINE, kernel_sha
+            lib = os.environ.get("DSY_LIB_PATH") or os.path.join(ROOT, "dispersy_amd", "libdsybloom.so")
             rec = {"kernel": k, "fetch_size_kib": cs["FETCH_SIZE"], "write_size_kib": cs.get("WRITE_SIZE"),
+                   "kernel_sha": kernel_sha(lib, HEADLINE) if kind == "md5" else None,
                    "hbm_bytes_per_launch": 2 * cs["FETCH_SIZE"] * 1024 + (cs.get("WRITE_SIZE") or 0) * 1024,
                    "correction": "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950: FETCH_SIZE counts half of a "
                                  "16 B/lane streaming read, MI355X_MICROARCH.md §HBM)",
