@@ -99,8 +99,8 @@ SIGNATURES = {
     "dsy_claim_largest": (ctypes.c_int, [_P, ctypes.POINTER(BloomParams), _P, _P, _U32, _U64, _U64, _U64, _U64, _P, _P]),
     "dsy_sync_respond": (ctypes.c_int, [_P, _P, ctypes.POINTER(Request), _U32, _P, _U64, ctypes.POINTER(Meta), _U32,
                                         _U64, ctypes.c_int, ctypes.c_int64, _U64, _P, _U64, _P]),
-    "dsy_sync_respond_gather": (ctypes.c_int, [_P, _P, _P, _U32, _P, ctypes.POINTER(Meta), _U32, _U64, ctypes.c_int,
-                                               ctypes.c_int64, _U64, _P, _U64, _P]),
+    "dsy_sync_respond_refs": (ctypes.c_int, [_P, _P, _P, _P, _U32, ctypes.POINTER(Meta), _U32, _U64, ctypes.c_int,
+                                             ctypes.c_int64, _U64, _P, _U64, _P]),
     "dsy_sync_respond_dev": (ctypes.c_int, [_P, _P, ctypes.POINTER(Request), _U32, _P, ctypes.POINTER(Meta), _U32,
                                             _U64, ctypes.c_int, ctypes.c_int64, _U64, ctypes.POINTER(_P),
                                             ctypes.POINTER(_P), _PU64]),

@@ -13,6 +13,7 @@ itself is kept as its serialised little-endian bytes (`.bytes`), which is the ex
 There is no CPU path for the digests: without the HIP library, add/test raise `NativeUnavailable`.
 """
 import ctypes
+import struct
 import logging
 from math import ceil, log
 
@@ -102,10 +103,17 @@ class BloomFilter(object):
         self._m_size, self._k_functions, self._prefix = m_size, k_functions, prefix
         self._hash_name, self._chunk = hash_family(m_size, k_functions)
         self._raw = bytearray(raw) if raw is not None else bytearray(m_size // 8)
-        # the filter bytes' address, for dsy_sync_respond_gather: the ctypes view exports the bytearray's buffer, so
+        # the filter bytes' address, for dsy_sync_respond_refs: the ctypes view exports the bytearray's buffer, so
         # it can never be reallocated under the address (every update is an equal-length slice assignment)
         self._view = (ctypes.c_char * len(self._raw)).from_buffer(self._raw)
         self._addr = ctypes.addressof(self._view)
+        # this filter's part of a dsy_request (m, k, hash family, prefix; range and filter offset unused) and the two
+        # addresses dsy_sync_respond_refs takes per claim, as 16 bytes: a batch's refs are one join
+        q = self._req = _native.Request()
+        q.m_bits, q.k, q.hash_kind, q.chunk_bytes = m_size, k_functions, _native.HASH_KINDS[self._hash_name], self._chunk
+        q.prefix_len = len(prefix)
+        ctypes.memmove(q.prefix, prefix, len(prefix))
+        self._refs = struct.pack("<QQ", ctypes.addressof(q), self._addr)
         self._params = None
         self._record = None
 
@@ -124,12 +132,7 @@ class BloomFilter(object):
         offset left zero), as bytes: built once -- the shape and prefix never change -- so a batch of claims is one
         join of records (SyncCommunity.request_records), not a field-by-field fill per claim."""
         if self._record is None:
-            q = _native.Request()
-            q.m_bits, q.k, q.hash_kind, q.chunk_bytes = (self._m_size, self._k_functions,
-                                                         _native.HASH_KINDS[self._hash_name], self._chunk)
-            q.prefix_len = len(self._prefix)
-            ctypes.memmove(q.prefix, self._prefix, len(self._prefix))
-            self._record = bytes(q)
+            self._record = bytes(self._req)
         return self._record
 
     @staticmethod

@@ -37,7 +37,10 @@ _RANGE_OF = operator.itemgetter(0, 1, 2, 3)  # a ClaimRequest's (time_low, time_
 _BLOOM_OF = operator.itemgetter(4)
 _RECORD_OF = operator.attrgetter("request_record")
 _RAW_OF = operator.attrgetter("_raw")
-_ADDR_OF = operator.attrgetter("_addr")
+_REFS_OF = operator.attrgetter("_refs")  # a BloomFilter's (record, filter bytes) addresses, 16 B
+_DIST_OF = operator.attrgetter("distribution")
+_GT_OF = operator.attrgetter("global_time")
+_PACKET_OF = operator.attrgetter("packet")
 
 # the sync part of an introduction-request payload (payload.py:31-153): time_high == 0 means "up to the
 # responder's global time"
@@ -462,29 +465,29 @@ class SyncCommunity(object):
         double_signed_sync table) is outside this path.  Returns the new store rows."""
         if not messages:
             return np.zeros(0, dtype=np.int64)
-        # one pass over the messages; what a meta needs (history, sequence numbers, its checks) is worked out once
-        # per meta object, and everything is checked before anything is stored, so a refused batch changes neither
-        # copy
+        # column by column (C-level getters over the list, no Python frame per message); what a meta needs (history,
+        # sequence numbers, its checks) is worked out once per meta object, and everything is checked before anything
+        # is stored, so a refused batch changes neither copy
+        n = len(messages)
         has_member = self._store.member is not None
+        meta_objs = list(map(getattr, messages, itertools.repeat("meta", n), itertools.repeat(None, n)))
         per_meta = {}
-        metas, gts, seqs, packets = [], [], [], []
-        members = [] if has_member else None
-        for m in messages:
-            meta = getattr(m, "meta", None)
-            info = per_meta.get(id(meta))
-            if info is None:
-                info = per_meta[id(meta)] = self._meta_store_info(meta)
-            dist = m.distribution
-            metas.append(m.database_id if hasattr(m, "database_id") else meta.database_id)
-            gts.append(dist.global_time)
-            seqs.append(dist.sequence_number if info[0] else 0)
-            packets.append(m.packet)
-            if has_member:
-                members.append(_member_id(m))
+        for meta in dict(zip(map(id, meta_objs), meta_objs)).values():
+            per_meta[id(meta)] = self._meta_store_info(meta)
+        dists = list(map(_DIST_OF, messages))
+        gts = np.fromiter(map(_GT_OF, dists), dtype=np.uint64, count=n)
+        packets = list(map(_PACKET_OF, messages))
+        metas = list(map(getattr, messages, itertools.repeat("database_id", n), itertools.repeat(None, n)))
+        if None in metas:  # messages that carry their meta's id on .meta only
+            metas = [d if d is not None else meta.database_id for d, meta in zip(metas, meta_objs)]
+        seqs = None
+        if any(info[0] for info in per_meta.values()):
+            seqs = [d.sequence_number if per_meta[id(meta)][0] else 0 for d, meta in zip(dists, meta_objs)]
+        members = list(map(_member_id, messages)) if has_member else None
         rows = self._store.append(packets, gts, metas, member=members, sequence=seqs)
         if any(h for _, h in per_meta.values()):
             self._last_sync_history(messages)
-        self.update_global_time(max(gts))
+        self.update_global_time(int(gts.max()))
         self.dispersy_store(messages)
         return rows
 
@@ -711,12 +714,21 @@ class SyncCommunity(object):
 
     def respond(self, requests, include_inactive=False, byte_limit=None, random_seed=None):
         """Batched responder (community.py:2531-2572): for each ClaimRequest (time_high already resolved), the store
-        rows the reference would send, in send order.  One call into the HIP library for the whole batch."""
-        reqs, R, bfs = self._request_table(requests)
-        # the filters stay where the BloomFilters hold them: the library gathers them into pinned staging itself
-        # (dsy_sync_respond_gather writes each record's filter_offset)
-        ptrs = np.fromiter(map(_ADDR_OF, bfs), dtype=np.uint64, count=R) if R else np.zeros(1, dtype=np.uint64)
-        return self._respond_requests(reqs, R, None, include_inactive, byte_limit, random_seed, ptrs)
+        rows the reference would send, in send order.  One call into the HIP library for the whole batch
+        (dsy_sync_respond_refs): per claim its four range fields and its BloomFilter's two addresses -- the library
+        reads the filter's shape and bytes where the BloomFilter keeps them."""
+        R = len(requests)
+        if not R:
+            return self._respond_requests(np.zeros(1, dtype=_REQUEST_DTYPE), 0, b"", include_inactive, byte_limit,
+                                          random_seed)
+        try:
+            ranges = np.fromiter(itertools.chain.from_iterable(map(_RANGE_OF, requests)), dtype=np.uint64, count=4 * R)
+        except OverflowError:  # a bound past 2^64: clamp in Python first (the library clamps to 2^63-1)
+            ranges = np.fromiter(itertools.chain.from_iterable((min(q.time_low, MAX_GT), min(q.time_high, MAX_GT),
+                                                                q.modulo, q.offset) for q in requests),
+                                 dtype=np.uint64, count=4 * R)
+        refs = b"".join(map(_REFS_OF, map(_BLOOM_OF, requests)))
+        return self._respond_requests(None, R, None, include_inactive, byte_limit, random_seed, (ranges, refs))
 
     @staticmethod
     def _request_table(requests):
@@ -797,9 +809,9 @@ class SyncCommunity(object):
             out[int(i)] = r
         return out
 
-    def _respond_requests(self, reqs, R, blob, include_inactive, byte_limit, random_seed, ptrs=None):
-        """One dsy_sync_respond call for R dsy_request records whose filters sit in `blob` -- or, with `ptrs` (the
-        filters' addresses), one dsy_sync_respond_gather call."""
+    def _respond_requests(self, reqs, R, blob, include_inactive, byte_limit, random_seed, refs=None):
+        """One dsy_sync_respond call for R dsy_request records whose filters sit in `blob` -- or, with `refs` (the
+        claims' ranges and (record, filter) addresses, SyncCommunity.respond), one dsy_sync_respond_refs call."""
         byte_limit = self.dispersy_sync_response_limit if byte_limit is None else byte_limit
         seed = self._random.getrandbits(64) if random_seed is None else random_seed
         st = self._store
@@ -809,15 +821,15 @@ class SyncCommunity(object):
         cap = 1 << 16
         while True:
             out = np.empty(cap, dtype=np.uint64)
-            if ptrs is None:
+            if refs is None:
                 rc = ctx.lib.dsy_sync_respond(ctx.handle, st.handle,
                                               reqs.ctypes.data_as(ctypes.POINTER(_native.Request)), R, blob, len(blob),
                                               mt, n_metas, self.global_time, 1 if include_inactive else 0,
                                               int(byte_limit), seed, out.ctypes.data, cap, out_off.ctypes.data)
             else:
-                rc = ctx.lib.dsy_sync_respond_gather(ctx.handle, st.handle, reqs.ctypes.data, R, ptrs.ctypes.data, mt,
-                                                     n_metas, self.global_time, 1 if include_inactive else 0,
-                                                     int(byte_limit), seed, out.ctypes.data, cap, out_off.ctypes.data)
+                rc = ctx.lib.dsy_sync_respond_refs(ctx.handle, st.handle, refs[0].ctypes.data, refs[1], R, mt, n_metas,
+                                                   self.global_time, 1 if include_inactive else 0, int(byte_limit),
+                                                   seed, out.ctypes.data, cap, out_off.ctypes.data)
             if rc == _native.DSY_ECAPACITY and int(out_off[R]) > cap:
                 cap = int(out_off[R])
                 continue

@@ -102,7 +102,18 @@ struct RespondJob {
 // each slot on streams of its own, and selection / compaction on high-priority streams beside a low-priority hashing
 // stream -- concurrent launches only slowed each other (a k_compact beside a hashing launch took 50-145 us instead of
 // 6, the hashing launch 280-355 us instead of 210).
+// dsy_sync_respond_refs: the claims' filters, copied into pinned staging and uploaded after the first window's
+// selection is enqueued (job_window), so the host gathers them while the GPU selects
+struct FilterGather {
+    const uint64_t* refs = nullptr;  // claim r's filter bytes at refs[2r + 1]
+    const uint64_t* foff = nullptr;  // and their place in the filters workspace
+    uint32_t R = 0;
+    uint64_t total = 0;              // bytes of the laid-out filters
+    uint8_t* d_dst = nullptr;        // the filters workspace
+};
+
 struct RespondSlot {
+    FilterGather gather;     // pending for the slot's next first window (dsy_sync_respond_refs), else empty
     Workspace w;
     hipEvent_t ev_done = nullptr;
     bool busy = false;       // submitted, not yet waited for
@@ -1771,6 +1782,20 @@ static int job_window(dsy_ctx* c, RespondSlot& sl) {
         HIP_TRY(launch_fill(L));
     jb.first_fill = false;
     timer_end(c, &t, st);
+    if (sl.gather.refs) {  // the claims' filters, gathered and uploaded while the selection runs
+        FilterGather& fg = sl.gather;
+        uint8_t* h;
+        if ((rc = stage_get(c->main, fg.total + 64, &h))) return rc;
+        for (uint32_t r = 0; r < fg.R; ++r) {
+            const uint64_t n = ((const dsy_request*)(uintptr_t)fg.refs[2 * (size_t)r])->m_bits / 8;
+            uint8_t* dst = h + fg.foff[r];
+            memcpy(dst, (const void*)(uintptr_t)fg.refs[2 * (size_t)r + 1], n);
+            memset(dst + n, 0, ((n + 3) & ~uint64_t(3)) - n);
+        }
+        memset(h + fg.total, 0, 64);
+        HIP_TRY(hipMemcpyAsync(fg.d_dst, h, fg.total + 64, hipMemcpyHostToDevice, st));
+        fg = FilterGather{};
+    }
     if (fill_profile) {  // per-window stderr line: k_fill phase durations over the workgroups (s_memtime ticks)
         std::vector<uint64_t> fc(n_act * 4);
         HIP_TRY(hipMemcpyAsync(fc.data(), d_fc, n_act * 32, hipMemcpyDeviceToHost, st));
@@ -1851,8 +1876,28 @@ static int job_window(dsy_ctx* c, RespondSlot& sl) {
     return DSY_OK;
 }
 
+// The claims of a responder call as job_start reads them: an array of dsy_request records, or (dsy_sync_respond_refs)
+// per claim its range (ranges[4r .. 4r+3]: time_low, time_high, modulo, offset) and the address of a record that
+// carries its filter's shape and prefix (refs[2r]), with the filter offsets the library laid out (foff).
+struct Claims {
+    const dsy_request* reqs = nullptr;
+    const uint64_t* ranges = nullptr;
+    const uint64_t* refs = nullptr;
+    const uint64_t* foff = nullptr;
+    const dsy_request& shape(uint32_t r) const {
+        return reqs ? reqs[r] : *(const dsy_request*)(uintptr_t)refs[2 * (size_t)r];
+    }
+    uint64_t field(uint32_t r, int i) const { return ranges[4 * (size_t)r + i]; }
+    uint64_t time_low(uint32_t r) const { return reqs ? reqs[r].time_low : std::min<uint64_t>(field(r, 0), kMaxGtHost); }
+    uint64_t time_high(uint32_t r) const { return reqs ? reqs[r].time_high : std::min<uint64_t>(field(r, 1), kMaxGtHost); }
+    uint64_t modulo(uint32_t r) const { return reqs ? reqs[r].modulo : field(r, 2); }
+    uint64_t offset(uint32_t r) const { return reqs ? reqs[r].offset : field(r, 3); }
+    uint64_t filter_offset(uint32_t r) const { return reqs ? reqs[r].filter_offset : foff[r]; }
+    static constexpr uint64_t kMaxGtHost = 0x7fffffffffffffffull;  // community.py:2545-2548
+};
+
 // Validate and stage a batch of claims into slot sl and enqueue its first window (no host wait).
-static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_request* reqs, uint32_t R,
+static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const Claims& cl, uint32_t R,
                      const uint8_t* d_filters, uint64_t filters_len, const dsy_meta* metas, uint32_t J,
                      uint64_t responder_gt, int include_inactive, int64_t byte_limit, uint64_t seed) {
     sl.job = RespondJob{};
@@ -1868,9 +1913,11 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
     uint32_t memo_k = 0, memo_chunk = 0;
     int32_t memo_kind = -1;
     for (uint32_t r = 0; r < R; ++r) {
-        const dsy_request& q = reqs[r];
-        if (q.modulo == 0 || q.offset >= q.modulo)
-            return fail(DSY_EINVAL, "claim %u: need 0 <= offset < modulo (offset=%u modulo=%u)", r, q.offset, q.modulo);
+        const dsy_request& q = cl.shape(r);
+        const uint64_t q_modulo = cl.modulo(r), q_offset = cl.offset(r);
+        if (q_modulo == 0 || q_offset >= q_modulo || q_modulo > 0xffffffffull)
+            return fail(DSY_EINVAL, "claim %u: need 0 <= offset < modulo < 2^32 (offset=%llu modulo=%llu)", r,
+                        (unsigned long long)q_offset, (unsigned long long)q_modulo);
         int32_t kind;
         uint32_t chunk;
         if (memo_kind >= 0 && q.m_bits == memo_m && q.k == memo_k) {
@@ -1883,8 +1930,9 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
         }
         if (kind != q.hash_kind || chunk != q.chunk_bytes) return fail(DSY_EINVAL, "claim %u: hash family mismatch", r);
         if (q.prefix_len > 255) return fail(DSY_EINVAL, "claim %u: prefix too long", r);
-        if (q.filter_offset % 4) return fail(DSY_EINVAL, "claim %u: filter_offset must be a multiple of 4", r);
-        if (filters_len && q.filter_offset + filter_words(q.m_bits) * 4 > filters_len)
+        const uint64_t q_foff = cl.filter_offset(r);
+        if (q_foff % 4) return fail(DSY_EINVAL, "claim %u: filter_offset must be a multiple of 4", r);
+        if (filters_len && q_foff + filter_words(q.m_bits) * 4 > filters_len)
             return fail(DSY_EINVAL, "claim %u: filter beyond the filters buffer", r);
         // prefixes of 1-4 bytes take the line-staged hashing; longer ones and the empty prefix the byte-wise path
         std::vector<uint32_t>& fm =
@@ -1906,7 +1954,7 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
     // and the overflow flag over the bus and the pack kernel folds the counters, so a window's status needs no
     // copy dispatch
     size_t prefix_b = 0;
-    for (uint32_t r = 0; r < R; ++r) prefix_b += reqs[r].prefix_len;
+    for (uint32_t r = 0; r < R; ++r) prefix_b += cl.shape(r).prefix_len;
     const size_t reqs_b = (size_t)R * sizeof(DevRequest), metas_b = (size_t)J * sizeof(SegMeta);
     const size_t in_b = (reqs_b + metas_b + (size_t)R * 8 + (prefix_b + 15) / 16 * 16 + 64 + 15) / 16 * 16;
     const size_t act_done_b = ((size_t)R + 15) / 16 * 16;
@@ -1959,14 +2007,14 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const dsy_
         const uint8_t* d_pre = (const uint8_t*)d_in + reqs_b + metas_b + (size_t)R * 8;
         size_t at = 0;
         for (uint32_t r = 0; r < R; ++r) {
-            const dsy_request& q = reqs[r];
+            const dsy_request& q = cl.shape(r);
             DevRequest d;
-            d.time_low = q.time_low;
-            d.time_high = q.time_high;
-            d.filter_offset = q.filter_offset;
+            d.time_low = cl.time_low(r);
+            d.time_high = cl.time_high(r);
+            d.filter_offset = cl.filter_offset(r);
             d.m_bits = q.m_bits;
-            d.modulo = q.modulo;
-            d.offset = q.offset;
+            d.modulo = (uint32_t)cl.modulo(r);
+            d.offset = (uint32_t)cl.offset(r);
             d.k = q.k;
             d.hash_kind = (uint32_t)q.hash_kind;
             d.chunk_bytes = q.chunk_bytes;
@@ -2201,23 +2249,38 @@ static int job_finish(dsy_ctx* c, RespondSlot& sl, uint64_t** d_packed, uint64_t
 
 static RespondSlot& sync_slot(dsy_ctx* c) { return c->rs[0]; }
 
-static int respond_core(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, uint32_t R, const uint8_t* d_filters,
+static int respond_core(dsy_ctx* c, const dsy_store* s, const Claims& cl, uint32_t R, const uint8_t* d_filters,
                         uint64_t filters_len, const dsy_meta* metas, uint32_t J, uint64_t responder_gt,
                         int include_inactive, int64_t byte_limit, uint64_t seed, uint64_t** d_packed,
                         uint64_t** d_packed_off, uint64_t* total_pairs) {
     if (c->inflight()) return fail(DSY_EINVAL, "submitted responder batches are in flight: dsy_sync_respond_wait them first");
     RespondSlot& sl = sync_slot(c);
     sl.last_use = ++c->use_clock;
-    int rc = job_start(c, sl, s, reqs, R, d_filters, filters_len, metas, J, responder_gt, include_inactive, byte_limit,
+    int rc = job_start(c, sl, s, cl, R, d_filters, filters_len, metas, J, responder_gt, include_inactive, byte_limit,
                        seed);
     if (rc) return rc;
     return job_finish(c, sl, d_packed, d_packed_off, total_pairs);
 }
 
-static int respond_to_host(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, uint32_t R, const void* d_f,
+// the device step of a host-buffer call and its result download, the filters in the "filters" workspace (or, with
+// jb.gather set by the caller, gathered there behind the first window's selection)
+static int respond_to_host(dsy_ctx* c, const dsy_store* s, const Claims& cl, uint32_t R, const void* d_f,
                            uint64_t filters_len, const dsy_meta* metas, uint32_t nmeta, uint64_t responder_global_time,
                            int include_inactive, int64_t byte_limit, uint64_t random_seed, uint64_t* out_idx,
-                           uint64_t out_cap, uint64_t* out_req_offsets);
+                           uint64_t out_cap, uint64_t* out_req_offsets) {
+    int rc;
+    uint64_t *d_packed, *d_off, pairs;
+    if ((rc = respond_core(c, s, cl, R, (const uint8_t*)d_f, filters_len + 64, metas, nmeta, responder_global_time,
+                           include_inactive, byte_limit, random_seed, &d_packed, &d_off, &pairs)))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(out_req_offsets, d_off, ((size_t)R + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const uint64_t total = out_req_offsets[R];
+    if (total > out_cap) return fail(DSY_ECAPACITY, "out_cap %llu < %llu rows", (unsigned long long)out_cap, (unsigned long long)total);
+    if (total) HIP_TRY(hipMemcpyAsync(out_idx, d_packed, total * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return DSY_OK;
+}
 
 int dsy_sync_respond(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, uint32_t R, const uint8_t* filters,
                      uint64_t filters_len, const dsy_meta* metas, uint32_t nmeta, uint64_t responder_global_time,
@@ -2231,60 +2294,44 @@ int dsy_sync_respond(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, ui
     if ((rc = ws_get(c, "filters", filters_len + 64, &d_f))) return rc;
     if (filters_len) HIP_TRY(hipMemcpyAsync(d_f, filters, filters_len, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemsetAsync((uint8_t*)d_f + filters_len, 0, 64, c->stream));
-    return respond_to_host(c, s, reqs, R, d_f, filters_len, metas, nmeta, responder_global_time, include_inactive,
+    Claims cl;
+    cl.reqs = reqs;
+    return respond_to_host(c, s, cl, R, d_f, filters_len, metas, nmeta, responder_global_time, include_inactive,
                            byte_limit, random_seed, out_idx, out_cap, out_req_offsets);
 }
 
-// dsy_sync_respond's device step and result download, the filters already in the "filters" workspace
-static int respond_to_host(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, uint32_t R, const void* d_f,
-                           uint64_t filters_len, const dsy_meta* metas, uint32_t nmeta, uint64_t responder_global_time,
-                           int include_inactive, int64_t byte_limit, uint64_t random_seed, uint64_t* out_idx,
-                           uint64_t out_cap, uint64_t* out_req_offsets) {
-    int rc;
-    uint64_t *d_packed, *d_off, pairs;
-    if ((rc = respond_core(c, s, reqs, R, (const uint8_t*)d_f, filters_len + 64, metas, nmeta, responder_global_time,
-                           include_inactive, byte_limit, random_seed, &d_packed, &d_off, &pairs)))
-        return rc;
-    HIP_TRY(hipMemcpyAsync(out_req_offsets, d_off, ((size_t)R + 1) * 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    const uint64_t total = out_req_offsets[R];
-    if (total > out_cap) return fail(DSY_ECAPACITY, "out_cap %llu < %llu rows", (unsigned long long)out_cap, (unsigned long long)total);
-    if (total) HIP_TRY(hipMemcpyAsync(out_idx, d_packed, total * 8, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return DSY_OK;
-}
-
-int dsy_sync_respond_gather(dsy_ctx* c, const dsy_store* s, dsy_request* reqs, uint32_t R,
-                            const uint8_t* const* filters, const dsy_meta* metas, uint32_t nmeta,
-                            uint64_t responder_global_time, int include_inactive, int64_t byte_limit,
-                            uint64_t random_seed, uint64_t* out_idx, uint64_t out_cap, uint64_t* out_req_offsets) {
-    if (!c || !s || (R && (!reqs || !filters)) || (nmeta && !metas) || !out_req_offsets)
+int dsy_sync_respond_refs(dsy_ctx* c, const dsy_store* s, const uint64_t* ranges, const uint64_t* refs, uint32_t R,
+                          const dsy_meta* metas, uint32_t nmeta, uint64_t responder_global_time, int include_inactive,
+                          int64_t byte_limit, uint64_t random_seed, uint64_t* out_idx, uint64_t out_cap,
+                          uint64_t* out_req_offsets) {
+    if (!c || !s || (R && (!ranges || !refs)) || (nmeta && !metas) || !out_req_offsets)
         return fail(DSY_EINVAL, "NULL argument");
     Guard g(c);
+    // the library lays the filters out: claim r's at foff[r], 4-byte aligned
+    std::vector<uint64_t> foff(std::max<uint32_t>(R, 1));
     uint64_t total = 0;
     for (uint32_t r = 0; r < R; ++r) {
-        if (!filters[r]) return fail(DSY_EINVAL, "claim %u: NULL filter", r);
-        if (reqs[r].m_bits == 0 || reqs[r].m_bits % 8) return fail(DSY_EINVAL, "claim %u: m_bits %llu is not a positive multiple of 8", r, (unsigned long long)reqs[r].m_bits);
-        reqs[r].filter_offset = total;
-        total += (reqs[r].m_bits / 8 + 3) & ~uint64_t(3);
+        if (!refs[2 * (size_t)r] || !refs[2 * (size_t)r + 1]) return fail(DSY_EINVAL, "claim %u: NULL record or filter", r);
+        const uint64_t m = ((const dsy_request*)(uintptr_t)refs[2 * (size_t)r])->m_bits;
+        if (m == 0 || m % 8) return fail(DSY_EINVAL, "claim %u: m_bits %llu is not a positive multiple of 8", r, (unsigned long long)m);
+        foff[r] = total;
+        total += (m / 8 + 3) & ~uint64_t(3);
     }
-    // one host pass gathers the filters into pinned staging (the upload is then a plain DMA, no pageable bounce);
-    // the previous call's upload from this staging finished at its closing stream sync
-    uint8_t* h;
     void* d_f;
     int rc;
-    if ((rc = stage_get(c->main, total + 64, &h))) return rc;
     if ((rc = ws_get(c, "filters", total + 64, &d_f))) return rc;
-    for (uint32_t r = 0; r < R; ++r) {
-        const uint64_t n = reqs[r].m_bits / 8;
-        uint8_t* dst = h + reqs[r].filter_offset;
-        memcpy(dst, filters[r], n);
-        memset(dst + n, 0, ((n + 3) & ~uint64_t(3)) - n);
-    }
-    memset(h + total, 0, 64);
-    HIP_TRY(hipMemcpyAsync(d_f, h, total + 64, hipMemcpyHostToDevice, c->stream));
-    return respond_to_host(c, s, reqs, R, d_f, total, metas, nmeta, responder_global_time, include_inactive,
-                           byte_limit, random_seed, out_idx, out_cap, out_req_offsets);
+    Claims cl;
+    cl.ranges = ranges;
+    cl.refs = refs;
+    cl.foff = foff.data();
+    RespondSlot& sl = sync_slot(c);
+    // the filters are gathered into pinned staging and uploaded once the first window's selection is enqueued: the
+    // host copies them while the GPU selects (job_window, jb.gather)
+    sl.gather = FilterGather{refs, foff.data(), R, total, (uint8_t*)d_f};
+    rc = respond_to_host(c, s, cl, R, d_f, total, metas, nmeta, responder_global_time, include_inactive, byte_limit,
+                         random_seed, out_idx, out_cap, out_req_offsets);
+    sl.gather = FilterGather{};
+    return rc;
 }
 
 int dsy_sync_respond_dev(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs, uint32_t R,
@@ -2295,7 +2342,9 @@ int dsy_sync_respond_dev(dsy_ctx* c, const dsy_store* s, const dsy_request* reqs
     if (!c || !s || (R && (!reqs || !d_filters)) || (nmeta && !metas)) return fail(DSY_EINVAL, "NULL argument");
     Guard g(c);
     uint64_t *d_packed, *d_off, pairs = 0;
-    int rc = respond_core(c, s, reqs, R, d_filters, 0, metas, nmeta, responder_global_time, include_inactive,
+    Claims cl;
+    cl.reqs = reqs;
+    int rc = respond_core(c, s, cl, R, d_filters, 0, metas, nmeta, responder_global_time, include_inactive,
                           byte_limit, random_seed, &d_packed, &d_off, &pairs);
     if (rc) return rc;
     if (d_out_idx) *d_out_idx = d_packed;
@@ -2318,7 +2367,9 @@ int dsy_sync_respond_submit(dsy_ctx* c, const dsy_store* s, const dsy_request* r
     if (k < 0) return fail(DSY_EINVAL, "%d responder batches are in flight: dsy_sync_respond_wait one first", dsy_ctx::kSlots);
     RespondSlot& sl = c->rs[k];
     sl.last_use = ++c->use_clock;
-    int rc = job_start(c, sl, s, reqs, R, d_filters, 0, metas, nmeta, responder_global_time, include_inactive,
+    Claims cl;
+    cl.reqs = reqs;
+    int rc = job_start(c, sl, s, cl, R, d_filters, 0, metas, nmeta, responder_global_time, include_inactive,
                        byte_limit, random_seed);
     if (rc) {
         hipStreamSynchronize(c->stream);  // whatever was enqueued before the failure

@@ -23,6 +23,7 @@ asks for that meta's rows (live_rows).  Rows past the constructor's are therefor
 `live_rows` always is.  `dup_check` / `replace_packet` are the duplicate check of received packets and its UPDATE
 (dispersy.py:831-918); `prune` and `delete_rows` are the DELETEs.
 """
+import bisect
 import ctypes
 
 import numpy as np
@@ -89,6 +90,9 @@ class SyncStore(object):
         self._keys = None    # (member, global_time) -> row, built on first use (rows_of_keys)
         self._gpending = {}
         self._blob_base = 0  # offsets[] of the host blob's first byte (attach: earlier packets are device-only)
+        # packets appended later, one bytes object per batch (appending to one growing buffer copied it every batch:
+        # 8 MB per 10 k packets); _tail_at[i] = offsets[] of batch i's first byte
+        self._tail, self._tail_at = [], []
         self._owns_handle = True
 
     # ------------------------------------------------------------------------------------------ columns
@@ -155,10 +159,21 @@ class SyncStore(object):
             if p is not None:
                 return p
         off = self._buf["offsets"]
-        a, b = int(off[i]) - self._blob_base, int(off[i + 1]) - self._blob_base
+        a, b = int(off[i]), int(off[i + 1])
+        if self._tail and a >= self._tail_at[0]:
+            k = bisect.bisect_right(self._tail_at, a) - 1
+            return self._tail[k][a - self._tail_at[k]:b - self._tail_at[k]]
+        a, b = a - self._blob_base, b - self._blob_base
         if a < 0:
             raise KeyError("row %d's packet lives only on the device (SyncStore.attach)" % int(i))
         return bytes(self.blob[a:b])
+
+    def _host_blob(self):
+        """Every host-held packet byte in one buffer (the initial blob, then the appended batches)."""
+        if self._tail:
+            self.blob = bytes(self.blob) + b"".join(self._tail)
+            self._tail, self._tail_at = [], []
+        return self.blob
 
     def packets(self, rows):
         return [self.packet(int(i)) for i in rows]
@@ -290,11 +305,8 @@ class SyncStore(object):
             b["member"] = np.empty(0, dtype=np.uint64) if b["member"] is None else b["member"]
             b["member"] = _room(b["member"], n0, n0 + a)
             b["member"][n0:n0 + a] = mem
-        if isinstance(self.blob, np.ndarray):
-            self.blob = bytearray(self.blob.tobytes())
-        elif not isinstance(self.blob, bytearray):
-            self.blob = bytearray(self.blob)
-        self.blob += data
+        self._tail_at.append(int(b["offsets"][n0]))
+        self._tail.append(data)
         self.n = n0 + a
         self._top = int(ids[-1])
         if self._row_of_id is not None:
@@ -508,7 +520,8 @@ class SyncStore(object):
         """dsy_store* on the device (uploaded on first use)."""
         if self._handle is None:
             ctx = self.ctx
-            blob = self.blob if isinstance(self.blob, bytes) else bytes(self.blob)
+            blob = self._host_blob()
+            blob = blob if isinstance(blob, bytes) else bytes(blob)
             h = ctypes.c_void_p()
             n0 = self._n_sorted
             offsets = np.ascontiguousarray(self.offsets)

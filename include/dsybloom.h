@@ -272,14 +272,17 @@ int dsy_sync_respond(dsy_ctx* ctx, const dsy_store* store, const dsy_request* re
                      uint64_t responder_global_time, int include_inactive, int64_t byte_limit, uint64_t random_seed,
                      uint64_t* out_idx, uint64_t out_cap, uint64_t* out_req_offsets);
 
-/* Gather form of dsy_sync_respond, for a caller whose filters are separate objects (one BloomFilter per claim,
- * community.py:2531-2545): filters[r] points at claim r's m_bits/8 filter bytes.  The library lays the filters out
- * itself -- it WRITES reqs[r].filter_offset -- gathering them in one host pass into pinned staging, so the upload
- * is one DMA and the caller builds no packed buffer.  Output and errors as dsy_sync_respond. */
-int dsy_sync_respond_gather(dsy_ctx* ctx, const dsy_store* store, dsy_request* reqs, uint32_t R,
-                            const uint8_t* const* filters, const dsy_meta* metas, uint32_t nmeta,
-                            uint64_t responder_global_time, int include_inactive, int64_t byte_limit,
-                            uint64_t random_seed, uint64_t* out_idx, uint64_t out_cap, uint64_t* out_req_offsets);
+/* Object form of dsy_sync_respond, for a caller whose claims are separate objects (one BloomFilter per claim,
+ * community.py:2531-2553): claim r is ranges[4r .. 4r+3] = time_low, time_high, modulo, offset (the bounds clamped to
+ * 2^63-1 here) and refs[2r] = the address of a dsy_request that carries its filter's shape and prefix (m_bits, k,
+ * hash_kind, chunk_bytes, prefix_len, prefix; its range and filter_offset fields are ignored), refs[2r+1] = the
+ * address of its m_bits/8 filter bytes.  The library lays the filters out and gathers them into pinned staging while
+ * the GPU runs the first window's selection; the caller builds no record array and no packed buffer.  Output and
+ * errors as dsy_sync_respond.  Replaces community.py:2531-2572's per-request loop for SyncCommunity.respond. */
+int dsy_sync_respond_refs(dsy_ctx* ctx, const dsy_store* store, const uint64_t* ranges, const uint64_t* refs, uint32_t R,
+                          const dsy_meta* metas, uint32_t nmeta, uint64_t responder_global_time, int include_inactive,
+                          int64_t byte_limit, uint64_t random_seed, uint64_t* out_idx, uint64_t out_cap,
+                          uint64_t* out_req_offsets);
 
 /* Device form: reqs/metas stay host structs (uploaded into the ctx workspace), filters are device memory
  * (d_filters), results stay in device memory owned by the ctx until the next call:

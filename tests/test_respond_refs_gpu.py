@@ -1,8 +1,8 @@
-"""dsy_sync_respond_gather (the drop-in SyncCommunity.respond path: the library gathers each BloomFilter's bytes into
-pinned staging itself and writes the records' filter_offset) against dsy_sync_respond over a caller-packed blob and
-against the sqlite + hashlib oracle (oracle/sync_ref.respond_lists = community.py:2746-2811 + :2555-2567): filter
-sizes that are not a multiple of 4 bytes (10160 bits = 1270 bytes), mixed shapes in one batch, an empty batch, and
-the argument checks."""
+"""dsy_sync_respond_refs (the drop-in SyncCommunity.respond path: per claim its four range fields and its BloomFilter's
+(record, filter bytes) addresses; the library lays the filters out and gathers them into pinned staging while the GPU
+selects) against dsy_sync_respond over a caller-packed blob and against the sqlite + hashlib oracle
+(oracle/sync_ref.respond_lists = community.py:2746-2811 + :2555-2567): filter sizes that are not a multiple of 4 bytes
+(10160 bits = 1270 bytes), mixed shapes in one batch, an empty batch, and the argument checks."""
 import numpy as np
 import pytest
 
@@ -47,7 +47,7 @@ def test_gather_equals_blob_and_oracle(shapes):
     served_oracle = [dict(name=n, id=i, direction=d, priority=p, pruning=None) for n, i, d, p, _ in chosen]
     reqs, blooms = _claims(rows, gt_now, np.random.Generator(np.random.PCG64(5)), shapes, 40)
     for limit in (2048, 1 << 40):
-        got = com.respond(reqs, byte_limit=limit, random_seed=7)  # the gather path
+        got = com.respond(reqs, byte_limit=limit, random_seed=7)  # the refs path
         packed, R, blob = com.request_records(reqs)
         want_blob = com._respond_requests(packed, R, blob, False, limit, 7)  # a caller-packed blob
         for q, ob, g, b in zip(reqs, blooms, got, want_blob):
@@ -57,30 +57,35 @@ def test_gather_equals_blob_and_oracle(shapes):
             assert store.rowid[g].tolist() == want, (q.time_low, q.time_high, q.modulo, q.offset, limit)
 
 
-def test_gather_writes_offsets_and_checks_arguments():
+def test_refs_layout_and_argument_checks():
     rows, _ = build(12, 2_000, 9_000, False)
     store = SyncStore.from_rows(rows)
     com = SyncCommunity(store, [MetaMessage("a", 1, SyncDistribution("ASC", 128, None))], global_time=9_100)
     assert len(com.respond([])) == 0
-    reqs = [ClaimRequest(1, 9_000, 1, 0, BloomFilter(m, 0.01, b"")) for m in (10160, 4096, 10160)]
-    table, R, bfs = SyncCommunity._request_table(reqs)
-    ptrs = np.array([bf._addr for bf in bfs], dtype=np.uint64)
+    bfs = [BloomFilter(m, 0.01, b"") for m in (10160, 4096, 10160)]
+    R = len(bfs)
+    ranges = np.array([[1, 9_000, 1, 0]] * R, dtype=np.uint64)
+    refs = np.frombuffer(b"".join(bf._refs for bf in bfs), dtype=np.uint64).copy()
     ctx, lib = store.ctx, store.ctx.lib
     mt, nm = com.meta_records()
     out, off = np.empty(1 << 16, dtype=np.uint64), np.zeros(R + 1, dtype=np.uint64)
 
-    def call(tab, p):
-        return lib.dsy_sync_respond_gather(ctx.handle, store.handle, tab.ctypes.data, R, p.ctypes.data, mt, nm,
-                                           9_100, 0, 1 << 40, 1, out.ctypes.data, len(out), off.ctypes.data)
+    def call(rg, rf):
+        return lib.dsy_sync_respond_refs(ctx.handle, store.handle, rg.ctypes.data, rf.ctypes.data, R, mt, nm, 9_100, 0,
+                                         1 << 40, 1, out.ctypes.data, len(out), off.ctypes.data)
 
-    _native.check(call(table, ptrs))
-    assert table["filter_offset"].tolist() == [0, 1272, 1272 + 512]  # 4-byte aligned, in claim order
+    _native.check(call(ranges, refs))
     # every row of gt 1..9000 is missing from the empty filters: the whole meta comes back, three times
     n_rows = int(sum(1 for r in rows if r[2] == 1 and r[1] <= 9_000 and not r[3]))
     assert np.diff(off).tolist() == [n_rows] * 3
-    bad = ptrs.copy()
-    bad[1] = 0
-    assert call(table, bad) == _native.DSY_EINVAL
-    odd = table.copy()
-    odd["m_bits"][2] = 10161
-    assert call(odd, ptrs) == _native.DSY_EINVAL
+    # a bound past 2^63-1 is clamped, as the record form requires of its caller (community.py:2545-2548)
+    big = ranges.copy()
+    big[:, 1] = np.uint64(1 << 64) - np.uint64(1)
+    _native.check(call(big, refs))
+    assert np.diff(off).tolist() == [n_rows] * 3
+    bad = refs.copy()
+    bad[3] = 0  # claim 1's filter address
+    assert call(ranges, bad) == _native.DSY_EINVAL
+    odd = ranges.copy()
+    odd[2, 3] = 5  # offset >= modulo
+    assert call(odd, refs) == _native.DSY_EINVAL

@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round 4: drop-in path changes (dsy_sync_respond_refs, column-wise store_messages, chunked host blob) -- their GPU
+# tests, then the drop-in bench leg.  Each GPU step has its own limit; the first failure ends the call.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_respond_refs_gpu.py \
+    tests/test_ingest.py tests/test_sequence.py tests/test_undo.py tests/test_pipeline_gpu.py tests/test_sync_golden.py \
+    > gpurun_out/r4_dropin_tests.log 2>&1 &&
+DSY_HOST_PROFILE=1 timeout -k 10 400 python -u bench.py --extra dropin --cpu-claims 0 > gpurun_out/r4_dropin.json 2> gpurun_out/r4_dropin.err
