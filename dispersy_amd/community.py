@@ -461,8 +461,9 @@ class SyncCommunity(object):
         community's global time to the highest stored one, then dispersy_store(messages) updates the cached claim
         filter.  A message carries .packet, .distribution.global_time and its meta's database id (.database_id, or
         .meta.database_id); .meta.distribution selects the sequence/history handling.  As in the reference, the
-        caller has already dropped duplicates (dispersy.py:1496-1498).  Double-member authentication (the
-        double_signed_sync table) is outside this path.  Returns the new store rows."""
+        caller has already dropped duplicates (dispersy.py:1496-1498).  Messages of a double-member-signed meta
+        (meta.double_signed; .authentication.members, .member = members[0]) also record their member pair
+        (double_signed_sync, :1537-1541), and their LastSync history is kept per pair.  Returns the new store rows."""
         if not messages:
             return np.zeros(0, dtype=np.int64)
         # column by column (C-level getters over the list, no Python frame per message); what a meta needs (history,
@@ -484,29 +485,32 @@ class SyncCommunity(object):
         if any(info[0] for info in per_meta.values()):
             seqs = [d.sequence_number if per_meta[id(meta)][0] else 0 for d, meta in zip(dists, meta_objs)]
         members = list(map(_member_id, messages)) if has_member else None
+        double = ([i for i, meta in enumerate(meta_objs) if per_meta[id(meta)][2]]
+                  if any(info[2] for info in per_meta.values()) else [])
+        pairs = [[int(x.database_id) for x in messages[i].authentication.members] for i in double]
         rows = self._store.append(packets, gts, metas, member=members, sequence=seqs)
-        if any(h for _, h in per_meta.values()):
+        if double:  # INSERT INTO double_signed_sync (dispersy.py:1537-1541)
+            p = np.asarray(pairs, dtype=np.int64).reshape(-1, 2)
+            self._store.set_pairs(rows[double], p[:, 0], p[:, 1])
+        if any(info[1] for info in per_meta.values()):
             self._last_sync_history(messages)
         self.update_global_time(int(gts.max()))
         self.dispersy_store(messages)
         return rows
 
     def _meta_store_info(self, meta):
-        """(sequence, history): whether messages of `meta` store a sequence number (a sequence-numbered
-        FullSyncDistribution, dispersy.py:1529-1531) and keep a LastSyncDistribution history; raises for what this path does not store: the LastSyncDistribution history of a
-        double-member-signed meta (the reference keeps it per member pair in double_signed_sync, dispersy.py:1567-1578,
-        :1593-1594 -- pruning it per single member would delete the wrong rows), and per-member history or sequence
-        numbers in a store without its member column."""
+        """(sequence, history, double): whether messages of `meta` store a sequence number (a sequence-numbered
+        FullSyncDistribution, dispersy.py:1529-1531), keep a LastSyncDistribution history, and are double-member
+        signed (their member pair goes to double_signed_sync, :1537-1541; the history is then kept per pair,
+        :1567-1578).  Raises for per-member history or sequence numbers in a store without its member column."""
         dist = getattr(meta, "distribution", None)
         history = isinstance(dist, LastSyncDistribution)
         seq = isinstance(dist, FullSyncDistribution) and bool(dist.enable_sequence_number)
-        if history and getattr(meta, "double_signed", False) and not dist.custom_callback:
-            raise NotImplementedError("LastSyncDistribution history of a double-member-signed meta (%s): the "
-                                      "double_signed_sync table is outside this path" % getattr(meta, "name", "?"))
-        if self._store.member is None and (history or seq):
+        double = bool(getattr(meta, "double_signed", False))
+        if self._store.member is None and (history or seq or double):
             raise ValueError("store_messages: meta %s keeps per-member history; the store needs its member column"
                              % getattr(meta, "name", "?"))
-        return seq, history
+        return seq, history, double
 
     def _last_sync_history(self, messages):
         st = self._store
@@ -524,6 +528,13 @@ class SyncCommunity(object):
                         drop.append(st.row_of_id(syncid))
                     except KeyError:
                         pass
+                continue
+            if getattr(meta, "double_signed", False):  # per member pair, through double_signed_sync (:1567-1578)
+                for pair in OrderedDict.fromkeys(tuple(sorted(int(x.database_id) for x in m.authentication.members))
+                                                 for m in msgs):
+                    rows = st.pair_rows(meta.database_id, *pair)
+                    if len(rows) > dist.history_size:
+                        drop.extend(rows[:len(rows) - dist.history_size].tolist())
                 continue
             for member in OrderedDict.fromkeys(_member_id(m) for m in msgs):
                 rows = st.member_rows(meta.database_id, member)

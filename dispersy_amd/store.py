@@ -93,6 +93,7 @@ class SyncStore(object):
         # packets appended later, one bytes object per batch (appending to one growing buffer copied it every batch:
         # 8 MB per 10 k packets); _tail_at[i] = offsets[] of batch i's first byte
         self._tail, self._tail_at = [], []
+        self._pair_groups = {}  # (meta, member1, member2) -> rows: the double_signed_sync table (set_pairs)
         self._owns_handle = True
 
     # ------------------------------------------------------------------------------------------ columns
@@ -251,6 +252,23 @@ class SyncStore(object):
             rows = rows[np.argsort(self.global_time[rows], kind="stable")]
         self._groups[key] = rows
         return rows
+
+    # ------------------------------------------------------------------------------ double_signed_sync
+    def set_pairs(self, rows, member_a, member_b):
+        """INSERT INTO double_signed_sync (sync, member1, member2) for the given rows of double-member-signed messages:
+        the member pair, smaller id first (dispersy.py:1537-1541)."""
+        for r, a, b in zip(np.asarray(rows).tolist(), np.asarray(member_a).tolist(), np.asarray(member_b).tolist()):
+            pair = (a, b) if a < b else (b, a)
+            self._pair_groups.setdefault((int(self.meta[r]),) + pair, []).append(r)
+
+    def pair_rows(self, meta_id, member1, member2):
+        """Rows of one meta signed by the member pair (member1 < member2), deleted ones not, in the order of
+        `SELECT sync.id FROM sync JOIN double_signed_sync ON double_signed_sync.sync = sync.id WHERE
+        sync.meta_message = ? AND member1 = ? AND member2 = ? ORDER BY sync.global_time, sync.packet`
+        (dispersy.py:1571-1578): global time, then the packet bytes."""
+        rows = [r for r in self._pair_groups.get((int(meta_id), int(member1), int(member2)), ()) if not self.deleted[r]]
+        self._pair_groups[(int(meta_id), int(member1), int(member2))] = rows
+        return np.asarray(sorted(rows, key=lambda r: (int(self.global_time[r]), self.packet(r))), dtype=np.int64)
 
     # ------------------------------------------------------------------------------------------ ingest
     def append(self, packets, global_time, meta, rowid=None, member=None, sequence=None):

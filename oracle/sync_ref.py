@@ -26,6 +26,8 @@ CREATE TABLE sync(id INTEGER PRIMARY KEY AUTOINCREMENT, community INTEGER, membe
                   meta_message INTEGER, undone INTEGER DEFAULT 0, packet BLOB, sequence INTEGER,
                   UNIQUE(community, member, global_time));
 CREATE INDEX sync_mug ON sync(meta_message, undone, global_time);
+CREATE TABLE double_signed_sync(sync INTEGER REFERENCES sync(id), member1 INTEGER, member2 INTEGER);
+CREATE INDEX double_signed_sync_index_0 ON double_signed_sync(member1, member2);
 """
 
 
@@ -155,6 +157,33 @@ def store_last_sync(conn, community, meta_id, history_size, messages):
         if len(all_items) > history_size:
             items.extend(all_items[:len(all_items) - history_size])
     conn.executemany("DELETE FROM sync WHERE id = ?", [(i,) for i, _ in items])
+    return ids
+
+
+def store_double_signed(conn, community, meta_id, history_size, messages):
+    """_store for a double-member-signed LastSyncDistribution meta (dispersy.py:1521-1594): INSERT every message into
+    sync (member = members[0]) and its member pair, smaller id first, into double_signed_sync (:1537-1541); then per
+    member pair of the batch, the pair's rows joined through double_signed_sync in (global_time, packet) order, and the
+    ones beyond the newest history_size DELETEd from both tables (:1567-1578, :1589-1594).
+    messages: (member_a, member_b, gt, packet).  Returns the new row ids."""
+    ids = []
+    for a, b, gt, packet in messages:
+        cur = conn.execute("INSERT INTO sync (community, member, global_time, meta_message, packet, sequence) "
+                           "VALUES (?, ?, ?, ?, ?, ?)", (community, a, gt, meta_id, packet, None))
+        ids.append(cur.lastrowid)
+        conn.execute("INSERT INTO double_signed_sync (sync, member1, member2) VALUES (?, ?, ?)",
+                     (cur.lastrowid, min(a, b), max(a, b)))
+    items = set()
+    for m1, m2 in set((min(a, b), max(a, b)) for a, b, _, _ in messages):
+        all_items = conn.execute("SELECT sync.id, sync.global_time FROM sync JOIN double_signed_sync ON "
+                                 "double_signed_sync.sync = sync.id WHERE sync.meta_message = ? AND "
+                                 "double_signed_sync.member1 = ? AND double_signed_sync.member2 = ? "
+                                 "ORDER BY sync.global_time, sync.packet", (meta_id, m1, m2)).fetchall()
+        if len(all_items) > history_size:
+            items.update(all_items[:len(all_items) - history_size])
+    if items:
+        conn.executemany("DELETE FROM sync WHERE id = ?", [(i,) for i, _ in items])
+        conn.executemany("DELETE FROM double_signed_sync WHERE sync = ?", [(i,) for i, _ in items])
     return ids
 
 

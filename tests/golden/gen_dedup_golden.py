@@ -9,7 +9,7 @@ mechanical edits as gen_sync_golden.py (`__debug__` -> False, decorators dropped
 table built from the reference's schema string.  Only those two methods' text is parsed (the rest of dispersy.py is Python 2).  Bound in their
 globals: `str`/`buffer` -> bytes, `cmp`, `Message.Implementation` (the message stand-in class), and a
 `sorted` that accepts the py2 positional comparison function.  Only the resulting data is committed
-(dedup_vectors.json, dedup_seq_vectors.json, laststore_vectors.json).
+(dedup_vectors.json, dedup_seq_vectors.json, laststore_vectors.json, doublestore_vectors.json).
 """
 import ast
 import collections
@@ -413,7 +413,94 @@ def laststore_main():
     print("laststore vectors: %d batches, table %d -> %d rows" % (len(steps), len(initial), len(steps[-1]["table"])))
 
 
+class _DoubleImpl(_DoubleAuth.Implementation):
+    """A DoubleMemberAuthentication.Implementation stand-in: .member is members[0] (authentication.py:276-290)."""
+    encoding = "bin"
+    is_signed = True
+
+    def __init__(self, members):
+        self.members = members
+        self.member = members[0]
+
+
+def _double_table(conn):
+    return [list(r) for r in conn.execute("SELECT sync, member1, member2 FROM double_signed_sync ORDER BY sync")]
+
+
+def doublestore_main():
+    """_store (dispersy.py:1475-1612) for a double-member-signed LastSyncDistribution meta: each INSERT into sync
+    (member = members[0]) is paired with one into double_signed_sync (the member pair, smaller id first, :1537-1541);
+    the history is kept per member pair -- rows joined through double_signed_sync, ordered by (global_time, packet)
+    (:1567-1578) -- and what falls out is DELETEd from both tables (:1589-1594).  Batches in sequence; both tables
+    after each.  Member ids are few, so pairs recur in both orders and global times tie within a pair."""
+    rng = np.random.Generator(np.random.PCG64(4242))
+    conn = sqlite3.connect(":memory:")
+    conn.executescript(reference_schema())
+    used = set()
+    n0 = 0
+    for _ in range(30):
+        a, b = (int(x) for x in rng.choice(np.arange(1, 9), size=2, replace=False))
+        gt = int(rng.integers(1, 12))
+        if (a, gt) in used:
+            continue
+        used.add((a, gt))
+        n0 += 1
+        conn.execute("INSERT INTO sync (id, community, member, global_time, meta_message, undone, packet) "
+                     "VALUES (?, 1, ?, ?, 5, 0, ?)", (n0, a, gt, rng.bytes(int(rng.integers(20, 40)))))
+        conn.execute("INSERT INTO double_signed_sync (sync, member1, member2) VALUES (?, ?, ?)", (n0, min(a, b), max(a, b)))
+    stored = []
+
+    class Community(object):
+        database_id = 1
+
+        def update_global_time(self, gt):
+            stored.append(["update_global_time", gt])
+
+        def dispersy_store(self, messages):
+            stored.append(["dispersy_store", [m.index for m in messages]])
+
+    community = Community()
+    meta = _Obj(name="double", community=community, database_id=5, authentication=_DoubleAuth(),
+                distribution=LastSync(history_size=2))
+    d = StubDispersy(conn, lift())
+    initial, initial_double = _table(conn), _double_table(conn)
+    steps, idx = [], 0
+    for _ in range(16):
+        msgs = []
+        for _ in range(int(rng.integers(1, 9))):
+            a, b = (int(x) for x in rng.choice(np.arange(1, 9), size=2, replace=False))
+            gt = int(rng.integers(1, 16))
+            if (a, gt) in used:
+                continue
+            used.add((a, gt))
+            packet = rng.bytes(int(rng.integers(20, 60))) + b"\x01"
+            m = _Obj(index=idx, name="double", community=community, meta=meta, database_id=5, packet=packet,
+                     authentication=_DoubleImpl([_Obj(database_id=a, has_identity=lambda c: True),
+                                                 _Obj(database_id=b, has_identity=lambda c: True)]),
+                     distribution=_Dist(global_time=gt))
+            idx += 1
+            msgs.append(m)
+        if not msgs:
+            continue
+        stored.clear()
+        d.store(msgs)
+        steps.append(dict(messages=[dict(index=m.index, members=[x.database_id for x in m.authentication.members],
+                                         gt=m.distribution.global_time, packet=m.packet.hex()) for m in msgs],
+                          packet_ids=[m.packet_id for m in msgs], calls=list(stored), table=_table(conn),
+                          double=_double_table(conn)))
+    out = dict(history_size=2, meta=5, initial_table=initial, initial_double=initial_double, steps=steps)
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "doublestore_vectors.json"), "w") as f:
+        json.dump(out, f, separators=(",", ":"))
+    print("doublestore vectors: %d batches, table %d -> %d rows, double_signed_sync %d -> %d" % (
+        len(steps), len(initial), len(steps[-1]["table"]), len(initial_double), len(steps[-1]["double"])))
+
+
 if __name__ == "__main__":
-    main()
-    seq_main()
-    laststore_main()
+    import sys
+    if sys.argv[1:] == ["double"]:
+        doublestore_main()
+    else:
+        main()
+        seq_main()
+        laststore_main()
+        doublestore_main()

@@ -20,6 +20,7 @@ from oracle import sync_ref
 
 SEQ = load("dedup_seq_vectors.json")
 LAST = load("laststore_vectors.json")
+DOUBLE = load("doublestore_vectors.json")
 
 
 def sqlite_of(table):
@@ -62,6 +63,24 @@ def test_oracle_last_sync_store_matches_reference():
                                        [(m["member"], m["gt"], bytes.fromhex(m["packet"])) for m in step["messages"]])
         assert ids == step["packet_ids"]
         assert table_of(conn) == step["table"]
+
+
+def double_table_of(conn):
+    return [list(r) for r in conn.execute("SELECT sync, member1, member2 FROM double_signed_sync ORDER BY sync")]
+
+
+def test_oracle_double_signed_store_matches_reference():
+    """dispersy.py:1537-1541, :1567-1594 (double_signed_sync), replayed by the lifted reference _store."""
+    conn = sqlite_of(DOUBLE["initial_table"])
+    conn.executemany("INSERT INTO double_signed_sync (sync, member1, member2) VALUES (?, ?, ?)",
+                     [tuple(r) for r in DOUBLE["initial_double"]])
+    for step in DOUBLE["steps"]:
+        ids = sync_ref.store_double_signed(conn, 1, DOUBLE["meta"], DOUBLE["history_size"],
+                                           [(m["members"][0], m["members"][1], m["gt"], bytes.fromhex(m["packet"]))
+                                            for m in step["messages"]])
+        assert ids == step["packet_ids"]
+        assert table_of(conn) == step["table"]
+        assert double_table_of(conn) == step["double"]
 
 
 # ------------------------------------------------------------------------------------------------- GPU
@@ -161,9 +180,8 @@ def test_last_sync_history_matches_reference(lazy):
 
 
 def test_store_messages_refuses_what_it_cannot_keep_consistent():
-    """store_messages checks a batch before storing any of it: a LastSync meta without the store's member column, and
-    the history of a double-member-signed LastSync meta (double_signed_sync, dispersy.py:1567-1578), are refused with
-    both store copies unchanged (CPU: the store is not on the device)."""
+    """store_messages checks a batch before storing any of it: a LastSync meta, or a double-member-signed one, without
+    the store's member column is refused with both store copies unchanged (CPU: the store is not on the device)."""
     import pytest as _pytest
     from dispersy_amd.community import SyncCommunity
     from dispersy_amd.distribution import LastSyncDistribution, MetaMessage
@@ -185,8 +203,71 @@ def test_store_messages_refuses_what_it_cannot_keep_consistent():
         com.store_messages([M(last, 7, 3)])
     assert store.n == 1
     dbl = MetaMessage("dbl", 2, LastSyncDistribution("ASC", 128, history_size=1), double_signed=True)
-    store2 = SyncStore.from_rows([(1, 5, 2, 0, b"x", 4)], ctx=object())
+    store2 = SyncStore.from_rows([(1, 5, 2, 0, b"x")], ctx=object())  # no member column
     com2 = SyncCommunity(store2, [dbl], global_time=10)
-    with _pytest.raises(NotImplementedError):
+    with _pytest.raises(ValueError):
         com2.store_messages([M(dbl, 7, 4)])
     assert store2.n == 1
+
+
+class _DoubleAuth(object):
+    """DoubleMemberAuthentication.Implementation's surface: .members, and .member = members[0] (authentication.py:276-290)."""
+
+    def __init__(self, a, b):
+        self.members = [_Member(a, 60), _Member(b, 60)]
+        self.member = self.members[0]
+
+
+class _DoubleMsg(_Msg):
+    def __init__(self, meta, a, b, gt, packet, index):
+        super(_DoubleMsg, self).__init__(meta, a, gt, packet, index)
+        self.authentication = _DoubleAuth(a, b)
+
+
+def _double_replay(store, com, meta):
+    for step in DOUBLE["steps"]:
+        msgs = [_DoubleMsg(meta, m["members"][0], m["members"][1], m["gt"], bytes.fromhex(m["packet"]), m["index"])
+                for m in step["messages"]]
+        rows = com.store_messages(msgs)
+        assert store.rowid[rows].tolist() == step["packet_ids"]
+        assert alive(store) == sorted((r[0], r[5]) for r in step["table"])
+        # the double_signed_sync rows that join a live sync row: each live row's pair
+        pairs = {}
+        for (mid, m1, m2), rs in store._pair_groups.items():
+            for r in rs:
+                if not store.deleted[r]:
+                    pairs[int(store.rowid[r])] = [m1, m2]
+        assert sorted([k] + v for k, v in pairs.items()) == step["double"]
+
+
+def _double_store():
+    store = store_of(DOUBLE["initial_table"])
+    rid = {int(store.rowid[r]): r for r in range(store.n)}
+    d = DOUBLE["initial_double"]
+    store.set_pairs([rid[s] for s, _, _ in d], [a for _, a, _ in d], [b for _, _, b in d])
+    meta = MetaMessage("double", DOUBLE["meta"], LastSyncDistribution("ASC", 128, DOUBLE["history_size"]),
+                       double_signed=True)
+    return store, meta
+
+
+def test_double_signed_history_matches_reference_host():
+    """Double-member-signed LastSync messages (dispersy.py:1537-1541, :1567-1594) replayed by SyncCommunity on a store
+    not yet on the device (the host copy: rows, DELETEs, double_signed_sync)."""
+    store, meta = _double_store()
+    store._ctx = object()  # never uploaded
+    _double_replay(store, SyncCommunity(store, [meta], global_time=1), meta)
+
+
+@pytest.mark.gpu
+def test_double_signed_history_matches_reference():
+    """The same replay with the store in HBM: the DELETEs go through dsy_store_delete, and a claim over everything
+    with an empty filter returns exactly the rows the reference keeps."""
+    store, meta = _double_store()
+    store.handle  # noqa: B018
+    com = SyncCommunity(store, [meta], global_time=1)
+    _double_replay(store, com, meta)
+    from dispersy_amd import BloomFilter
+    from dispersy_amd.community import ClaimRequest
+    (got,) = com.respond([ClaimRequest(1, 10 ** 6, 1, 0, BloomFilter(1024, 0.01, b"\x00"))], include_inactive=True,
+                         byte_limit=1 << 40)
+    assert sorted(store.rowid[got].tolist()) == sorted(r[0] for r in DOUBLE["steps"][-1]["table"])
