@@ -195,6 +195,10 @@ struct dsy_store {
     uint64_t* spare_gt = nullptr;   // the ingest's second index buffer pair (the next merge's target)
     uint64_t* spare_row = nullptr;
     uint64_t spare_cap = 0;
+    // appended rows not yet in the live index (dsy_store_append is O(batch): the index absorbs every pending row in
+    // ONE merge when something next reads it -- store_flush, called by every reader of the index)
+    std::vector<uint32_t> pend_meta;
+    std::vector<uint64_t> pend_gt, pend_row;
 };
 
 namespace {
@@ -1099,6 +1103,19 @@ static int live_insert(dsy_ctx* c, dsy_store* s, const uint32_t* meta, const uin
     return DSY_OK;
 }
 
+// Merge the rows appended since the last read into the live index (one device merge, live_insert).  Every reader of
+// the index calls it first; the caller holds the ctx lock and nothing is in flight on the store.
+static int store_flush(dsy_ctx* c, const dsy_store* cs) {
+    dsy_store* s = const_cast<dsy_store*>(cs);
+    if (s->pend_row.empty()) return DSY_OK;
+    int rc = live_insert(c, s, s->pend_meta.data(), s->pend_gt.data(), s->pend_row.data(), s->pend_row.size(), false);
+    if (rc) return rc;
+    s->pend_meta.clear();
+    s->pend_gt.clear();
+    s->pend_row.clear();
+    return DSY_OK;
+}
+
 int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blob_len, const uint64_t* offsets,
                      uint64_t a, const uint64_t* gt, const uint32_t* meta, const uint64_t* member) {
     if (!c || !s || !offsets || (a && (!gt || !meta || (blob_len && !blob)))) return fail(DSY_EINVAL, "NULL argument");
@@ -1151,10 +1168,11 @@ int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blo
     HIP_TRY(hipMemcpyAsync(const_cast<RowRec*>(s->d_rec) + n0, up_rec, b_rec, hipMemcpyDeviceToDevice, c->stream));
     HIP_TRY(launch_store_lines(up, (const uint64_t*)up_off, s->d_rec + n0, a, const_cast<uint8_t*>(s->d_lines),
                                c->stream));
-    // the new rows join the live index (positions n0 .. n0+a-1: after every stored row of equal global time)
-    std::vector<uint64_t> pos(a);
-    for (uint64_t j = 0; j < a; ++j) pos[j] = n0 + j;
-    if ((rc = live_insert(c, s, meta, gt, pos.data(), a, false))) return rc;
+    // the new rows join the live index (positions n0 .. n0+a-1: after every stored row of equal global time) at the
+    // next read of the index (store_flush): a stream of appends costs O(batch) each and one merge in all
+    s->pend_meta.insert(s->pend_meta.end(), meta, meta + a);
+    s->pend_gt.insert(s->pend_gt.end(), gt, gt + a);
+    for (uint64_t j = 0; j < a; ++j) s->pend_row.push_back(n0 + j);
     if (s->dup && (rc = dup_insert(c, s, member, gt, n0, a))) return rc;
     s->min_len = n0 ? std::min(s->min_len, minlen) : minlen;
     s->n += a;
@@ -1168,10 +1186,11 @@ int dsy_store_prune(dsy_ctx* c, dsy_store* s, uint32_t meta, uint64_t max_gt, ui
     if (!c || !s || !out_deleted) return fail(DSY_EINVAL, "NULL argument");
     if (s->ctx != c) return fail(DSY_EINVAL, "store belongs to another context");
     *out_deleted = 0;
-    auto it = s->segs.find(meta);
-    if (it == s->segs.end() || it->second.first == it->second.second) return DSY_OK;
     Guard g(c);
     if (c->inflight()) return fail(DSY_EINVAL, "the store cannot change while submitted responder batches are in flight");
+    if (int rc = store_flush(c, s)) return rc;
+    auto it = s->segs.find(meta);
+    if (it == s->segs.end() || it->second.first == it->second.second) return DSY_OK;
     const uint64_t a = it->second.first, b = it->second.second;
     void* d_k;
     int rc;
@@ -1310,6 +1329,7 @@ int dsy_store_delete(dsy_ctx* c, dsy_store* s, const uint64_t* rows, uint64_t k,
     if (!k) return DSY_OK;
     Guard g(c);
     if (c->inflight()) return fail(DSY_EINVAL, "the store cannot change while submitted responder batches are in flight");
+    if (int rc = store_flush(c, s)) return rc;
     return live_remove(c, s, rows, k, true, out_deleted);
 }
 
@@ -1323,6 +1343,7 @@ int dsy_store_set_undone(dsy_ctx* c, dsy_store* s, const uint64_t* rows, uint64_
     if (!k) return DSY_OK;
     Guard g(c);
     if (c->inflight()) return fail(DSY_EINVAL, "the store cannot change while submitted responder batches are in flight");
+    if (int rc = store_flush(c, s)) return rc;
     if (undone) return live_remove(c, s, rows, k, false, out_changed);
     std::vector<uint64_t> r(rows, rows + k);
     std::vector<uint64_t> sorted_r(r);
@@ -1460,6 +1481,8 @@ int dsy_claim_modulo(dsy_ctx* c, const dsy_bloom_params* p, const dsy_store* s, 
     int rc = check_params(p);
     if (rc) return rc;
     *out_count = 0;
+    Guard g(c);
+    if ((rc = store_flush(c, s))) return rc;
     std::vector<std::pair<uint64_t, uint64_t>> spans;
     uint64_t total = 0;
     // `meta_message IN (...)` counts each row once, however often an id is listed
@@ -1472,7 +1495,6 @@ int dsy_claim_modulo(dsy_ctx* c, const dsy_bloom_params* p, const dsy_store* s, 
         spans.push_back(it->second);
         total += it->second.second - it->second.first;
     }
-    Guard g(c);
     const uint64_t nbytes = p->m_bits / 8, words = filter_words(p->m_bits);
     void *df, *dr, *dn;
     if ((rc = ws_get(c, "filter", words * 4, &df))) return rc;
@@ -1595,6 +1617,8 @@ int dsy_claim_largest(dsy_ctx* c, const dsy_bloom_params* p, const dsy_store* s,
     if (capacity == 0) return fail(DSY_EINVAL, "capacity must be positive");
     int rc = check_params(p);
     if (rc) return rc;
+    Guard g(c);
+    if ((rc = store_flush(c, s))) return rc;
     // the syncable metas' live segments (`meta_message IN (...)`: each id once)
     std::vector<uint32_t> ids(meta_ids, meta_ids + nmeta);
     std::sort(ids.begin(), ids.end());
@@ -1607,7 +1631,6 @@ int dsy_claim_largest(dsy_ctx* c, const dsy_bloom_params* p, const dsy_store* s,
         segs.push_back(it->second.second);
     }
     const uint32_t J = (uint32_t)(segs.size() / 2);
-    Guard g(c);
     out_claim[0] = out_claim[1] = out_claim[2] = 0;
     out_claim[3] = nrsyncpackets;
     const size_t b_segs = (size_t)J * 16, b_cand = (size_t)J * (capacity + 2) * 8, b_spans = (size_t)4 * J * 16,
@@ -1904,6 +1927,7 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const Clai
     RespondJob& jb = sl.job;
     const hipStream_t st = c->stream;
     if (!sl.ev_done) HIP_TRY(hipEventCreate(&sl.ev_done));  // (recorded by a dispatch: hipExtLaunchKernelGGL)
+    if (int rc = store_flush(c, s)) return rc;  // rows appended since the last read join the index first
     if (g_host_profile) jb.hp[0] = host_us();
     // ---- validate claims (payload.py:89-101, conversion.py:772-789) and their filters; group them by hash family
     // (kind x chunk width: one pair-test launch per family)
