@@ -554,23 +554,50 @@ struct ChunkLimit {
     static constexpr int kmax = H::digest_bytes / CHUNK;
 };
 
-// pos = chunk % m  (bloomfilter.py:171).  'H'/'L' chunks are < 2^32 and their filters have m < 2^31.
+// ceil(2^32 / m) for 2 <= m < 2^31, else 0: the multiplier bit_position uses instead of a division per probe (the
+// claim records carry it, DevRequest::m_recip, so the responder does not divide at all).
+__host__ __device__ inline uint32_t mod_recip(uint64_t m) {
+    return (m >= 2 && m < (1ull << 31)) ? (uint32_t)(0xFFFFFFFFu / (uint32_t)m) + 1u : 0u;
+}
+
+// pos = chunk % m  (bloomfilter.py:171), by multiply-high with recip = mod_recip(m) (m < 2^31 for 'H'/'L' chunks,
+// bloomfilter.py:135-140).  A generic 32-bit remainder costs two quarter-rate multiplies and two conditional
+// subtractions per probe (k probes per key); these cost one multiply-high and two full-rate ops:
+//   'H' (a < 2^16, 8 <= m < 2^15): q = mulhi(a, ceil(2^32/m)) is floor(a/m) exactly -- the excess a*e/2^32 < 2^-16
+//        is below the 1/m gap to the next integer -- so r = a - q*m (a 24-bit multiply).  m >= 8: check_family
+//        refuses sizes that are not positive multiples of eight.
+//   'L' (a < 2^32, 2^15 <= m < 2^31): q is floor(a/m) or one more, so r = a - q*m is right or wrapped below zero
+//        (>= 2^32 - m); min(r, r + m) picks the right one.
+// tests/test_bitmod.py checks both against % (every 'H' pair exhaustively) and the device positions against hashlib.
+template <int CHUNK>
+__device__ __forceinline__ uint64_t bit_position(uint64_t chunk, uint64_t m, uint32_t recip) {
+    if constexpr (CHUNK == 8) {
+        return chunk % m;
+    } else if constexpr (CHUNK == 2) {
+        const uint32_t a = (uint32_t)chunk;
+        return a - __umul24(__umulhi(a, recip), (uint32_t)m);
+    } else {
+        const uint32_t a = (uint32_t)chunk;
+        const uint32_t r = a - __umulhi(a, recip) * (uint32_t)m;
+        return min(r, r + (uint32_t)m);
+    }
+}
+
 template <int CHUNK>
 __device__ __forceinline__ uint64_t bit_position(uint64_t chunk, uint64_t m) {
-    if (CHUNK == 8) return chunk % m;
-    return (uint32_t)chunk % (uint32_t)m;
+    return bit_position<CHUNK>(chunk, m, CHUNK == 8 ? 0u : mod_recip(m));
 }
 
 // Membership of one key: 1 when all k probed bits are set (bloomfilter.py:185-197).  Every chunk the digest holds
 // is looked up -- no branch per probe, so the k loads go out together behind one wait instead of one round trip
 // each -- and the ones past k do not count (their positions are < m, so the reads stay inside the filter).
 template <class H, int CHUNK, class W>
-__device__ __forceinline__ uint32_t filter_has_all(W* fb, const H& st, uint32_t k, uint64_t m) {
+__device__ __forceinline__ uint32_t filter_has_all(W* fb, const H& st, uint32_t k, uint64_t m, uint32_t recip) {
     constexpr int kmax = ChunkLimit<H, CHUNK>::kmax;
     uint32_t w[kmax], sh[kmax];
 #pragma unroll
     for (int j = 0; j < kmax; ++j) {
-        const uint64_t pos = bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, j), m);
+        const uint64_t pos = bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, j), m, recip);
         w[j] = fb[pos >> 5];
         sh[j] = (uint32_t)pos & 31u;
     }
@@ -582,6 +609,11 @@ __device__ __forceinline__ uint32_t filter_has_all(W* fb, const H& st, uint32_t 
 #pragma unroll
     for (int j = 0; j < kmax; ++j) ok &= (w[j] >> sh[j]) | (uint32_t)(j >= (int)k);
     return ok & 1u;
+}
+
+template <class H, int CHUNK, class W>
+__device__ __forceinline__ uint32_t filter_has_all(W* fb, const H& st, uint32_t k, uint64_t m) {
+    return filter_has_all<H, CHUNK>(fb, st, k, m, CHUNK == 8 ? 0u : mod_recip(m));
 }
 
 // Filter build of one key per lane (bloomfilter.py:172-178: filter |= 1 << pos for its k positions).  Called by the
@@ -598,11 +630,12 @@ template <class H, int CHUNK, int OR_MODE, class W>
 __device__ __forceinline__ void filter_set_all(W* fb, const H& st, uint32_t k, uint64_t m, bool active,
                                                uint32_t wbase = 0) {
     constexpr int kmax = ChunkLimit<H, CHUNK>::kmax;
+    const uint32_t recip = CHUNK == 8 ? 0u : mod_recip(m);
     if constexpr (OR_MODE == 0) {
 #pragma unroll
         for (int j = 0; j < kmax; ++j) {
             if (active && j < (int)k) {
-                const uint64_t pos = bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, j), m);
+                const uint64_t pos = bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, j), m, recip);
                 atomicOr(&fb[wbase + (uint32_t)(pos >> 5)], 1u << (pos & 31));
             }
         }
@@ -611,7 +644,7 @@ __device__ __forceinline__ void filter_set_all(W* fb, const H& st, uint32_t k, u
     uint32_t w[kmax], idx[kmax], bit[kmax];
 #pragma unroll
     for (int j = 0; j < kmax; ++j) {
-        const uint64_t pos = active ? bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, j), m) : 0;
+        const uint64_t pos = active ? bit_position<CHUNK>(digest_chunk<H, CHUNK>(st, j), m, recip) : 0;
         idx[j] = wbase + (uint32_t)(pos >> 5);
         bit[j] = 1u << (pos & 31);
         w[j] = fb[idx[j]];

@@ -1275,7 +1275,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         if (raised) __builtin_amdgcn_s_setprio(0);
         const uint32_t* filt = (const uint32_t*)(L.filters + q.filter_offset);
         const uint64_t m = q.m_bits;
-        const uint32_t ok = filter_has_all<H, CHUNK>(filt, st, q.k, m);
+        const uint32_t ok = filter_has_all<H, CHUNK>(filt, st, q.k, m, q.m_recip);
         if (active) {
             // misses are rare (the requester holds most of its range): one atomic bit per missing pair
             if (!ok && DIAG == 0)  // (the diagnostics' digests are garbage: their misses would be mostly atomics)

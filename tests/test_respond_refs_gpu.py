@@ -80,7 +80,7 @@ def test_refs_layout_and_argument_checks():
     assert np.diff(off).tolist() == [n_rows] * 3
     # a bound past 2^63-1 is clamped, as the record form requires of its caller (community.py:2545-2548)
     big = ranges.copy()
-    big[:, 1] = np.uint64(1 << 64) - np.uint64(1)
+    big[:, 1] = np.uint64(0xFFFFFFFFFFFFFFFF)
     _native.check(call(big, refs))
     assert np.diff(off).tolist() == [n_rows] * 3
     bad = refs.copy()
