@@ -935,12 +935,18 @@ def ingest_bench(args, ctx, lib, store, step, N, batch=10_000, batches=10, cpu_l
     import torch
     rng = np.random.Generator(np.random.PCG64(99))
 
-    def make():
+    top = [N]  # the highest global time stored so far
+
+    def make(recent):
         lens = rng.integers(100, 1501, size=batch)
         off = np.zeros(batch + 1, dtype=np.uint64)
         np.cumsum(lens, out=off[1:])
         data = rng.bytes(int(off[-1]))
-        gts = rng.integers(1, N + 1, size=batch).astype(np.uint64)
+        if recent:  # new messages: global times around the community's current one (the last 10 k and above)
+            gts = rng.integers(top[0] - 10_000, top[0] + batch, size=batch).astype(np.uint64)
+            top[0] += batch
+        else:  # old messages (a peer catching up): anywhere in the history
+            gts = rng.integers(1, N + 1, size=batch).astype(np.uint64)
         metas = np.ones(batch, dtype=np.uint32)
         return data, off, gts, metas
 
@@ -953,29 +959,52 @@ def ingest_bench(args, ctx, lib, store, step, N, batch=10_000, batches=10, cpu_l
         _native.check(lib.dsy_store_append(ctx.handle, store, data, len(data), off.ctypes.data, batch,
                                            gts.ctypes.data, metas.ctypes.data, mem.ctypes.data))
 
-    work = [make() for _ in range(batches + 1)]
-    t0 = time.perf_counter()
-    append(work[0])
-    first_ms = (time.perf_counter() - t0) * 1e3
-    times = []
-    for b in work[1:]:
+    def ix_stats():
+        out = np.zeros(6, dtype=np.uint64)
+        _native.check(lib.dsy_store_index_stats(store, out.ctypes.data))
+        return out.astype(np.int64)
+
+    def timed_step():
+        ctx.synchronize()
         t0 = time.perf_counter()
-        append(b)
-        times.append(time.perf_counter() - t0)
-    ms = sorted(times)[len(times) // 2] * 1e3
+        pairs = step()
+        ctx.synchronize()
+        return (time.perf_counter() - t0) * 1e3, pairs
+
+    first_ms = None
+    work_legs = {}
+    after_pairs = 0
+    for kind, recent in (("history", False), ("recent", True)):
+        work = [make(recent) for _ in range(batches + (1 if first_ms is None else 0))]
+        if first_ms is None:  # the first append moves the attached store into buffers of its own
+            t0 = time.perf_counter()
+            append(work.pop(0))
+            first_ms = (time.perf_counter() - t0) * 1e3
+            timed_step()  # merges it
+        # interleaved, as a Dispersy peer runs: one received batch stored, then the next responder step reads the
+        # index (store_flush merges the batch)
+        s0, t_app, t_read = ix_stats(), [], []
+        for b in work:
+            t0 = time.perf_counter()
+            append(b)
+            t_app.append(time.perf_counter() - t0)
+            t_read.append(timed_step()[0])
+        s1 = ix_stats()
+        base_ms, after_pairs = timed_step()  # a step with nothing to merge
+        work_legs[kind] = {
+            "global_times": ("anywhere in the store's history [1, %d]" % N if not recent else
+                             "the newest 10 k and above (new messages)"),
+            "median_ms_per_append": round(sorted(t_app)[len(t_app) // 2] * 1e3, 3),
+            "median_responder_step_after_an_append_ms": round(sorted(t_read)[len(t_read) // 2], 3),
+            "responder_step_without_merge_ms": round(base_ms, 3),
+            "in_place_tail_merges": int(s1[2] - s0[2]), "whole_index_merges": int(s1[3] - s0[3]),
+            "index_bytes_per_append": int((s1[4] - s0[4]) // len(work)),
+            "index_bytes_per_append_over_batch_index_bytes": round(float(s1[4] - s0[4]) / len(work) / (16 * batch), 2),
+            "index_entries_live_and_slack": [int(s1[0]), int(s1[1])]}
+        ms_list = t_app
+    ms = sorted(ms_list)[len(ms_list) // 2] * 1e3
     rows = int(lib.dsy_store_rows(store))
-    pkt_bytes = sum(len(b[0]) for b in work[1:]) / batches
-    # the first read of the index after the appends merges every pending row into it (store_flush: one O(store)
-    # merge for all 11 batches); a responder step before and after shows that merge's cost
-    ctx.synchronize()
-    t0 = time.perf_counter()
-    after_pairs = step()
-    ctx.synchronize()
-    first_read_ms = (time.perf_counter() - t0) * 1e3
-    t0 = time.perf_counter()
-    step()
-    ctx.synchronize()
-    next_read_ms = (time.perf_counter() - t0) * 1e3
+    pkt_bytes = float(np.mean([len(w[0]) for w in work]))
     torch.cuda.synchronize()
     cpu = None
     if cpu_leg and args.cpu_claims > 0:  # the CPU baseline leg: the reference's INSERT through sqlite3 (oracle/sync_ref.py)
@@ -1020,14 +1049,13 @@ def ingest_bench(args, ctx, lib, store, step, N, batch=10_000, batches=10, cpu_l
     return {"metric": "received packets stored/sec", "batch": batch, "batches": batches, "cpu_baseline": cpu,
             "store_rows_after": rows, "median_ms_per_batch": round(ms, 3),
             "packets_per_s": round(batch / (ms / 1e3), 1),
-            "first_append_ms": round(first_ms, 2),
-            "index_bytes_per_append": 16 * batch, "packet_bytes_per_append": int(pkt_bytes),
-            "index_maintenance": "an append queues its rows' (meta, global_time, row) entries (16 B each); the next "
-                                 "read of the index merges every queued row in one device merge (32 B per indexed "
-                                 "row: %d B for this store, once for all %d batches)" % (32 * rows, batches + 1),
-            "deferred_merge": {"first_responder_step_after_appends_ms": round(first_read_ms, 3),
-                               "next_responder_step_ms": round(next_read_ms, 3),
-                               "merge_ms_estimate": round(first_read_ms - next_read_ms, 3)},
+            "first_append_ms": round(first_ms, 2), "packet_bytes_per_append": int(pkt_bytes),
+            "index_maintenance": "an append queues its rows' (meta, global_time, row) entries (16 B each) on the "
+                                 "device; the next read of the index orders them (radix sort) and merges each meta's "
+                                 "tail from its first new entry in place into the slack of its region, or merges the "
+                                 "whole index once (32 B per entry) when the tails would move more",
+            "index_bytes_per_append": work_legs["recent"]["index_bytes_per_append"],
+            "workloads": work_legs,
             "roofline": {"kernel": "the whole append call: packet upload (PCIe), line copy, row records",
                          "bound": "hbm", "unit": "GB/s", "peak": PEAK_HBM_GBS,
                          "achieved": round((16 * batch + pkt_bytes) / (ms / 1e3) / 1e9, 1),

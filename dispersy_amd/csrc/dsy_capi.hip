@@ -160,6 +160,10 @@ struct dsy_ctx {
     uint64_t window_cap = 0; // dsy_ctx_set_window: upper bound on the responder's window (0: the default 2^18)
     hipStream_t aux = nullptr;  // dsy_sim_claim_matrix: work that depends on nothing queued on `stream`
     hipEvent_t xev = nullptr;   // dsy_ctx_wait_stream / dsy_ctx_signal_stream
+    // pinned staging of dsy_store_append's small columns (offsets, records, global times, metas, members): one
+    // upload per append; the next append synchronises the stream before it writes here again
+    uint8_t* in_stage = nullptr;
+    size_t in_stage_bytes = 0;
     // the simulator's device-side counters (work of build / respond, pairs tested, response overflow): the calls
     // enqueue without reading them back; the synchronising accessors fold them (sim_collect)
     void* sim_acc = nullptr;
@@ -197,8 +201,14 @@ struct dsy_store {
     uint64_t spare_cap = 0;
     // appended rows not yet in the live index (dsy_store_append is O(batch): the index absorbs every pending row in
     // ONE merge when something next reads it -- store_flush, called by every reader of the index)
-    std::vector<uint32_t> pend_meta;
-    std::vector<uint64_t> pend_gt, pend_row;
+    // on the device: (meta, global_time) of pending entry j, whose row is pend_base + j (appended rows are contiguous)
+    uint32_t* d_pend_meta = nullptr;
+    uint64_t* d_pend_gt = nullptr;
+    uint64_t pend_n = 0, pend_cap = 0, pend_base = 0, pend_glo = 0, pend_ghi = 0;
+    std::map<uint32_t, uint64_t> pend_cnt;  // pending entries per meta
+    // entries of the live index arrays: the live ones (n_live) and each meta region's slack (store_flush)
+    uint64_t n_phys = 0;
+    uint64_t ix_fast = 0, ix_full = 0, ix_bytes = 0;  // in-place tail merges, whole-index merges, index bytes moved
 };
 
 namespace {
@@ -542,6 +552,7 @@ int dsy_ctx_destroy(dsy_ctx* c) {
         if (c->xev) hipEventDestroy(c->xev);
         if (c->aux) hipStreamDestroy(c->aux);
         if (c->pinned) hipHostFree(c->pinned);
+        if (c->in_stage) hipHostFree(c->in_stage);
         hipStreamDestroy(c->stream);
     }
     delete c;
@@ -759,6 +770,7 @@ static int store_index(dsy_store* s, const uint64_t* offsets, const uint64_t* gt
         ++li;
     }
     s->n_live = li;
+    s->n_phys = li;
     return DSY_OK;
 }
 
@@ -971,7 +983,9 @@ int dup_reserve(dsy_ctx* c, dsy_store* s, uint64_t count) {
 }
 
 // insert rows first_row .. first_row+n-1 of the given (member, global_time) host arrays into the table
-int dup_insert(dsy_ctx* c, dsy_store* s, const uint64_t* member, const uint64_t* gt, uint64_t first_row, uint64_t n) {
+// (member, global_time) keys of rows first_row .. first_row+n-1 into the table, from device columns (stream-ordered)
+int dup_insert_dev(dsy_ctx* c, dsy_store* s, const uint64_t* d_member, const uint64_t* d_gt, uint64_t first_row,
+                   uint64_t n) {
     int rc;
     if (!n) return DSY_OK;
     if ((rc = dup_reserve(c, s, s->dup_count + n))) return rc;
@@ -986,83 +1000,63 @@ int dup_insert(dsy_ctx* c, dsy_store* s, const uint64_t* member, const uint64_t*
         s->dup_keys = (DupKey*)nk;
         s->keys_cap = cap;
     }
+    HIP_TRY(launch_dup_insert(d_member, d_gt, first_row, n, s->dup, s->dup_cap - 1, s->dup_keys, c->stream));
+    s->dup_count += n;
+    return DSY_OK;
+}
+
+// the same from host columns
+int dup_insert(dsy_ctx* c, dsy_store* s, const uint64_t* member, const uint64_t* gt, uint64_t first_row, uint64_t n) {
+    int rc;
+    if (!n) return DSY_OK;
     void* d;
     if ((rc = ws_get(c, "dup_keys", n * 16, &d))) return rc;
     HIP_TRY(hipMemcpyAsync(d, member, n * 8, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync((uint64_t*)d + n, gt, n * 8, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(launch_dup_insert((const uint64_t*)d, (const uint64_t*)d + n, first_row, n, s->dup, s->dup_cap - 1,
-                              s->dup_keys, c->stream));
+    if ((rc = dup_insert_dev(c, s, (const uint64_t*)d, (const uint64_t*)d + n, first_row, n))) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
-    s->dup_count += n;
     return DSY_OK;
 }
 
 }  // namespace
 
-// New live-index entries: rows (store positions, any order) with their meta and global time join the index at their
-// (meta_message, global_time, row) place -- appended rows (positions past every stored row: after the stored rows of
-// equal global time) and redone rows alike -- merged on the device into the spare buffer pair, which then becomes the
-// index.  check_present: fail (index unchanged) when a row is in the index already.  Caller holds the ctx lock.
-static int live_insert(dsy_ctx* c, dsy_store* s, const uint32_t* meta, const uint64_t* gt, const uint64_t* row,
-                       uint64_t a, bool check_present) {
-    if (!a) return DSY_OK;
-    // the new entries in index order (meta_message, global_time, row)
-    std::vector<uint64_t> ord(a);
-    for (uint64_t j = 0; j < a; ++j) ord[j] = j;
-    std::sort(ord.begin(), ord.end(), [&](uint64_t x, uint64_t y) {
-        return meta[x] != meta[y] ? meta[x] < meta[y] : gt[x] != gt[y] ? gt[x] < gt[y] : row[x] < row[y];
-    });
-    // each entry's meta segment in the old live index; a new meta sits after every smaller meta's segment
-    std::vector<std::pair<uint32_t, std::pair<uint64_t, uint64_t>>> old(s->segs.begin(), s->segs.end());
-    std::sort(old.begin(), old.end());
-    std::vector<IngestRow> rows(a);
-    for (uint64_t t = 0; t < a; ++t) {
-        const uint64_t j = ord[t];
-        auto it = s->segs.find(meta[j]);
-        uint64_t sa, sb;
-        if (it != s->segs.end()) {
-            sa = it->second.first, sb = it->second.second;
-        } else {
-            sa = 0;
-            for (auto& e : old)
-                if (e.first < meta[j]) sa = std::max(sa, e.second.second);
-            sb = sa;
-        }
-        rows[t] = IngestRow{gt[j], sa, sb, row[j]};
-    }
-    const size_t b_rows = a * sizeof(IngestRow);
-    void* d_up;
-    int rc;
-    if ((rc = ws_get(c, "live_insert", b_rows + a * 8 + 64, &d_up))) return rc;
-    uint8_t* up_rows = (uint8_t*)d_up;
-    unsigned int* d_present = (unsigned int*)(up_rows + b_rows + a * 8);
-    HIP_TRY(hipMemcpyAsync(up_rows, rows.data(), b_rows, hipMemcpyHostToDevice, c->stream));
-    if (check_present) HIP_TRY(hipMemsetAsync(d_present, 0, 4, c->stream));
-    // the live index, merged into fresh buffers (the old ones are read by the merge); double-buffered: the previous
-    // merge's index becomes the next one's target, so a steady stream of appends allocates nothing
-    const uint64_t live = s->n_live + a;
-    if (s->spare_cap < live) {
-        store_release(s, s->spare_gt);
-        store_release(s, s->spare_row);
-        s->spare_gt = s->spare_row = nullptr;
-        s->spare_cap = 0;
-        const uint64_t cap = grown(live, s->n_live);
-        void *pg, *pr;
-        if (hipMalloc(&pg, cap * 8) != hipSuccess) return fail(DSY_ENOMEM, "store live index growth");
-        s->owned.push_back(pg);
-        if (hipMalloc(&pr, cap * 8) != hipSuccess) { store_release(s, pg); return fail(DSY_ENOMEM, "store live index growth"); }
-        s->owned.push_back(pr);
-        s->spare_gt = (uint64_t*)pg;
-        s->spare_row = (uint64_t*)pr;
-        s->spare_cap = cap;
-    }
-    HIP_TRY(launch_ingest_merge(s->d_live_gt, s->d_live_row, s->n_live, (const IngestRow*)up_rows, a,
-                                (uint64_t*)(up_rows + b_rows), s->spare_gt, s->spare_row,
-                                check_present ? d_present : nullptr, c->max_grid, c->stream));
-    unsigned int present = 0;
-    if (check_present) HIP_TRY(hipMemcpyAsync(&present, d_present, 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    if (present) return fail(DSY_EINVAL, "a row to insert is in the live index already");
+// The live index: per meta, in meta order, a region [a, next meta's a) (the last: [a, n_phys)) holding its live
+// entries [a, b) in (global_time, row) order and then slack entries (row kGapRow) that appends fill in place.
+static uint64_t region_end(const dsy_store* s, uint32_t meta) {
+    uint64_t end = s->n_phys;
+    for (auto& e : s->segs)
+        if (e.first > meta) end = std::min(end, e.second.first);
+    return end;
+}
+
+// a meta's live segment, or -- for a meta without one -- the empty segment at its place (the next meta's region start)
+static std::pair<uint64_t, uint64_t> seg_or_place(const dsy_store* s, uint32_t meta) {
+    auto it = s->segs.find(meta);
+    if (it != s->segs.end()) return it->second;
+    const uint64_t p = region_end(s, meta);
+    return {p, p};
+}
+
+static int spare_reserve(dsy_store* s, uint64_t need, uint64_t have) {
+    if (s->spare_cap >= need) return DSY_OK;
+    store_release(s, s->spare_gt);
+    store_release(s, s->spare_row);
+    s->spare_gt = s->spare_row = nullptr;
+    s->spare_cap = 0;
+    const uint64_t cap = grown(need, have);
+    void *pg, *pr;
+    if (hipMalloc(&pg, cap * 8) != hipSuccess) return fail(DSY_ENOMEM, "store live index growth");
+    s->owned.push_back(pg);
+    if (hipMalloc(&pr, cap * 8) != hipSuccess) { store_release(s, pg); return fail(DSY_ENOMEM, "store live index growth"); }
+    s->owned.push_back(pr);
+    s->spare_gt = (uint64_t*)pg;
+    s->spare_row = (uint64_t*)pr;
+    s->spare_cap = cap;
+    return DSY_OK;
+}
+
+// the spare buffer pair holds the new index: swap (double-buffered -- the previous index becomes the next target)
+static void spare_swap(dsy_store* s) {
     uint64_t* prev_gt = const_cast<uint64_t*>(s->d_live_gt);
     uint64_t* prev_row = const_cast<uint64_t*>(s->d_live_row);
     const uint64_t prev_cap = s->live_cap;
@@ -1079,40 +1073,205 @@ static int live_insert(dsy_ctx* c, dsy_store* s, const uint32_t* meta, const uin
         s->spare_gt = s->spare_row = nullptr;
         s->spare_cap = 0;
     }
-    // segments: a meta's segment moves by the new entries of smaller metas and grows by its own
-    std::map<uint32_t, uint64_t> cnt;
-    for (uint64_t j = 0; j < a; ++j) ++cnt[meta[j]];
-    for (auto& e : s->segs) {
-        uint64_t before = 0;
-        for (auto& m : cnt)
-            if (m.first < e.first) before += m.second;
+}
+
+// Merge `a` entries -- device IngestRows in (meta_message, global_time, row) order; cnt: per meta (live entries, slack
+// entries), the slack ones last in their meta and ranked at its region's end -- into the whole index on the device,
+// into the spare buffer pair, which then becomes the index.  check_present: fail (index unchanged) when a row is in the
+// index already.  Caller holds the ctx lock.
+static int live_merge(dsy_ctx* c, dsy_store* s, const IngestRow* d_rows, uint64_t a,
+                      const std::map<uint32_t, std::pair<uint64_t, uint64_t>>& cnt, bool check_present) {
+    if (!a) return DSY_OK;
+    void* d_tmp;
+    int rc;
+    if ((rc = ws_get(c, "live_merge", a * 8 + 64, &d_tmp))) return rc;
+    uint64_t* d_rank = (uint64_t*)d_tmp;
+    unsigned int* d_present = (unsigned int*)(d_rank + a);
+    if (check_present) HIP_TRY(hipMemsetAsync(d_present, 0, 4, c->stream));
+    const uint64_t phys = s->n_phys + a;
+    if ((rc = spare_reserve(s, phys, s->n_phys))) return rc;
+    HIP_TRY(launch_ingest_merge(s->d_live_gt, s->d_live_row, s->n_phys, d_rows, a, d_rank, s->spare_gt, s->spare_row,
+                                check_present ? d_present : nullptr, c->max_grid, c->stream));
+    unsigned int present = 0;
+    if (check_present) HIP_TRY(hipMemcpyAsync(&present, d_present, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (present) return fail(DSY_EINVAL, "a row to insert is in the live index already");
+    spare_swap(s);
+    // segments: a meta's segment moves by every entry of the smaller metas and grows by its own live ones; a meta new
+    // to the index starts at its place
+    std::map<uint32_t, std::pair<uint64_t, uint64_t>> all;
+    for (auto& e : s->segs) all[e.first] = e.second;
+    for (auto& m : cnt)
+        if (!all.count(m.first)) all[m.first] = seg_or_place(s, m.first);
+    uint64_t before = 0, live_add = 0;
+    for (auto& e : all) {
         auto own = cnt.find(e.first);
-        e.second.first += before;
-        e.second.second += before + (own == cnt.end() ? 0 : own->second);
+        const uint64_t real = own == cnt.end() ? 0 : own->second.first;
+        const uint64_t gap = own == cnt.end() ? 0 : own->second.second;
+        s->segs[e.first] = {e.second.first + before, e.second.second + before + real};
+        before += real + gap;
+        live_add += real;
     }
-    for (auto& m : cnt) {
-        if (s->segs.count(m.first)) continue;
-        uint64_t start = 0;
-        for (auto& e : old)
-            if (e.first < m.first) start = std::max(start, e.second.second);
-        for (auto& m2 : cnt)
-            if (m2.first < m.first) start += m2.second;
-        s->segs[m.first] = {start, start + m.second};
-    }
-    s->n_live = live;
+    s->n_live += live_add;
+    s->n_phys = phys;
+    s->ix_full += 1;
+    s->ix_bytes += 32 * (s->n_phys - a) + 48 * a;  // the old index read and written, the new entries read and written
     return DSY_OK;
 }
 
-// Merge the rows appended since the last read into the live index (one device merge, live_insert).  Every reader of
-// the index calls it first; the caller holds the ctx lock and nothing is in flight on the store.
+// New live-index entries given on the host: rows (store positions, any order) with their meta and global time join
+// the index at their (meta_message, global_time, row) place -- redone rows (dsy_store_set_undone).  Caller holds the
+// ctx lock.
+static int live_insert(dsy_ctx* c, dsy_store* s, const uint32_t* meta, const uint64_t* gt, const uint64_t* row,
+                       uint64_t a, bool check_present) {
+    if (!a) return DSY_OK;
+    // the new entries in index order (meta_message, global_time, row)
+    std::vector<uint64_t> ord(a);
+    for (uint64_t j = 0; j < a; ++j) ord[j] = j;
+    std::sort(ord.begin(), ord.end(), [&](uint64_t x, uint64_t y) {
+        return meta[x] != meta[y] ? meta[x] < meta[y] : gt[x] != gt[y] ? gt[x] < gt[y] : row[x] < row[y];
+    });
+    std::vector<IngestRow> rows(a);
+    std::map<uint32_t, std::pair<uint64_t, uint64_t>> cnt;
+    for (uint64_t t = 0; t < a; ++t) {
+        const uint64_t j = ord[t];
+        const auto sg = seg_or_place(s, meta[j]);
+        rows[t] = IngestRow{gt[j], sg.first, sg.second, row[j]};
+        ++cnt[meta[j]].first;
+    }
+    void* d_rows;
+    int rc;
+    if ((rc = ws_get(c, "live_insert", a * sizeof(IngestRow), &d_rows))) return rc;
+    HIP_TRY(hipMemcpyAsync(d_rows, rows.data(), a * sizeof(IngestRow), hipMemcpyHostToDevice, c->stream));
+    return live_merge(c, s, (const IngestRow*)d_rows, a, cnt, check_present);
+}
+
+// slack a meta's region gets when the whole index is re-laid out: a quarter of its entries, at least kSlackMin
+static constexpr uint64_t kSlackMin = 16384;
+
+// Merge the rows appended since the last read into the live index.  Every reader of the index calls it first; the
+// caller holds the ctx lock and nothing is in flight on the store.  The pending (meta, global_time) columns are on the
+// device already (dsy_store_append uploads them with the packets) and are put in index order there (two radix sorts,
+// launch_pend_order).  When every meta's new entries fit its region's slack, each meta's tail from its first new entry
+// on is merged in place -- O(batch + that tail), the common case of new global times at or near the top; otherwise one
+// merge of the whole index lays it out again with fresh slack.
 static int store_flush(dsy_ctx* c, const dsy_store* cs) {
     dsy_store* s = const_cast<dsy_store*>(cs);
-    if (s->pend_row.empty()) return DSY_OK;
-    int rc = live_insert(c, s, s->pend_meta.data(), s->pend_gt.data(), s->pend_row.data(), s->pend_row.size(), false);
-    if (rc) return rc;
-    s->pend_meta.clear();
-    s->pend_gt.clear();
-    s->pend_row.clear();
+    const uint64_t P = s->pend_n;
+    if (!P) return DSY_OK;
+    std::map<uint32_t, uint64_t> cntm(s->pend_cnt.begin(), s->pend_cnt.end());
+    for (auto& e : s->segs) cntm.emplace(e.first, 0);
+    const uint32_t nm = (uint32_t)cntm.size();
+    std::vector<uint32_t> metas;
+    std::vector<uint64_t> segs, ends, cnt, starts, gap_before, extra;
+    bool fast = s->d_live_row != nullptr;
+    uint64_t at = 0, gaps = 0;
+    for (auto& m : cntm) {
+        const bool known = s->segs.count(m.first) != 0;
+        const auto sg = seg_or_place(s, m.first);
+        const uint64_t end = region_end(s, m.first);
+        metas.push_back(m.first);
+        segs.push_back(sg.first);
+        segs.push_back(sg.second);
+        ends.push_back(end);
+        cnt.push_back(m.second);
+        starts.push_back(at);
+        at += m.second;
+        if (m.second && (!known || end - sg.second < m.second)) fast = false;
+        const uint64_t live = sg.second - sg.first, want = std::max(kSlackMin, (live + m.second) / 4);
+        const uint64_t slack = known ? end - sg.second : 0;
+        extra.push_back((live || m.second) && want > slack ? want - slack : 0);
+        gap_before.push_back(gaps);
+        gaps += extra.back();
+    }
+    // the in-place tails need the first ranks; when they would move more than one whole merge does, the whole merge
+    // runs instead (its rows are ordered again, with the slack entries placed)
+    bool tried_fast = false;
+again:
+    const uint64_t total = fast ? P : P + gaps;
+    // 256-byte aligned parts: the metas | segments | gap_before | starts | counts | first ranks | the ordered rows | the
+    // sort's scratch
+    const size_t b_m = ((size_t)nm * 4 + 255) / 256 * 256, b_u = ((size_t)nm * 8 + 255) / 256 * 256;
+    const size_t b_tab = b_m + 2 * b_u + 4 * b_u;
+    const size_t b_scr = pend_order_scratch(P), b_rows = ((size_t)total * sizeof(IngestRow) + 255) / 256 * 256;
+    void* d_tab;
+    int rc;
+    if ((rc = ws_get(c, "pend_order", b_tab + b_rows + b_scr, &d_tab))) return rc;
+    uint8_t* tab = (uint8_t*)d_tab;
+    uint64_t* d_segs = (uint64_t*)(tab + b_m);
+    uint64_t* d_gapb = (uint64_t*)(tab + b_m + 2 * b_u);
+    uint64_t* d_starts = (uint64_t*)(tab + b_m + 3 * b_u);
+    uint64_t* d_cnt = (uint64_t*)(tab + b_m + 4 * b_u);
+    uint64_t* d_first = (uint64_t*)(tab + b_m + 5 * b_u);
+    IngestRow* d_rows = (IngestRow*)(tab + b_tab);
+    {  // one upload of the table (the first ranks are written on the device)
+        std::vector<uint8_t> h(b_m + 5 * b_u);
+        std::memcpy(h.data(), metas.data(), (size_t)nm * 4);
+        std::memcpy(h.data() + b_m, segs.data(), (size_t)nm * 16);
+        std::memcpy(h.data() + b_m + 2 * b_u, gap_before.data(), (size_t)nm * 8);
+        std::memcpy(h.data() + b_m + 3 * b_u, starts.data(), (size_t)nm * 8);
+        std::memcpy(h.data() + b_m + 4 * b_u, cnt.data(), (size_t)nm * 8);
+        HIP_TRY(hipMemcpyAsync(tab, h.data(), h.size(), hipMemcpyHostToDevice, c->stream));
+    }
+    HIP_TRY(launch_pend_order(s->d_pend_meta, s->d_pend_gt, P, s->pend_glo, s->pend_ghi, (const uint32_t*)tab, d_segs,
+                              fast ? nullptr : d_gapb, nm, s->pend_base, (uint8_t*)d_rows + b_rows, b_scr, d_rows,
+                              c->stream));
+    if (!fast) {
+        std::map<uint32_t, std::pair<uint64_t, uint64_t>> cm;
+        for (uint32_t r = 0; r < nm; ++r) {
+            HIP_TRY(launch_gap_rows(d_rows + starts[r] + cnt[r] + gap_before[r], extra[r], ends[r], c->stream));
+            if (cnt[r] || extra[r]) cm[metas[r]] = {cnt[r], extra[r]};
+        }
+        if ((rc = live_merge(c, s, d_rows, total, cm, false))) return rc;
+        s->pend_n = 0;
+        s->pend_cnt.clear();
+        return DSY_OK;
+    }
+    // in place: each meta's tail [p, b) -- p: its first new entry's position -- is copied aside and merged with the
+    // meta's new entries back into [p, b + k), inside the region's slack
+    std::vector<uint64_t> first(nm);
+    HIP_TRY(launch_first_rank(s->d_live_gt, s->d_live_row, d_rows, d_starts, d_cnt, nm, d_first, c->stream));
+    HIP_TRY(hipMemcpyAsync(first.data(), d_first, (size_t)nm * 8, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    uint64_t tail_max = 0, tail_sum = 0;
+    for (uint32_t r = 0; r < nm; ++r)
+        if (cnt[r]) {
+            tail_max = std::max(tail_max, segs[2 * r + 1] - first[r]);
+            tail_sum += segs[2 * r + 1] - first[r];
+        }
+    if (!tried_fast && 48 * tail_sum > 32 * s->n_phys) {  // 48 B per tail entry (copied out, read, written) vs 32
+        tried_fast = true;
+        fast = false;
+        goto again;
+    }
+    void* d_tmp;
+    if ((rc = ws_get(c, "live_merge", P * 8 + 64 + tail_max * 16, &d_tmp))) return rc;
+    uint64_t* d_rank = (uint64_t*)d_tmp;
+    uint64_t* tail_gt = d_rank + P + 8;
+    uint64_t* tail_row = tail_gt + tail_max;
+    uint64_t* live_gt = const_cast<uint64_t*>(s->d_live_gt);
+    uint64_t* live_row = const_cast<uint64_t*>(s->d_live_row);
+    uint64_t moved = 0;
+    for (uint32_t r = 0; r < nm; ++r) {
+        if (!cnt[r]) continue;
+        const uint64_t p = first[r], b = segs[2 * r + 1], L = b - p;
+        if (L) {
+            HIP_TRY(hipMemcpyAsync(tail_gt, live_gt + p, L * 8, hipMemcpyDeviceToDevice, c->stream));
+            HIP_TRY(hipMemcpyAsync(tail_row, live_row + p, L * 8, hipMemcpyDeviceToDevice, c->stream));
+        }
+        HIP_TRY(launch_rows_seg(d_rows + starts[r], cnt[r], 0, L, c->stream));
+        HIP_TRY(launch_ingest_merge(tail_gt, tail_row, L, d_rows + starts[r], cnt[r], d_rank, live_gt + p,
+                                    live_row + p, nullptr, c->max_grid, c->stream));
+        // (the copies on one stream: the next meta's tail copy waits for this merge's reads of the scratch)
+        moved += L;
+        s->segs[metas[r]].second += cnt[r];
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    s->n_live += P;
+    s->ix_fast += 1;
+    s->ix_bytes += 16 * P + 48 * moved;  // the new entries written, each moved tail entry copied out and back
+    s->pend_n = 0;
+    s->pend_cnt.clear();
     return DSY_OK;
 }
 
@@ -1131,14 +1290,34 @@ int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blo
     for (uint64_t j = 0; j < a; ++j) minlen = std::min(minlen, offsets[j + 1] - offsets[j]);
 
     HIP_TRY(hipStreamSynchronize(c->stream));  // nothing in flight reads a buffer that is about to be replaced
+    // the small columns, staged in pinned memory for one upload: [offsets | row records | global times | metas |
+    // members]
+    const size_t b_off = (a + 1) * 8, b_rec = a * sizeof(RowRec), b_gt = a * 8, b_meta = (a * 4 + 15) / 16 * 16,
+                 b_mem = member ? a * 8 : 0, b_cols = b_off + b_rec + b_gt + b_meta + b_mem;
+    if (c->in_stage_bytes < b_cols) {
+        if (c->in_stage) hipHostFree(c->in_stage);
+        c->in_stage = nullptr;
+        c->in_stage_bytes = 0;
+        const size_t want = std::max<size_t>(b_cols + b_cols / 4, 4096);
+        if (hipHostMalloc((void**)&c->in_stage, want, hipHostMallocDefault) != hipSuccess) {
+            c->in_stage = nullptr;
+            return fail(DSY_ENOMEM, "hipHostMalloc(%zu) for the ingest staging failed", want);
+        }
+        c->in_stage_bytes = want;
+    }
+    uint64_t* h_off = (uint64_t*)c->in_stage;
+    RowRec* h_rec = (RowRec*)(c->in_stage + b_off);
     // the line copy the responder hashes from, and its row records
-    std::vector<RowRec> nrec(a);
     uint64_t at = s->lines_used;
     for (uint64_t j = 0; j < a; ++j) {
         const uint64_t len = offsets[j + 1] - offsets[j];
-        nrec[j] = RowRec{at + kLineBias, (uint32_t)len, 0u};
+        h_rec[j] = RowRec{at + kLineBias, (uint32_t)len, 0u};
         at += (len + kLineBias + 127) & ~127ull;
     }
+    for (uint64_t j = 0; j <= a; ++j) h_off[j] = offsets[j] - base0;
+    std::memcpy(c->in_stage + b_off + b_rec, gt, a * 8);
+    std::memcpy(c->in_stage + b_off + b_rec + b_gt, meta, a * 4);
+    if (member) std::memcpy(c->in_stage + b_off + b_rec + b_gt + b_meta, member, a * 8);
     if ((rc = lines_reserve(c, s, at))) return rc;
     if (n0 + a > s->rec_cap) {
         const uint64_t cap = grown(n0 + a, s->rec_cap);
@@ -1151,29 +1330,62 @@ int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blo
         s->d_rec = (const RowRec*)nr;
         s->rec_cap = cap;
     }
+    // the new rows join the live index (positions n0 .. n0+a-1: after every stored row of equal global time) at the
+    // next read of the index (store_flush): their (meta, global_time) entries wait on the device
+    if (s->pend_n + a > s->pend_cap) {
+        const uint64_t cap = grown(s->pend_n + a, s->pend_cap);
+        void *pg, *pm;
+        if (hipMalloc(&pg, cap * 8) != hipSuccess) return fail(DSY_ENOMEM, "store pending index growth");
+        if (hipMalloc(&pm, cap * 4) != hipSuccess) { hipFree(pg); return fail(DSY_ENOMEM, "store pending index growth"); }
+        if (s->pend_n) {
+            HIP_TRY(hipMemcpyAsync(pg, s->d_pend_gt, s->pend_n * 8, hipMemcpyDeviceToDevice, c->stream));
+            HIP_TRY(hipMemcpyAsync(pm, s->d_pend_meta, s->pend_n * 4, hipMemcpyDeviceToDevice, c->stream));
+        }
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        store_release(s, s->d_pend_gt);
+        store_release(s, s->d_pend_meta);
+        s->owned.push_back(pg);
+        s->owned.push_back(pm);
+        s->d_pend_gt = (uint64_t*)pg;
+        s->d_pend_meta = (uint32_t*)pm;
+        s->pend_cap = cap;
+    }
 
-    // staged uploads (one workspace): the packets, their offsets and records; the packets then move to their
-    // line-aligned places
-    std::vector<uint64_t> noff(a + 1);
-    for (uint64_t j = 0; j <= a; ++j) noff[j] = offsets[j] - base0;
-    const size_t b_blob = (add + 15) / 16 * 16, b_off = (a + 1) * 8, b_rec = a * sizeof(RowRec);
+    // uploads (one workspace): the packets from the caller's buffer, the staged columns in one copy; the packets then
+    // move to their line-aligned places
+    const size_t b_blob = (add + 15) / 16 * 16;
     void* d_up;
-    if ((rc = ws_get(c, "ingest", b_blob + b_off + b_rec, &d_up))) return rc;
+    if ((rc = ws_get(c, "ingest", b_blob + b_cols, &d_up))) return rc;
     uint8_t* up = (uint8_t*)d_up;
     uint8_t* up_off = up + b_blob;
     uint8_t* up_rec = up_off + b_off;
+    uint8_t* up_gt = up_rec + b_rec;
+    uint8_t* up_meta = up_gt + b_gt;
+    uint8_t* up_mem = up_meta + b_meta;
     if (add) HIP_TRY(hipMemcpyAsync(up, blob + base0, add, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(up_off, noff.data(), b_off, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(up_rec, nrec.data(), b_rec, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(up_off, c->in_stage, b_cols, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(const_cast<RowRec*>(s->d_rec) + n0, up_rec, b_rec, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(s->d_pend_gt + s->pend_n, up_gt, b_gt, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(s->d_pend_meta + s->pend_n, up_meta, a * 4, hipMemcpyDeviceToDevice, c->stream));
     HIP_TRY(launch_store_lines(up, (const uint64_t*)up_off, s->d_rec + n0, a, const_cast<uint8_t*>(s->d_lines),
                                c->stream));
-    // the new rows join the live index (positions n0 .. n0+a-1: after every stored row of equal global time) at the
-    // next read of the index (store_flush): a stream of appends costs O(batch) each and one merge in all
-    s->pend_meta.insert(s->pend_meta.end(), meta, meta + a);
-    s->pend_gt.insert(s->pend_gt.end(), gt, gt + a);
-    for (uint64_t j = 0; j < a; ++j) s->pend_row.push_back(n0 + j);
-    if (s->dup && (rc = dup_insert(c, s, member, gt, n0, a))) return rc;
+    if (!s->pend_n) {
+        s->pend_base = n0;
+        s->pend_glo = ~0ull;
+        s->pend_ghi = 0;
+    }
+    for (uint64_t j = 0; j < a; ++j) {
+        s->pend_glo = std::min(s->pend_glo, gt[j]);
+        s->pend_ghi = std::max(s->pend_ghi, gt[j]);
+    }
+    for (uint64_t j = 0; j < a;) {  // runs of one meta: one map update each
+        uint64_t e = j + 1;
+        while (e < a && meta[e] == meta[j]) ++e;
+        s->pend_cnt[meta[j]] += e - j;
+        j = e;
+    }
+    s->pend_n += a;
+    if (s->dup && (rc = dup_insert_dev(c, s, (const uint64_t*)up_mem, (const uint64_t*)up_gt, n0, a))) return rc;
     s->min_len = n0 ? std::min(s->min_len, minlen) : minlen;
     s->n += a;
     s->blob_len += add;
@@ -1181,6 +1393,17 @@ int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blo
     return DSY_OK;
 }
 
+
+int dsy_store_index_stats(const dsy_store* s, uint64_t* out) {
+    if (!s || !out) return fail(DSY_EINVAL, "NULL argument");
+    out[0] = s->n_live;
+    out[1] = s->n_phys;
+    out[2] = s->ix_fast;
+    out[3] = s->ix_full;
+    out[4] = s->ix_bytes;
+    out[5] = s->pend_n;
+    return DSY_OK;
+}
 
 int dsy_store_prune(dsy_ctx* c, dsy_store* s, uint32_t meta, uint64_t max_gt, uint64_t* out_deleted) {
     if (!c || !s || !out_deleted) return fail(DSY_EINVAL, "NULL argument");
@@ -1202,45 +1425,17 @@ int dsy_store_prune(dsy_ctx* c, dsy_store* s, uint32_t meta, uint64_t max_gt, ui
     if (!k) return DSY_OK;
     // the deleted rows leave the (member, global_time) table too: a later lookup finds nothing (dispersy.py:868)
     if (s->dup) HIP_TRY(launch_dup_erase(nullptr, s->d_live_row, a, k, s->dup_keys, s->dup, s->dup_cap - 1, c->stream));
-    const uint64_t live = s->n_live - k;
-    if (s->spare_cap < live) {  // the ingest's second buffer pair is the target, as for a merge
-        store_release(s, s->spare_gt);
-        store_release(s, s->spare_row);
-        s->spare_gt = s->spare_row = nullptr;
-        s->spare_cap = 0;
-        const uint64_t cap = grown(s->n_live, s->n_live);
-        void *pg, *pr;
-        if (hipMalloc(&pg, cap * 8) != hipSuccess) return fail(DSY_ENOMEM, "store live index");
-        s->owned.push_back(pg);
-        if (hipMalloc(&pr, cap * 8) != hipSuccess) { store_release(s, pg); return fail(DSY_ENOMEM, "store live index"); }
-        s->owned.push_back(pr);
-        s->spare_gt = (uint64_t*)pg;
-        s->spare_row = (uint64_t*)pr;
-        s->spare_cap = cap;
-    }
-    HIP_TRY(launch_live_cut(s->d_live_gt, s->d_live_row, live, a, k, s->spare_gt, s->spare_row, c->max_grid, c->stream));
+    const uint64_t n_out = s->n_phys - k;  // the index arrays without the k entries (slack included)
+    if ((rc = spare_reserve(s, std::max<uint64_t>(n_out, 1), s->n_phys))) return rc;
+    HIP_TRY(launch_live_cut(s->d_live_gt, s->d_live_row, n_out, a, k, s->spare_gt, s->spare_row, c->max_grid, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    uint64_t* prev_gt = const_cast<uint64_t*>(s->d_live_gt);
-    uint64_t* prev_row = const_cast<uint64_t*>(s->d_live_row);
-    const uint64_t prev_cap = s->live_cap;
-    s->d_live_gt = s->spare_gt;
-    s->d_live_row = s->spare_row;
-    s->live_cap = s->spare_cap;
-    if (prev_cap) {
-        s->spare_gt = prev_gt;
-        s->spare_row = prev_row;
-        s->spare_cap = prev_cap;
-    } else {
-        store_release(s, prev_gt);
-        store_release(s, prev_row);
-        s->spare_gt = s->spare_row = nullptr;
-        s->spare_cap = 0;
-    }
+    spare_swap(s);
     for (auto& e : s->segs) {  // this meta's segment loses its first k rows; later segments move down by k
         if (e.first == meta) e.second.second -= k;
         else if (e.second.first >= b) { e.second.first -= k; e.second.second -= k; }
     }
-    s->n_live = live;
+    s->n_live -= k;
+    s->n_phys = n_out;
     *out_deleted = k;
     return DSY_OK;
 }
@@ -1259,8 +1454,8 @@ static int live_remove(dsy_ctx* c, dsy_store* s, const uint64_t* rows, uint64_t 
         bounds.push_back(e.second.first);
         bounds.push_back(e.second.second);
     }
-    bounds.push_back(s->n_live);
-    const uint64_t words = (s->n + 31) / 32, tiles = (s->n_live + kDelTile - 1) / kDelTile;
+    bounds.push_back(s->n_phys);
+    const uint64_t words = (s->n + 31) / 32, tiles = (s->n_phys + kDelTile - 1) / kDelTile;
     const size_t b_bits = (words * 4 + 15) / 16 * 16, b_rows = k * 8, b_tiles = (tiles + 1) * 8,
                  b_bounds = bounds.size() * 8;
     void* d;
@@ -1276,47 +1471,19 @@ static int live_remove(dsy_ctx* c, dsy_store* s, const uint64_t* rows, uint64_t 
     HIP_TRY(launch_mark_rows(d_rows, k, s->n, d_bits, c->stream));
     // the deleted rows' (member, global_time) slots become tombstones (also rows outside the live index: undone ones)
     if (erase_dup && s->dup) HIP_TRY(launch_dup_erase(d_rows, nullptr, 0, k, s->dup_keys, s->dup, s->dup_cap - 1, c->stream));
-    const uint64_t cap_need = std::max<uint64_t>(s->n_live, 1);
-    if (s->spare_cap < cap_need) {  // the ingest's second buffer pair is the target, as for a merge
-        store_release(s, s->spare_gt);
-        store_release(s, s->spare_row);
-        s->spare_gt = s->spare_row = nullptr;
-        s->spare_cap = 0;
-        const uint64_t cap = grown(cap_need, s->n_live);
-        void *pg, *pr;
-        if (hipMalloc(&pg, cap * 8) != hipSuccess) return fail(DSY_ENOMEM, "store live index");
-        s->owned.push_back(pg);
-        if (hipMalloc(&pr, cap * 8) != hipSuccess) { store_release(s, pg); return fail(DSY_ENOMEM, "store live index"); }
-        s->owned.push_back(pr);
-        s->spare_gt = (uint64_t*)pg;
-        s->spare_row = (uint64_t*)pr;
-        s->spare_cap = cap;
-    }
-    HIP_TRY(launch_live_delete(s->d_live_gt, s->d_live_row, s->n_live, d_bits, d_tiles, s->spare_gt, s->spare_row,
+    // (the compaction drops the slack entries too: the new index is dense)
+    if ((rc = spare_reserve(s, std::max<uint64_t>(s->n_phys, 1), s->n_phys))) return rc;
+    HIP_TRY(launch_live_delete(s->d_live_gt, s->d_live_row, s->n_phys, d_bits, d_tiles, s->spare_gt, s->spare_row,
                                d_bounds, (uint32_t)bounds.size(), c->stream));
     HIP_TRY(hipMemcpyAsync(bounds.data(), d_bounds, b_bounds, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     const uint64_t live = bounds.back();
     *out_deleted = s->n_live - live;
     if (live == s->n_live) return DSY_OK;  // none of the rows was in the live index: the old index stays
-    uint64_t* prev_gt = const_cast<uint64_t*>(s->d_live_gt);
-    uint64_t* prev_row = const_cast<uint64_t*>(s->d_live_row);
-    const uint64_t prev_cap = s->live_cap;
-    s->d_live_gt = s->spare_gt;
-    s->d_live_row = s->spare_row;
-    s->live_cap = s->spare_cap;
-    if (prev_cap) {
-        s->spare_gt = prev_gt;
-        s->spare_row = prev_row;
-        s->spare_cap = prev_cap;
-    } else {
-        store_release(s, prev_gt);
-        store_release(s, prev_row);
-        s->spare_gt = s->spare_row = nullptr;
-        s->spare_cap = 0;
-    }
+    spare_swap(s);
     for (size_t j = 0; j < seg_ids.size(); ++j) s->segs[seg_ids[j]] = {bounds[2 * j], bounds[2 * j + 1]};
     s->n_live = live;
+    s->n_phys = live;
     return DSY_OK;
 }
 
@@ -2046,7 +2213,8 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const Clai
             d.prefix = d_pre + at;
             d.prefix_word = 0;
             for (uint32_t j = 0; j < std::min<uint32_t>(q.prefix_len, 4); ++j) d.prefix_word |= (uint32_t)q.prefix[j] << (8 * j);
-            d.pad[0] = d.pad[1] = d.pad[2] = 0;
+            d.m_recip = mod_recip(q.m_bits);
+            d.pad[0] = d.pad[1] = 0;
             std::memcpy(h_pre + at, q.prefix, q.prefix_len);
             at += q.prefix_len;
             dq[r] = d;

@@ -184,7 +184,8 @@ struct DevRequest {
     uint32_t modulo, offset, k, hash_kind, chunk_bytes, prefix_len;
     const uint8_t* prefix;  // device pointer into the call's prefix buffer
     uint32_t prefix_word;   // the first min(prefix_len, 4) prefix bytes, little-endian (the LDS-DMA paths' prefix)
-    uint32_t pad[3];
+    uint32_t m_recip;       // mod_recip(m_bits): bit positions by multiply-high (dsy_message.h bit_position)
+    uint32_t pad[2];
 };
 
 struct SegMeta {          // one syncable meta in serving order, resolved against the store
@@ -354,6 +355,22 @@ hipError_t launch_live_delete(const uint64_t* live_gt, const uint64_t* live_row,
 hipError_t launch_ingest_merge(const uint64_t* live_gt, const uint64_t* live_row, uint64_t n_live,
                                const IngestRow* rows, uint64_t a, uint64_t* rank, uint64_t* out_gt, uint64_t* out_row,
                                unsigned int* present, uint32_t max_grid, hipStream_t stream);
+// the P pending index entries (meta[j], gt[j], row base + j), glo <= gt <= ghi, as IngestRows in (meta, global_time,
+// row) order; metas: the nm distinct pending metas ascending, segs: their live segments (a, b) in the old index
+// (gap_before, optional: slack rows kept before rank r's rows -- the caller fills them, launch_gap_rows)
+size_t pend_order_scratch(uint64_t P);
+hipError_t launch_pend_order(const uint32_t* meta, const uint64_t* gt, uint64_t P, uint64_t glo, uint64_t ghi,
+                             const uint32_t* metas, const uint64_t* segs, const uint64_t* gap_before, uint32_t nm,
+                             uint64_t base, void* scratch, size_t scratch_bytes, IngestRow* out, hipStream_t stream);
+// The live index keeps slack after each meta's live segment: entries [b, next meta's a) hold row kGapRow.  An append
+// whose new entries fit its metas' slack merges each meta's tail in place (O(batch + the tail after its first new
+// entry)); otherwise one merge of the whole index re-lays it out with fresh slack (k_gap_rows' entries).
+static constexpr uint64_t kGapRow = ~0ull;
+hipError_t launch_gap_rows(IngestRow* out, uint64_t k, uint64_t end, hipStream_t stream);
+hipError_t launch_first_rank(const uint64_t* live_gt, const uint64_t* live_row, const IngestRow* rows,
+                             const uint64_t* starts, const uint64_t* counts, uint32_t nm, uint64_t* out,
+                             hipStream_t stream);
+hipError_t launch_rows_seg(IngestRow* rows, uint64_t k, uint64_t sa, uint64_t sb, hipStream_t stream);
 
 // ---------------------------------------------------------------------------------------- simulator
 static constexpr uint32_t kSimFilterWordsMax = 2048;  // m <= 65536 bits

@@ -12,6 +12,9 @@
 // Every output slot is written exactly once; reads and writes of the old index stream (16 B in, 16 B out per row).
 #include "dsy_kernels.h"
 
+#include <algorithm>
+#include <rocprim/device/device_radix_sort.hpp>
+
 namespace dsy {
 
 static constexpr uint32_t kIngestThreads = 256;
@@ -126,6 +129,153 @@ hipError_t launch_live_cut(const uint64_t* live_gt, const uint64_t* live_row, ui
     return hipGetLastError();
 }
 
+// ---- pending entries (rows appended since the index was last read) in index order, on the device: two stable radix
+// sorts of the entry numbers j, by global time and then by the meta's rank among the pending metas, leave equal
+// (meta, global_time) entries in j order = row order (row = base + j).  The host sorted them before (~6 ms for
+// 110 k entries on one core, the whole cost of the deferred merge).
+__global__ void __launch_bounds__(kIngestThreads) k_pend_key_gt(const uint64_t* __restrict__ gt, uint64_t P,
+                                                                 uint64_t glo, uint64_t* __restrict__ key,
+                                                                 uint32_t* __restrict__ idx) {
+    const uint64_t j = (uint64_t)blockIdx.x * kIngestThreads + threadIdx.x;
+    if (j >= P) return;
+    key[j] = gt[j] - glo;
+    idx[j] = (uint32_t)j;
+}
+
+// rank of a meta in the sorted table of the pending metas (it is there: the table holds every pending meta)
+__device__ __forceinline__ uint32_t meta_rank(const uint32_t* __restrict__ metas, uint32_t nm, uint32_t m) {
+    uint32_t lo = 0, hi = nm;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (metas[mid] < m) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(kIngestThreads) k_pend_key_meta(const uint32_t* __restrict__ meta, uint64_t P,
+                                                                   const uint32_t* __restrict__ order,
+                                                                   const uint32_t* __restrict__ metas, uint32_t nm,
+                                                                   uint64_t* __restrict__ key) {
+    const uint64_t t = (uint64_t)blockIdx.x * kIngestThreads + threadIdx.x;
+    if (t >= P) return;
+    key[t] = meta_rank(metas, nm, meta[order[t]]);
+}
+
+// gap_before (optional): slack entries placed before meta rank r's rows (after each smaller meta's own rows)
+__global__ void __launch_bounds__(kIngestThreads) k_pend_rows(const uint32_t* __restrict__ meta,
+                                                               const uint64_t* __restrict__ gt, uint64_t P,
+                                                               const uint32_t* __restrict__ order,
+                                                               const uint32_t* __restrict__ metas, uint32_t nm,
+                                                               const uint64_t* __restrict__ segs,
+                                                               const uint64_t* __restrict__ gap_before, uint64_t base,
+                                                               IngestRow* __restrict__ out) {
+    const uint64_t t = (uint64_t)blockIdx.x * kIngestThreads + threadIdx.x;
+    if (t >= P) return;
+    const uint32_t j = order[t];
+    const uint32_t r = meta_rank(metas, nm, meta[j]);
+    out[t + (gap_before ? gap_before[r] : 0)] = IngestRow{gt[j], segs[2 * r], segs[2 * r + 1], base + j};
+}
+
+// slack entries of one meta's region: ranked at the region's end (rank = seg_a = seg_b = end), row kGapRow
+__global__ void __launch_bounds__(kIngestThreads) k_gap_rows(IngestRow* __restrict__ out, uint64_t k, uint64_t end) {
+    const uint64_t t = (uint64_t)blockIdx.x * kIngestThreads + threadIdx.x;
+    if (t < k) out[t] = IngestRow{0, end, end, kGapRow};
+}
+
+// per meta r with pending entries: the position of its first (smallest) new entry in its live segment -- where the
+// in-place merge of the segment's tail starts (starts[r]: its first row in the ordered pending rows)
+__global__ void k_first_rank(const uint64_t* __restrict__ live_gt, const uint64_t* __restrict__ live_row,
+                             const IngestRow* __restrict__ rows, const uint64_t* __restrict__ starts,
+                             const uint64_t* __restrict__ counts, uint32_t nm, uint64_t* __restrict__ out) {
+    const uint32_t r = blockIdx.x * 64 + threadIdx.x;
+    if (r >= nm) return;
+    if (!counts[r]) { out[r] = 0; return; }
+    const IngestRow q = rows[starts[r]];
+    uint64_t lo = q.seg_a, hi = q.seg_b;
+    while (lo < hi) {
+        const uint64_t mid = lo + ((hi - lo) >> 1);
+        const uint64_t g = live_gt[mid], w = live_row[mid];
+        if (g < q.gt || (g == q.gt && w < q.row)) lo = mid + 1; else hi = mid;
+    }
+    out[r] = lo;
+}
+
+// rebase k ordered rows onto a segment [sa, sb) of a copied tail
+__global__ void __launch_bounds__(kIngestThreads) k_rows_seg(IngestRow* __restrict__ rows, uint64_t k, uint64_t sa,
+                                                              uint64_t sb) {
+    const uint64_t t = (uint64_t)blockIdx.x * kIngestThreads + threadIdx.x;
+    if (t < k) {
+        rows[t].seg_a = sa;
+        rows[t].seg_b = sb;
+    }
+}
+
+static int bit_width(uint64_t x) {
+    int b = 0;
+    while (b < 64 && (x >> b)) ++b;
+    return b;
+}
+
+// scratch: keys 2 x P u64, order 2 x P u32, then the radix sort's temporary storage
+size_t pend_order_scratch(uint64_t P) {
+    size_t tmp = 0;
+    rocprim::radix_sort_pairs(nullptr, tmp, (const uint64_t*)nullptr, (uint64_t*)nullptr, (const uint32_t*)nullptr,
+                              (uint32_t*)nullptr, (size_t)P, 0u, 64u, nullptr);
+    return (size_t)P * 24 + 256 + tmp;
+}
+
+hipError_t launch_pend_order(const uint32_t* meta, const uint64_t* gt, uint64_t P, uint64_t glo, uint64_t ghi,
+                             const uint32_t* metas, const uint64_t* segs, const uint64_t* gap_before, uint32_t nm,
+                             uint64_t base, void* scratch, size_t scratch_bytes, IngestRow* out, hipStream_t stream) {
+    if (!P) return hipSuccess;
+    uint64_t* key_a = (uint64_t*)scratch;
+    uint64_t* key_b = key_a + P;
+    uint32_t* ord_a = (uint32_t*)(key_b + P);
+    uint32_t* ord_b = ord_a + P;
+    void* tmp = (uint8_t*)scratch + (((size_t)P * 24 + 255) & ~(size_t)255);
+    size_t tmp_bytes = scratch_bytes - (((size_t)P * 24 + 255) & ~(size_t)255);
+    const uint32_t g = (uint32_t)((P + kIngestThreads - 1) / kIngestThreads);
+    hipLaunchKernelGGL(k_pend_key_gt, dim3(g), dim3(kIngestThreads), 0, stream, gt, P, glo, key_a, ord_a);
+    hipError_t e = rocprim::radix_sort_pairs(tmp, tmp_bytes, key_a, key_b, ord_a, ord_b, (size_t)P, 0u,
+                                             (unsigned)std::max(1, bit_width(ghi - glo)), stream);
+    if (e != hipSuccess) return e;
+    const uint32_t* order = ord_b;
+    if (nm > 1) {
+        hipLaunchKernelGGL(k_pend_key_meta, dim3(g), dim3(kIngestThreads), 0, stream, meta, P, ord_b, metas, nm,
+                           key_a);
+        e = rocprim::radix_sort_pairs(tmp, tmp_bytes, key_a, key_b, ord_b, ord_a, (size_t)P, 0u,
+                                      (unsigned)bit_width(nm - 1), stream);
+        if (e != hipSuccess) return e;
+        order = ord_a;
+    }
+    hipLaunchKernelGGL(k_pend_rows, dim3(g), dim3(kIngestThreads), 0, stream, meta, gt, P, order, metas, nm, segs,
+                       gap_before, base, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_gap_rows(IngestRow* out, uint64_t k, uint64_t end, hipStream_t stream) {
+    if (!k) return hipSuccess;
+    hipLaunchKernelGGL(k_gap_rows, dim3((uint32_t)((k + kIngestThreads - 1) / kIngestThreads)), dim3(kIngestThreads), 0,
+                       stream, out, k, end);
+    return hipGetLastError();
+}
+
+hipError_t launch_first_rank(const uint64_t* live_gt, const uint64_t* live_row, const IngestRow* rows,
+                             const uint64_t* starts, const uint64_t* counts, uint32_t nm, uint64_t* out,
+                             hipStream_t stream) {
+    if (!nm) return hipSuccess;
+    hipLaunchKernelGGL(k_first_rank, dim3((nm + 63) / 64), dim3(64), 0, stream, live_gt, live_row, rows, starts, counts,
+                       nm, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_rows_seg(IngestRow* rows, uint64_t k, uint64_t sa, uint64_t sb, hipStream_t stream) {
+    if (!k) return hipSuccess;
+    hipLaunchKernelGGL(k_rows_seg, dim3((uint32_t)((k + kIngestThreads - 1) / kIngestThreads)), dim3(kIngestThreads), 0,
+                       stream, rows, k, sa, sb);
+    return hipGetLastError();
+}
+
 hipError_t launch_ingest_merge(const uint64_t* live_gt, const uint64_t* live_row, uint64_t n_live,
                                const IngestRow* rows, uint64_t a, uint64_t* rank, uint64_t* out_gt, uint64_t* out_row,
                                unsigned int* present, uint32_t max_grid, hipStream_t stream) {
@@ -208,7 +358,7 @@ __global__ void __launch_bounds__(256) k_mark_rows(const uint64_t* __restrict__ 
 __device__ __forceinline__ bool entry_kept(const uint64_t* __restrict__ live_row, const uint32_t* __restrict__ bits,
                                            uint64_t i) {
     const uint64_t r = live_row ? live_row[i] : i;
-    return !((bits[r >> 5] >> (r & 31)) & 1u);
+    return r != kGapRow && !((bits[r >> 5] >> (r & 31)) & 1u);  // slack entries go too
 }
 
 // kept entries per tile of kDelTile (256 lanes x 4)

@@ -179,9 +179,16 @@ uint64_t dsy_store_rows(const dsy_store* store);
  * argument order (so they keep the rowid order of the inserts) and enter the responder's index by
  * (meta_message, global_time, rowid): a new row follows every stored row with the same meta and global time.
  * The device buffers grow by >= 1.25x when full (copied once); an attached store's caller buffers are left as they
- * were and are no longer read.  The index merge is O(n + a) HBM traffic on the device. */
+ * were and are no longer read.  The call is O(a): the rows' index entries are queued on the device and join the index
+ * when something next reads it (one merge for every append since): each meta's tail from its first new entry on is
+ * merged in place into the slack its index region keeps, or -- when a meta's slack is spent -- the whole index is
+ * merged once and laid out with fresh slack (a quarter of each region, at least 16384 entries). */
 int dsy_store_append(dsy_ctx* ctx, dsy_store* store, const uint8_t* blob, uint64_t blob_len, const uint64_t* offsets,
                      uint64_t a, const uint64_t* global_time, const uint32_t* meta, const uint64_t* member);
+/* The responder index's bookkeeping: out[0] live entries, out[1] entries of the index arrays (live + slack),
+ * out[2] in-place tail merges, out[3] whole-index merges, out[4] index bytes moved by them (reads + writes),
+ * out[5] queued entries not merged yet. */
+int dsy_store_index_stats(const dsy_store* store, uint64_t* out6);
 
 /* GlobalTimePruning's DELETE FROM sync WHERE meta_message = ? AND global_time <= ? (community.py:1092-1096, run by
  * update_global_time): the meta's rows up to max_global_time leave the responder's index and, when the store has a

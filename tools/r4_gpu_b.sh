@@ -4,7 +4,7 @@
 # has its own limit; the first failure ends the call.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_respond_refs_gpu.py \
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_ingest_slack.py tests/test_respond_refs_gpu.py \
     tests/test_ingest.py tests/test_sequence.py tests/test_undo.py tests/test_delete.py tests/test_claim_largest.py \
     tests/test_claim_modulo.py tests/test_dedup.py tests/test_pipeline_gpu.py tests/test_sync_golden.py \
     tests/test_bitmod.py tests/test_bloom_gpu.py tests/test_respond_order_gpu.py \
