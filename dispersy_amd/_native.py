@@ -88,6 +88,7 @@ SIGNATURES = {
     "dsy_store_free": (ctypes.c_int, [_P]),
     "dsy_store_rows": (_U64, [_P]),
     "dsy_store_append": (ctypes.c_int, [_P, _P, _P, _U64, _P, _U64, _P, _P, _P]),
+    "dsy_store_append_gather": (ctypes.c_int, [_P, _P, _P, _P, _U64, _P, _P, _P]),
     "dsy_store_index_stats": (ctypes.c_int, [_P, _P]),
     "dsy_store_index_members": (ctypes.c_int, [_P, _P, _P, _P, _U64]),
     "dsy_store_prune": (ctypes.c_int, [_P, _P, _U32, _U64, _PU64]),

@@ -39,7 +39,7 @@ _RECORD_OF = operator.attrgetter("request_record")
 _RAW_OF = operator.attrgetter("_raw")
 _REFS_OF = operator.attrgetter("_refs")  # a BloomFilter's (record, filter bytes) addresses, 16 B
 _DIST_OF = operator.attrgetter("distribution")
-_GT_OF = operator.attrgetter("global_time")
+_MSG_GT_OF = operator.attrgetter("distribution.global_time")
 _PACKET_OF = operator.attrgetter("packet")
 
 # the sync part of an introduction-request payload (payload.py:31-153): time_high == 0 means "up to the
@@ -475,15 +475,19 @@ class SyncCommunity(object):
         per_meta = {}
         for meta in dict(zip(map(id, meta_objs), meta_objs)).values():
             per_meta[id(meta)] = self._meta_store_info(meta)
-        dists = list(map(_DIST_OF, messages))
-        gts = np.fromiter(map(_GT_OF, dists), dtype=np.uint64, count=n)
+        gts = np.fromiter(map(_MSG_GT_OF, messages), dtype=np.uint64, count=n)
         packets = list(map(_PACKET_OF, messages))
-        metas = list(map(getattr, messages, itertools.repeat("database_id", n), itertools.repeat(None, n)))
-        if None in metas:  # messages that carry their meta's id on .meta only
-            metas = [d if d is not None else meta.database_id for d, meta in zip(metas, meta_objs)]
+        try:
+            metas = np.fromiter(map(getattr, messages, itertools.repeat("database_id", n), itertools.repeat(None, n)),
+                                dtype=np.uint32, count=n)
+        except TypeError:  # messages that carry their meta's id on .meta only
+            metas = [getattr(m, "database_id", None) for m in messages]
+            metas = np.array([d if d is not None else meta.database_id for d, meta in zip(metas, meta_objs)],
+                             dtype=np.uint32)
         seqs = None
         if any(info[0] for info in per_meta.values()):
-            seqs = [d.sequence_number if per_meta[id(meta)][0] else 0 for d, meta in zip(dists, meta_objs)]
+            seqs = [d.sequence_number if per_meta[id(meta)][0] else 0
+                    for d, meta in zip(map(_DIST_OF, messages), meta_objs)]
         members = list(map(_member_id, messages)) if has_member else None
         double = ([i for i, meta in enumerate(meta_objs) if per_meta[id(meta)][2]]
                   if any(info[2] for info in per_meta.values()) else [])

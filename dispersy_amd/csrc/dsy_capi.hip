@@ -1275,14 +1275,12 @@ again:
     return DSY_OK;
 }
 
-int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blob_len, const uint64_t* offsets,
-                     uint64_t a, const uint64_t* gt, const uint32_t* meta, const uint64_t* member) {
-    if (!c || !s || !offsets || (a && (!gt || !meta || (blob_len && !blob)))) return fail(DSY_EINVAL, "NULL argument");
-    if (s->ctx != c) return fail(DSY_EINVAL, "store belongs to another context");
-    if (s->dup && a && !member) return fail(DSY_EINVAL, "the store has a (member, global_time) table: members required");
-    int rc = check_offsets(offsets, a, blob_len);
-    if (rc) return rc;
-    if (a == 0) return DSY_OK;
+// dsy_store_append and dsy_store_append_gather: the packets are blob[offsets[j], offsets[j+1]) (blob form, addrs NULL)
+// or addrs[j] with offsets[] their running lengths from 0 (gather form: copied into the pinned staging here, one
+// upload with the columns).  The caller has checked the arguments.
+static int store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, const uint64_t* offsets, const uint64_t* addrs,
+                        uint64_t a, const uint64_t* gt, const uint32_t* meta, const uint64_t* member) {
+    int rc;
     Guard g(c);
     if (c->inflight()) return fail(DSY_EINVAL, "the store cannot change while submitted responder batches are in flight");
     const uint64_t n0 = s->n, base0 = offsets[0], add = offsets[a] - base0;
@@ -1294,11 +1292,12 @@ int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blo
     // members]
     const size_t b_off = (a + 1) * 8, b_rec = a * sizeof(RowRec), b_gt = a * 8, b_meta = (a * 4 + 15) / 16 * 16,
                  b_mem = member ? a * 8 : 0, b_cols = b_off + b_rec + b_gt + b_meta + b_mem;
-    if (c->in_stage_bytes < b_cols) {
+    const size_t b_blob = (add + 15) / 16 * 16, b_stage = b_cols + (addrs ? b_blob : 0);
+    if (c->in_stage_bytes < b_stage) {
         if (c->in_stage) hipHostFree(c->in_stage);
         c->in_stage = nullptr;
         c->in_stage_bytes = 0;
-        const size_t want = std::max<size_t>(b_cols + b_cols / 4, 4096);
+        const size_t want = std::max<size_t>(b_stage + b_stage / 4, 4096);
         if (hipHostMalloc((void**)&c->in_stage, want, hipHostMallocDefault) != hipSuccess) {
             c->in_stage = nullptr;
             return fail(DSY_ENOMEM, "hipHostMalloc(%zu) for the ingest staging failed", want);
@@ -1318,6 +1317,9 @@ int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blo
     std::memcpy(c->in_stage + b_off + b_rec, gt, a * 8);
     std::memcpy(c->in_stage + b_off + b_rec + b_gt, meta, a * 4);
     if (member) std::memcpy(c->in_stage + b_off + b_rec + b_gt + b_meta, member, a * 8);
+    if (addrs)  // the packets, gathered from the caller's objects
+        for (uint64_t j = 0; j < a; ++j)
+            std::memcpy(c->in_stage + b_cols + offsets[j], (const void*)(uintptr_t)addrs[j], offsets[j + 1] - offsets[j]);
     if ((rc = lines_reserve(c, s, at))) return rc;
     if (n0 + a > s->rec_cap) {
         const uint64_t cap = grown(n0 + a, s->rec_cap);
@@ -1353,7 +1355,6 @@ int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blo
 
     // uploads (one workspace): the packets from the caller's buffer, the staged columns in one copy; the packets then
     // move to their line-aligned places
-    const size_t b_blob = (add + 15) / 16 * 16;
     void* d_up;
     if ((rc = ws_get(c, "ingest", b_blob + b_cols, &d_up))) return rc;
     uint8_t* up = (uint8_t*)d_up;
@@ -1362,7 +1363,7 @@ int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blo
     uint8_t* up_gt = up_rec + b_rec;
     uint8_t* up_meta = up_gt + b_gt;
     uint8_t* up_mem = up_meta + b_meta;
-    if (add) HIP_TRY(hipMemcpyAsync(up, blob + base0, add, hipMemcpyHostToDevice, c->stream));
+    if (add) HIP_TRY(hipMemcpyAsync(up, addrs ? c->in_stage + b_cols : blob + base0, add, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(up_off, c->in_stage, b_cols, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(const_cast<RowRec*>(s->d_rec) + n0, up_rec, b_rec, hipMemcpyDeviceToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(s->d_pend_gt + s->pend_n, up_gt, b_gt, hipMemcpyDeviceToDevice, c->stream));
@@ -1391,6 +1392,33 @@ int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blo
     s->blob_len += add;
     s->lines_used = at;
     return DSY_OK;
+}
+
+int dsy_store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, uint64_t blob_len, const uint64_t* offsets,
+                     uint64_t a, const uint64_t* gt, const uint32_t* meta, const uint64_t* member) {
+    if (!c || !s || !offsets || (a && (!gt || !meta || (blob_len && !blob)))) return fail(DSY_EINVAL, "NULL argument");
+    if (s->ctx != c) return fail(DSY_EINVAL, "store belongs to another context");
+    if (s->dup && a && !member) return fail(DSY_EINVAL, "the store has a (member, global_time) table: members required");
+    int rc = check_offsets(offsets, a, blob_len);
+    if (rc) return rc;
+    if (a == 0) return DSY_OK;
+    return store_append(c, s, blob, offsets, nullptr, a, gt, meta, member);
+}
+
+int dsy_store_append_gather(dsy_ctx* c, dsy_store* s, const uint64_t* addrs, const uint64_t* lengths, uint64_t a,
+                            const uint64_t* gt, const uint32_t* meta, const uint64_t* member) {
+    if (!c || !s || (a && (!addrs || !lengths || !gt || !meta))) return fail(DSY_EINVAL, "NULL argument");
+    if (s->ctx != c) return fail(DSY_EINVAL, "store belongs to another context");
+    if (s->dup && a && !member) return fail(DSY_EINVAL, "the store has a (member, global_time) table: members required");
+    if (a == 0) return DSY_OK;
+    std::vector<uint64_t> off(a + 1);
+    off[0] = 0;
+    for (uint64_t j = 0; j < a; ++j) {
+        if (lengths[j] && !addrs[j]) return fail(DSY_EINVAL, "packet %llu: NULL address", (unsigned long long)j);
+        if (lengths[j] > 0xFFFFFFFFull) return fail(DSY_EINVAL, "packet %llu longer than 4 GiB", (unsigned long long)j);
+        off[j + 1] = off[j] + lengths[j];
+    }
+    return store_append(c, s, nullptr, off.data(), addrs, a, gt, meta, member);
 }
 
 

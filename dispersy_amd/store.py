@@ -42,6 +42,23 @@ def _room(buf, used, need):
     return out
 
 
+def _bytes_data_offset():
+    """Offset of a CPython bytes object's data from its id() (the object header; 32 on 64-bit CPython 3), checked on
+    live objects -- or None, and the appends join their packets instead."""
+    off = bytes.__basicsize__ - 1
+    try:
+        for probe in (b"\x01\x02probe", bytes(range(256)) * 3, b"x"):
+            if ctypes.string_at(id(probe) + off, len(probe)) != probe:
+                return None
+    except Exception:  # noqa: BLE001 -- any failure: take the join path
+        return None
+    return off
+
+
+_BYTES_DATA = _bytes_data_offset()
+_ONLY_BYTES = {bytes}
+
+
 class SyncStore(object):
     def __init__(self, blob, offsets, global_time, meta, undone=None, rowid=None, ctx=None, member=None,
                  communities=None, sequence=None):
@@ -90,9 +107,10 @@ class SyncStore(object):
         self._keys = None    # (member, global_time) -> row, built on first use (rows_of_keys)
         self._gpending = {}
         self._blob_base = 0  # offsets[] of the host blob's first byte (attach: earlier packets are device-only)
-        # packets appended later, one bytes object per batch (appending to one growing buffer copied it every batch:
-        # 8 MB per 10 k packets); _tail_at[i] = offsets[] of batch i's first byte
-        self._tail, self._tail_at = [], []
+        # packets appended later, per batch: its joined bytes, or the list of the caller's packet objects when they
+        # went to the device as a gather list (appending to one growing buffer copied it every batch: 8 MB per 10 k
+        # packets); _tail_at[i] = offsets[] of batch i's first byte, _tail_row[i] = its first row
+        self._tail, self._tail_at, self._tail_row = [], [], []
         self._pair_groups = {}  # (meta, member1, member2) -> rows: the double_signed_sync table (set_pairs)
         self._owns_handle = True
 
@@ -160,10 +178,14 @@ class SyncStore(object):
             if p is not None:
                 return p
         off = self._buf["offsets"]
+        if self._tail and i >= self._tail_row[0]:
+            k = bisect.bisect_right(self._tail_row, i) - 1
+            t = self._tail[k]
+            if isinstance(t, list):
+                return t[i - self._tail_row[k]]
+            a, b = int(off[i]) - self._tail_at[k], int(off[i + 1]) - self._tail_at[k]
+            return t[a:b]
         a, b = int(off[i]), int(off[i + 1])
-        if self._tail and a >= self._tail_at[0]:
-            k = bisect.bisect_right(self._tail_at, a) - 1
-            return self._tail[k][a - self._tail_at[k]:b - self._tail_at[k]]
         a, b = a - self._blob_base, b - self._blob_base
         if a < 0:
             raise KeyError("row %d's packet lives only on the device (SyncStore.attach)" % int(i))
@@ -172,8 +194,8 @@ class SyncStore(object):
     def _host_blob(self):
         """Every host-held packet byte in one buffer (the initial blob, then the appended batches)."""
         if self._tail:
-            self.blob = bytes(self.blob) + b"".join(self._tail)
-            self._tail, self._tail_at = [], []
+            self.blob = bytes(self.blob) + b"".join(t if not isinstance(t, list) else b"".join(t) for t in self._tail)
+            self._tail, self._tail_at, self._tail_row = [], [], []
         return self.blob
 
     def packets(self, rows):
@@ -298,12 +320,20 @@ class SyncStore(object):
         lens = np.fromiter(map(len, packets), dtype=np.uint64, count=a)
         new_off = np.zeros(a + 1, dtype=np.uint64)
         np.cumsum(lens, out=new_off[1:])
-        data = b"".join(packets)  # bytes-like items join as they are
-        if self._handle is not None:
-            lib = self.ctx.lib
-            _native.check(lib.dsy_store_append(self.ctx.handle, self._handle, data, len(data), new_off.ctypes.data, a,
-                                               gts.ctypes.data, metas.ctypes.data,
-                                               mem.ctypes.data if mem is not None else None))
+        if self._handle is not None and _BYTES_DATA is not None and set(map(type, packets)) == _ONLY_BYTES:
+            # the packet objects' own bytes as a gather list (no joined copy: it cost more than the device call)
+            packets = list(packets)
+            addrs = np.fromiter(map(id, packets), dtype=np.uint64, count=a) + np.uint64(_BYTES_DATA)
+            _native.check(self.ctx.lib.dsy_store_append_gather(
+                self.ctx.handle, self._handle, addrs.ctypes.data, lens.ctypes.data, a, gts.ctypes.data,
+                metas.ctypes.data, mem.ctypes.data if mem is not None else None))
+            data = packets
+        else:
+            data = b"".join(packets)  # bytes-like items join as they are
+            if self._handle is not None:
+                _native.check(self.ctx.lib.dsy_store_append(self.ctx.handle, self._handle, data, len(data),
+                                                            new_off.ctypes.data, a, gts.ctypes.data, metas.ctypes.data,
+                                                            mem.ctypes.data if mem is not None else None))
         # host columns: geometric growth, O(batch) per append
         b = self._buf
         b["offsets"] = _room(b["offsets"], n0 + 1, n0 + a + 1)
@@ -324,6 +354,7 @@ class SyncStore(object):
             b["member"] = _room(b["member"], n0, n0 + a)
             b["member"][n0:n0 + a] = mem
         self._tail_at.append(int(b["offsets"][n0]))
+        self._tail_row.append(n0)
         self._tail.append(data)
         self.n = n0 + a
         self._top = int(ids[-1])

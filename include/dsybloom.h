@@ -185,6 +185,11 @@ uint64_t dsy_store_rows(const dsy_store* store);
  * merged once and laid out with fresh slack (a quarter of each region, at least 16384 entries). */
 int dsy_store_append(dsy_ctx* ctx, dsy_store* store, const uint8_t* blob, uint64_t blob_len, const uint64_t* offsets,
                      uint64_t a, const uint64_t* global_time, const uint32_t* meta, const uint64_t* member);
+/* The same with the packets given as a gather list: packet j is lengths[j] bytes at host address addrs[j] (the
+ * caller's own packet objects -- no joined copy); they are copied into the library's pinned staging and uploaded
+ * with the columns in one transfer. */
+int dsy_store_append_gather(dsy_ctx* ctx, dsy_store* store, const uint64_t* addrs, const uint64_t* lengths, uint64_t a,
+                            const uint64_t* global_time, const uint32_t* meta, const uint64_t* member);
 /* The responder index's bookkeeping: out[0] live entries, out[1] entries of the index arrays (live + slack),
  * out[2] in-place tail merges, out[3] whole-index merges, out[4] index bytes moved by them (reads + writes),
  * out[5] queued entries not merged yet. */
