@@ -104,6 +104,8 @@ struct RespondJob {
 // 6, the hashing launch 280-355 us instead of 210).
 // dsy_sync_respond_refs: the claims' filters, copied into pinned staging and uploaded after the first window's
 // selection is enqueued (job_window), so the host gathers them while the GPU selects
+static constexpr size_t kOutPinMax = 64ull << 20;  // results of a host-buffer responder call kept in pinned memory
+
 struct FilterGather {
     const uint64_t* refs = nullptr;  // claim r's filter bytes at refs[2r + 1]
     const uint64_t* foff = nullptr;  // and their place in the filters workspace
@@ -160,6 +162,12 @@ struct dsy_ctx {
     uint64_t window_cap = 0; // dsy_ctx_set_window: upper bound on the responder's window (0: the default 2^18)
     hipStream_t aux = nullptr;  // dsy_sim_claim_matrix: work that depends on nothing queued on `stream`
     hipEvent_t xev = nullptr;   // dsy_ctx_wait_stream / dsy_ctx_signal_stream
+    hipEvent_t gev = nullptr;   // dsy_sync_respond_refs: the filters' upload on `aux` is done
+    // host-buffer responder calls: the pack kernel writes the results (offsets, then rows) straight into this pinned,
+    // device-visible buffer, so no download follows the step (respond_to_host; grow-only, up to kOutPinMax bytes)
+    bool host_out = false;
+    uint8_t* out_pin = nullptr;
+    size_t out_pin_bytes = 0;
     // pinned staging of dsy_store_append's small columns (offsets, records, global times, metas, members): one
     // upload per append; the next append synchronises the stream before it writes here again
     uint8_t* in_stage = nullptr;
@@ -551,6 +559,8 @@ int dsy_ctx_destroy(dsy_ctx* c) {
         for (auto e : c->event_pool) hipEventDestroy(e);
         if (c->xev) hipEventDestroy(c->xev);
         if (c->aux) hipStreamDestroy(c->aux);
+        if (c->gev) hipEventDestroy(c->gev);
+        if (c->out_pin) hipHostFree(c->out_pin);
         if (c->pinned) hipHostFree(c->pinned);
         if (c->in_stage) hipHostFree(c->in_stage);
         hipStreamDestroy(c->stream);
@@ -2001,17 +2011,30 @@ static int job_window(dsy_ctx* c, RespondSlot& sl) {
     jb.first_fill = false;
     timer_end(c, &t, st);
     if (sl.gather.refs) {  // the claims' filters, gathered and uploaded while the selection runs
+        // in chunks on the aux stream: chunk i's transfer overlaps chunk i+1's host copy and the selection kernel;
+        // the ctx stream waits for the last one before the hashing
         FilterGather& fg = sl.gather;
         uint8_t* h;
         if ((rc = stage_get(c->main, fg.total + 64, &h))) return rc;
-        for (uint32_t r = 0; r < fg.R; ++r) {
-            const uint64_t n = ((const dsy_request*)(uintptr_t)fg.refs[2 * (size_t)r])->m_bits / 8;
-            uint8_t* dst = h + fg.foff[r];
-            memcpy(dst, (const void*)(uintptr_t)fg.refs[2 * (size_t)r + 1], n);
-            memset(dst + n, 0, ((n + 3) & ~uint64_t(3)) - n);
+        if (!c->aux) HIP_TRY(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+        if (!c->gev) HIP_TRY(hipEventCreateWithFlags(&c->gev, hipEventDisableTiming));
+        const uint32_t chunks = fg.R >= 256 ? 4 : 1;
+        uint64_t sent = 0;
+        for (uint32_t k = 0; k < chunks; ++k) {
+            const uint32_t r0 = (uint32_t)((uint64_t)fg.R * k / chunks), r1 = (uint32_t)((uint64_t)fg.R * (k + 1) / chunks);
+            for (uint32_t r = r0; r < r1; ++r) {
+                const uint64_t n = ((const dsy_request*)(uintptr_t)fg.refs[2 * (size_t)r])->m_bits / 8;
+                uint8_t* dst = h + fg.foff[r];
+                memcpy(dst, (const void*)(uintptr_t)fg.refs[2 * (size_t)r + 1], n);
+                memset(dst + n, 0, ((n + 3) & ~uint64_t(3)) - n);
+            }
+            const uint64_t upto = k + 1 == chunks ? fg.total + 64 : fg.foff[r1];
+            if (k + 1 == chunks) memset(h + fg.total, 0, 64);
+            if (upto > sent) HIP_TRY(hipMemcpyAsync(fg.d_dst + sent, h + sent, upto - sent, hipMemcpyHostToDevice, c->aux));
+            sent = upto;
         }
-        memset(h + fg.total, 0, 64);
-        HIP_TRY(hipMemcpyAsync(fg.d_dst, h, fg.total + 64, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipEventRecord(c->gev, c->aux));
+        HIP_TRY(hipStreamWaitEvent(st, c->gev, 0));
         fg = FilterGather{};
     }
     if (fill_profile) {  // per-window stderr line: k_fill phase durations over the workgroups (s_memtime ticks)
@@ -2364,9 +2387,26 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const Clai
             HIP_TRY(hipStreamSynchronize(st));  // rst is pageable and goes out of scope
         }
     }
-    if ((rc = ws_get(w, "packed", std::max<uint64_t>(cap_total, 1) * 8, &jb.d_packed))) return rc;
     L.packed_cap = cap_total;
-    if ((rc = ws_get(w, "packed_off", ((size_t)R + 1) * 8, &jb.d_packed_off))) return rc;
+    const size_t b_pin = ((size_t)R + 1) * 8 + std::max<uint64_t>(cap_total, 1) * 8;
+    if (c->host_out && b_pin <= kOutPinMax) {  // results straight into pinned host memory
+        if (c->out_pin_bytes < b_pin) {
+            if (c->out_pin) hipHostFree(c->out_pin);
+            c->out_pin = nullptr;
+            c->out_pin_bytes = 0;
+            const size_t want = std::max<size_t>(b_pin + b_pin / 4, 1 << 16);
+            if (hipHostMalloc((void**)&c->out_pin, want, hipHostMallocDefault) != hipSuccess) {
+                c->out_pin = nullptr;
+                return fail(DSY_ENOMEM, "hipHostMalloc(%zu) for the responder's results failed", want);
+            }
+            c->out_pin_bytes = want;
+        }
+        jb.d_packed_off = c->out_pin;
+        jb.d_packed = c->out_pin + ((size_t)R + 1) * 8;
+    } else {
+        if ((rc = ws_get(w, "packed", std::max<uint64_t>(cap_total, 1) * 8, &jb.d_packed))) return rc;
+        if ((rc = ws_get(w, "packed_off", ((size_t)R + 1) * 8, &jb.d_packed_off))) return rc;
+    }
     size_t n_act = 0;
     for (auto& fa : jb.fam_active) n_act += fa.size();
     if (n_act) return job_window(c, sl);
@@ -2490,9 +2530,19 @@ static int respond_to_host(dsy_ctx* c, const dsy_store* s, const Claims& cl, uin
                            uint64_t out_cap, uint64_t* out_req_offsets) {
     int rc;
     uint64_t *d_packed, *d_off, pairs;
-    if ((rc = respond_core(c, s, cl, R, (const uint8_t*)d_f, filters_len + 64, metas, nmeta, responder_global_time,
-                           include_inactive, byte_limit, random_seed, &d_packed, &d_off, &pairs)))
-        return rc;
+    c->host_out = true;
+    rc = respond_core(c, s, cl, R, (const uint8_t*)d_f, filters_len + 64, metas, nmeta, responder_global_time,
+                      include_inactive, byte_limit, random_seed, &d_packed, &d_off, &pairs);
+    c->host_out = false;
+    if (rc) return rc;
+    if ((uint8_t*)d_off == c->out_pin) {  // written by the pack kernel into pinned memory; the step has completed
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        std::memcpy(out_req_offsets, d_off, ((size_t)R + 1) * 8);
+        const uint64_t total = out_req_offsets[R];
+        if (total > out_cap) return fail(DSY_ECAPACITY, "out_cap %llu < %llu rows", (unsigned long long)out_cap, (unsigned long long)total);
+        std::memcpy(out_idx, d_packed, total * 8);
+        return DSY_OK;
+    }
     HIP_TRY(hipMemcpyAsync(out_req_offsets, d_off, ((size_t)R + 1) * 8, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     const uint64_t total = out_req_offsets[R];
