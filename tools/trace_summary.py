@@ -66,6 +66,10 @@ def summary(w, r):
                 cur_b = max(cur_b, b)
         busy += cur_b - cur_a
     print("  SIMD occupied fraction of the span: %.3f" % (busy / float(len(simds) * (s1 - s0))))
+    # the critical path: the longest wave-tasks (their serial digests) against the span
+    top = np.argsort(dur)[::-1][:5]
+    print("  longest tasks (us / blocks / start us): %s" % "; ".join(
+        "%.1f / %d / %.1f" % (dur[i], r["blocks"][i], (t0[i] - s0) * 10e-3) for i in top))
 
 
 def main():
