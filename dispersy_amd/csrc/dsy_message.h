@@ -232,6 +232,11 @@ struct DmaLanes {
     }
 };
 
+// A wave's LDS buffer (a generic pointer into __shared__ memory) as a local address the wave holds in an SGPR.
+__device__ __forceinline__ uint32_t lds_local(uint8_t* p) {
+    return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)p);
+}
+
 // The store's line copy puts every packet kLineBias bytes into a 128-byte line.  With one byte of slack in front of
 // every packet, the message prefix || packet of a 1-byte prefix (every claim the reference builds, community.py:773,
 // :911) starts exactly on the line, and the responder's blocks need no byte shift.
@@ -260,8 +265,9 @@ struct DmaLinePieces {
     }
     // a 16-byte piece is loaded only when it holds packet bytes: the last line of a packet moves only the chunks
     // its bytes reach (the rest of that line is padding)
+    // lds: the wave's LDS buffer as a wave-uniform local address (lds_local), so each instruction's M0 is a scalar add
     template <bool SKIP = false>
-    __device__ __forceinline__ void issue(uint32_t s, const uint8_t* base, uint8_t* lds_wave) const {
+    __device__ __forceinline__ void issue(uint32_t s, const uint8_t* base, uint32_t lds) const {
         if constexpr (SKIP) return;
         const uint32_t lane = threadIdx.x & 63;
 #pragma unroll
@@ -271,7 +277,8 @@ struct DmaLinePieces {
             const uint32_t c = ((lane % G::kChunks) + ((uint32_t)p >> G::kShift)) % G::kChunks;
             if (s * 128 + 16 * c < lv)
                 __builtin_amdgcn_global_load_lds((const void*)(base + ((uint64_t)(line[i] + s) << 7) + 16 * c),
-                                                 (__attribute__((address_space(3))) void*)(lds_wave + i * 1024), 16, 0, 0);
+                                                 (__attribute__((address_space(3))) void*)(uintptr_t)(lds + i * 1024),
+                                                 16, 0, 0);
         }
     }
 };
@@ -487,7 +494,8 @@ __device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uin
     uint32_t carry = rr ? (preword & low_bytes_mask(rr)) << (8 * (4 - rr)) : 0u;
     const uint32_t slack = (preword >> (8 * rr)) & 0xffu;
     const uint32_t sh = (4 - rr) & 3;  // alignbyte shift for rr in 1..3
-    if (nst) dl.template issue<MODE == 1>(0, lines, lds_wave);
+    const uint32_t lds = lds_local(lds_wave);
+    if (nst) dl.template issue<MODE == 1>(0, lines, lds);
     for (uint32_t s = 0; s < nst; ++s) {
         __builtin_amdgcn_s_waitcnt(0x0f70);
         __builtin_amdgcn_wave_barrier();
@@ -503,7 +511,7 @@ __device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uin
         if (s == 0) d[1] = (d[1] & ~0xffu) | slack;
         __builtin_amdgcn_s_waitcnt(0xc07f);
         __builtin_amdgcn_wave_barrier();
-        if (s + 1 < nst) dl.template issue<MODE == 1>(s + 1, lines, lds_wave);
+        if (s + 1 < nst) dl.template issue<MODE == 1>(s + 1, lines, lds);
         carry = d[32];
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb) {
