@@ -4,7 +4,7 @@ shader clock it ran at (GRBM_GUI_ACTIVE summed over the 8 XCDs, over the dispatc
 dispatch, the VALU instructions per dispatch and the INT32 fraction against the spec peak and against the same
 peak at the measured clock.
 
-usage: clock_summary.py OUT_DIR [--ops md5=500,sha1=961] > profiles/<name>.json"""
+usage: clock_summary.py OUT_DIR [--match KERNEL_SUBSTRING] > profiles/<name>.json   (default k_bloom)"""
 import collections
 import csv
 import glob
@@ -17,6 +17,7 @@ XCDS = 8
 
 def main():
     root = sys.argv[1]
+    match = sys.argv[sys.argv.index("--match") + 1] if "--match" in sys.argv else "k_bloom"
     out = {}
     for trace in sorted(glob.glob(os.path.join(root, "trace_*"))):
         if not os.path.isdir(trace):
@@ -28,13 +29,13 @@ def main():
             continue
         durs = {}
         for r in csv.DictReader(open(stats[0])):
-            if "k_bloom" in r["Name"]:
+            if match in r["Name"]:
                 durs[r["Name"].split("(")[0].replace("void ", "")] = (int(r["Calls"]), float(r["AverageNs"]))
         acc = collections.defaultdict(lambda: collections.defaultdict(float))
         disp = collections.defaultdict(set)
         for r in csv.DictReader(open(pmc[0])):
             name = r.get("Kernel_Name", "").split("(")[0].replace("void ", "")
-            if "k_bloom" not in name:
+            if match not in name:
                 continue
             acc[name][r["Counter_Name"]] += float(r["Counter_Value"])
             disp[name].add(r.get("Dispatch_Id", r.get("Correlation_Id", "")))
