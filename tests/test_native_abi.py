@@ -67,3 +67,17 @@ def test_status_codes_match_header():
     defs = dict(re.findall(r"^#define\s+(DSY_E\w+|DSY_OK)\s+(-?\d+)\b", open(HEADER).read(), flags=re.M))
     for name, val in defs.items():
         assert getattr(_native, name) == int(val), name
+
+
+def test_bytes_gather_addresses_point_at_the_data():
+    """SyncStore.append hands bytes packets to dsy_store_append_gather by address (id + the object header): the
+    offset found at import reads back every packet's bytes, empty and large ones included (CPU)."""
+    import ctypes
+    import numpy as np
+    from dispersy_amd.store import _BYTES_DATA
+    assert _BYTES_DATA == bytes.__basicsize__ - 1
+    rng = np.random.Generator(np.random.PCG64(3))
+    packets = [b"", b"x"] + [rng.bytes(int(n)) for n in rng.integers(1, 70_000, 50)]
+    addrs = np.fromiter(map(id, packets), dtype=np.uint64, count=len(packets)) + np.uint64(_BYTES_DATA)
+    for p, a in zip(packets, addrs.tolist()):
+        assert ctypes.string_at(a, len(p)) == p
