@@ -937,12 +937,15 @@ def ingest_bench(args, ctx, lib, store, step, N, batch=10_000, batches=10, cpu_l
 
     top = [N]  # the highest global time stored so far
 
-    def make(recent):
+    def make(kind):
         lens = rng.integers(100, 1501, size=batch)
         off = np.zeros(batch + 1, dtype=np.uint64)
         np.cumsum(lens, out=off[1:])
         data = rng.bytes(int(off[-1]))
-        if recent:  # new messages: global times around the community's current one (the last 10 k and above)
+        if kind == "new":  # messages created after everything stored (the Lamport global time only grows)
+            gts = rng.integers(top[0] + 1, top[0] + 1 + batch, size=batch).astype(np.uint64)
+            top[0] += batch
+        elif kind == "recent":  # received messages of the last 10 k global times and above
             gts = rng.integers(top[0] - 10_000, top[0] + batch, size=batch).astype(np.uint64)
             top[0] += batch
         else:  # old messages (a peer catching up): anywhere in the history
@@ -974,8 +977,8 @@ def ingest_bench(args, ctx, lib, store, step, N, batch=10_000, batches=10, cpu_l
     first_ms = None
     work_legs = {}
     after_pairs = 0
-    for kind, recent in (("history", False), ("recent", True)):
-        work = [make(recent) for _ in range(batches + (1 if first_ms is None else 0))]
+    for kind in ("history", "recent", "new"):
+        work = [make(kind) for _ in range(batches + (1 if first_ms is None else 0))]
         if first_ms is None:  # the first append moves the attached store into buffers of its own
             t0 = time.perf_counter()
             append(work.pop(0))
@@ -992,8 +995,9 @@ def ingest_bench(args, ctx, lib, store, step, N, batch=10_000, batches=10, cpu_l
         s1 = ix_stats()
         base_ms, after_pairs = timed_step()  # a step with nothing to merge
         work_legs[kind] = {
-            "global_times": ("anywhere in the store's history [1, %d]" % N if not recent else
-                             "the newest 10 k and above (new messages)"),
+            "global_times": {"history": "anywhere in the store's history [1, %d]" % N,
+                             "recent": "the newest 10 k and above (received recent messages)",
+                             "new": "above every stored one (messages created since)"}[kind],
             "median_ms_per_append": round(sorted(t_app)[len(t_app) // 2] * 1e3, 3),
             "median_responder_step_after_an_append_ms": round(sorted(t_read)[len(t_read) // 2], 3),
             "responder_step_without_merge_ms": round(base_ms, 3),
@@ -1054,7 +1058,7 @@ def ingest_bench(args, ctx, lib, store, step, N, batch=10_000, batches=10, cpu_l
                                  "device; the next read of the index orders them (radix sort) and merges each meta's "
                                  "tail from its first new entry in place into the slack of its region, or merges the "
                                  "whole index once (32 B per entry) when the tails would move more",
-            "index_bytes_per_append": work_legs["recent"]["index_bytes_per_append"],
+            "index_bytes_per_append": work_legs["new"]["index_bytes_per_append"],
             "workloads": work_legs,
             "roofline": {"kernel": "the whole append call: packet upload (PCIe), line copy, row records",
                          "bound": "hbm", "unit": "GB/s", "peak": PEAK_HBM_GBS,

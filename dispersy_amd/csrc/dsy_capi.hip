@@ -1249,7 +1249,7 @@ again:
             tail_max = std::max(tail_max, segs[2 * r + 1] - first[r]);
             tail_sum += segs[2 * r + 1] - first[r];
         }
-    if (!tried_fast && 48 * tail_sum > 32 * s->n_phys) {  // 48 B per tail entry (copied out, read, written) vs 32
+    if (!tried_fast && 64 * tail_sum > 32 * s->n_phys) {  // 64 B per tail entry (copied out and back) vs 32
         tried_fast = true;
         fast = false;
         goto again;
@@ -1279,7 +1279,7 @@ again:
     HIP_TRY(hipStreamSynchronize(c->stream));
     s->n_live += P;
     s->ix_fast += 1;
-    s->ix_bytes += 16 * P + 48 * moved;  // the new entries written, each moved tail entry copied out and back
+    s->ix_bytes += 16 * P + 64 * moved;  // the new entries written; each tail entry copied out and merged back
     s->pend_n = 0;
     s->pend_cnt.clear();
     return DSY_OK;

@@ -103,7 +103,7 @@ def test_slack_merges_match_the_reference():
         st = check("top %d" % k)
     assert st["full"] == s0["full"] + 1 and st["fast"] == s0["fast"] + 2, st
     # 2. older global times (tails merged in place) and two appends before one read; then global times from the whole
-    # history: long tails, merged in place or -- when they would move more than the whole index (48 B per tail entry
+    # history: long tails, merged in place or -- when they would move more than the whole index (64 B per tail entry
     # against 32 B per entry of the index arrays) -- by one whole merge
     append(make(500, [(1, 0.5), (2, 0.5)], top - 700, top))
     append(make(300, [(2, 1.0)], top - 400, top))
