@@ -686,11 +686,17 @@ def dropin_bench(args, ctx, lib, store, offsets, N, claims, reps=5, batch=10_000
         def __init__(self, gt):
             self.global_time, self.priority = gt, 128
 
+    meta = com.get_meta_messages()[0]
+
     class Msg(object):
-        database_id = 1
+        """As the reference's Message.Implementation: .meta, and database_id read through it (message.py:265-266)."""
 
         def __init__(self, gt, packet):
-            self.distribution, self.packet, self.candidate = Dist(gt), packet, None
+            self.meta, self.distribution, self.packet, self.candidate = meta, Dist(gt), packet, None
+
+        @property
+        def database_id(self):
+            return self.meta.database_id
 
     rng = np.random.Generator(np.random.PCG64(314))
     work = []

@@ -29,6 +29,11 @@ from . import _native
 from .bloomfilter import BloomFilter
 from .distribution import FullSyncDistribution, GlobalTimePruning, LastSyncDistribution, SyncDistribution
 
+try:  # store_messages' column reader in C (csrc/dsy_host.c, built beside libdsybloom.so); same results as the Python path
+    from . import _dsyhost
+except ImportError:  # an unbuilt tree
+    _dsyhost = None
+
 MAX_GT = 2 ** 63 - 1  # sqlite's signed 64-bit ceiling (community.py:2545-2548)
 _REQUEST_DTYPE = np.dtype(_native.Request)  # the dsy_request layout, as a numpy record
 _RANGE_DTYPE = np.dtype([("time_low", np.uint64), ("time_high", np.uint64), ("modulo", np.uint64),
@@ -471,19 +476,37 @@ class SyncCommunity(object):
         # is stored, so a refused batch changes neither copy
         n = len(messages)
         has_member = self._store.member is not None
-        meta_objs = list(map(getattr, messages, itertools.repeat("meta", n), itertools.repeat(None, n)))
+        cols = None
+        if _dsyhost is not None and type(messages) is list:
+            # one C pass (dsy_host.c): global times, packets, their gather list, whether one meta object serves all
+            gts, lens, addrs = (np.empty(n, dtype=np.uint64) for _ in range(3))
+            packets, one_meta, first, all_bytes = _dsyhost.message_columns(messages, gts, lens, addrs)
+            meta_objs = [first] * n if one_meta else list(map(getattr, messages, itertools.repeat("meta", n),
+                                                                     itertools.repeat(None, n)))
+            cols = (lens, addrs) if all_bytes else None
+        else:
+            meta_objs = list(map(getattr, messages, itertools.repeat("meta", n), itertools.repeat(None, n)))
+            first = meta_objs[0]
+            # one meta object for the whole batch (the usual case): an identity scan instead of a dict over 10 k ids
+            one_meta = all(map(operator.is_, meta_objs, itertools.repeat(first, n)))
+            gts = np.fromiter(map(_MSG_GT_OF, messages), dtype=np.uint64, count=n)
+            packets = list(map(_PACKET_OF, messages))
+        uniq = [first] if one_meta else dict(zip(map(id, meta_objs), meta_objs)).values()
         per_meta = {}
-        for meta in dict(zip(map(id, meta_objs), meta_objs)).values():
+        for meta in uniq:
             per_meta[id(meta)] = self._meta_store_info(meta)
-        gts = np.fromiter(map(_MSG_GT_OF, messages), dtype=np.uint64, count=n)
-        packets = list(map(_PACKET_OF, messages))
-        try:
-            metas = np.fromiter(map(getattr, messages, itertools.repeat("database_id", n), itertools.repeat(None, n)),
-                                dtype=np.uint32, count=n)
-        except TypeError:  # messages that carry their meta's id on .meta only
-            metas = [getattr(m, "database_id", None) for m in messages]
-            metas = np.array([d if d is not None else meta.database_id for d, meta in zip(metas, meta_objs)],
-                             dtype=np.uint32)
+        meta_id = getattr(first, "database_id", None) if one_meta else None
+        if meta_id is not None:
+            # a message's database_id is its meta's (message.py:265-266): one value for the batch
+            metas = np.full(n, meta_id, dtype=np.uint32)
+        else:
+            try:
+                metas = np.fromiter(map(getattr, messages, itertools.repeat("database_id", n),
+                                        itertools.repeat(None, n)), dtype=np.uint32, count=n)
+            except TypeError:  # messages that carry their meta's id on .meta only
+                metas = [getattr(m, "database_id", None) for m in messages]
+                metas = np.array([d if d is not None else meta.database_id for d, meta in zip(metas, meta_objs)],
+                                 dtype=np.uint32)
         seqs = None
         if any(info[0] for info in per_meta.values()):
             seqs = [d.sequence_number if per_meta[id(meta)][0] else 0
@@ -492,7 +515,7 @@ class SyncCommunity(object):
         double = ([i for i, meta in enumerate(meta_objs) if per_meta[id(meta)][2]]
                   if any(info[2] for info in per_meta.values()) else [])
         pairs = [[int(x.database_id) for x in messages[i].authentication.members] for i in double]
-        rows = self._store.append(packets, gts, metas, member=members, sequence=seqs)
+        rows = self._store.append(packets, gts, metas, member=members, sequence=seqs, _gather=cols)
         if double:  # INSERT INTO double_signed_sync (dispersy.py:1537-1541)
             p = np.asarray(pairs, dtype=np.int64).reshape(-1, 2)
             self._store.set_pairs(rows[double], p[:, 0], p[:, 1])

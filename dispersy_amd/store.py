@@ -293,13 +293,14 @@ class SyncStore(object):
         return np.asarray(sorted(rows, key=lambda r: (int(self.global_time[r]), self.packet(r))), dtype=np.int64)
 
     # ------------------------------------------------------------------------------------------ ingest
-    def append(self, packets, global_time, meta, rowid=None, member=None, sequence=None):
+    def append(self, packets, global_time, meta, rowid=None, member=None, sequence=None, _gather=None):
         """INSERT INTO sync of a batch of received packets (dispersy.py:1475-1612), undone = 0.
 
         packets: list of bytes; global_time / meta (/ member): one per packet; rowid: increasing ids above every
         stored one (default: the next ids, as SQLite assigns them); sequence: the messages' sequence numbers (0 or None:
         NULL).  Returns the new rows' positions.  When the store is on the device already, the batch goes there in one
-        dsy_store_append call.  Host work is O(batch)."""
+        dsy_store_append call.  Host work is O(batch).  _gather: (lengths, addresses) of `packets`, all exactly bytes,
+        as SyncCommunity.store_messages' C column reader returns them (the gather list, not recomputed)."""
         a = len(packets)
         gts = np.ascontiguousarray(global_time, dtype=np.uint64)
         metas = np.ascontiguousarray(meta, dtype=np.uint32)
@@ -317,13 +318,20 @@ class SyncStore(object):
         rows = np.arange(n0, n0 + a, dtype=np.int64)
         if a == 0:
             return rows
-        lens = np.fromiter(map(len, packets), dtype=np.uint64, count=a)
+        if _gather is not None:
+            lens, addrs = _gather
+            if len(lens) != a or len(addrs) != a:
+                raise ValueError("append: one (length, address) per packet")
+        else:
+            lens = np.fromiter(map(len, packets), dtype=np.uint64, count=a)
         new_off = np.zeros(a + 1, dtype=np.uint64)
         np.cumsum(lens, out=new_off[1:])
-        if self._handle is not None and _BYTES_DATA is not None and set(map(type, packets)) == _ONLY_BYTES:
+        if self._handle is not None and (_gather is not None or
+                                         (_BYTES_DATA is not None and set(map(type, packets)) == _ONLY_BYTES)):
             # the packet objects' own bytes as a gather list (no joined copy: it cost more than the device call)
-            packets = list(packets)
-            addrs = np.fromiter(map(id, packets), dtype=np.uint64, count=a) + np.uint64(_BYTES_DATA)
+            if _gather is None:
+                packets = list(packets)
+                addrs = np.fromiter(map(id, packets), dtype=np.uint64, count=a) + np.uint64(_BYTES_DATA)
             _native.check(self.ctx.lib.dsy_store_append_gather(
                 self.ctx.handle, self._handle, addrs.ctypes.data, lens.ctypes.data, a, gts.ctypes.data,
                 metas.ctypes.data, mem.ctypes.data if mem is not None else None))

@@ -271,3 +271,99 @@ def test_double_signed_history_matches_reference():
     (got,) = com.respond([ClaimRequest(1, 10 ** 6, 1, 0, BloomFilter(1024, 0.01, b"\x00"))], include_inactive=True,
                          byte_limit=1 << 40)
     assert sorted(store.rowid[got].tolist()) == sorted(r[0] for r in DOUBLE["steps"][-1]["table"])
+
+
+def test_store_messages_meta_ids_by_batch_shape():
+    """store_messages reads a message's meta id through its meta when the batch has one meta object (message.py:265-266:
+    Message.database_id is its meta's), per message otherwise; each form stores the same columns (CPU, host store)."""
+    from dispersy_amd.community import SyncCommunity
+    from dispersy_amd.distribution import MetaMessage, SyncDistribution
+    from dispersy_amd.store import SyncStore
+
+    class D(object):
+        def __init__(self, gt):
+            self.global_time, self.priority = gt, 128
+
+    class WithMeta(object):  # the reference's shape: database_id is a property of the meta
+        def __init__(self, meta, gt):
+            self.meta, self.packet, self.distribution = meta, b"m%d-%d" % (meta.database_id, gt), D(gt)
+
+        @property
+        def database_id(self):
+            return self.meta.database_id
+
+    class Bare(object):  # no meta: the id on the message itself
+        def __init__(self, mid, gt):
+            self.database_id, self.packet, self.distribution = mid, b"b%d-%d" % (mid, gt), D(gt)
+
+    import dispersy_amd.community as community
+
+    a = MetaMessage("a", 3, SyncDistribution("ASC", 128))
+    b = MetaMessage("b", 5, SyncDistribution("ASC", 128))
+    batches = [[WithMeta(a, 10 + i) for i in range(40)],                          # one meta object
+               [WithMeta(a if i % 3 else b, 100 + i) for i in range(40)],         # two
+               [Bare(5 if i % 2 else 3, 200 + i) for i in range(40)]]             # none
+    assert community._dsyhost is not None, "the C column reader (dsy_host.c) is not built"
+    reader = community._dsyhost
+    try:
+        for use_c in (True, False):  # the C column reader and the Python path store the same columns
+            community._dsyhost = reader if use_c else None
+            store = SyncStore.from_rows([(1, 1, 3, 0, b"x")], ctx=object())
+            com = SyncCommunity(store, [a, b], global_time=1)
+            for msgs in batches:
+                rows = com.store_messages(msgs)
+                assert store.meta[rows].tolist() == [m.database_id for m in msgs]
+                assert store.global_time[rows].tolist() == [m.distribution.global_time for m in msgs]
+                assert [store.packet(int(r)) for r in rows] == [m.packet for m in msgs]
+            assert com.global_time == 239
+    finally:
+        community._dsyhost = reader
+
+
+def test_message_columns_reader():
+    """dsy_host.c message_columns: one pass over a message list -- global times (any integer type), packets, the
+    bytes packets' gather list, the one-meta test by identity -- and the errors the Python getters would raise."""
+    from dispersy_amd.community import _dsyhost
+
+    assert _dsyhost is not None, "the C column reader (dsy_host.c) is not built"
+
+    class D(object):
+        def __init__(self, gt):
+            self.global_time = gt
+
+    class M(object):
+        def __init__(self, gt, packet, **kw):
+            self.distribution, self.packet = D(gt), packet
+            self.__dict__.update(kw)
+
+    def run(msgs):
+        n = len(msgs)
+        gts, lens, addrs = (np.zeros(n, dtype=np.uint64) for _ in range(3))
+        out = _dsyhost.message_columns(msgs, gts, lens, addrs)
+        return out, gts, lens, addrs
+
+    meta = object()
+    msgs = [M(np.uint64(2 ** 63 + 5), b"abc", meta=meta), M(7, b"", meta=meta), M(np.int32(9), b"\x00" * 300, meta=meta)]
+    (packets, one, first, all_bytes), gts, lens, addrs = run(msgs)
+    assert packets == [m.packet for m in msgs] and packets is not msgs
+    assert one and first is meta and all_bytes
+    assert gts.tolist() == [2 ** 63 + 5, 7, 9] and lens.tolist() == [3, 0, 300]
+    # the addresses are the bytes' own buffers
+    import ctypes
+    assert ctypes.string_at(int(addrs[0]), 3) == b"abc" and ctypes.string_at(int(addrs[2]), 300) == b"\x00" * 300
+    # a second meta object, no meta (None), and a packet that is not exactly bytes
+    (_, one, first, all_bytes), _, _, _ = run([M(1, b"a", meta=meta), M(2, bytearray(b"b"), meta=object())])
+    assert not one and first is None and not all_bytes
+    (_, one, first, _), _, _, _ = run([M(1, b"a"), M(2, b"b")])
+    assert one and first is None
+    with pytest.raises(OverflowError):
+        run([M(-1, b"a")])
+    with pytest.raises(TypeError):
+        run([M(1.5, b"a")])
+    with pytest.raises(AttributeError):
+        run([M(1, b"a"), object()])
+    with pytest.raises(ValueError):
+        _dsyhost.message_columns([M(1, b"a"), M(2, b"b")], np.zeros(1, dtype=np.uint64), np.zeros(2, dtype=np.uint64),
+                                 np.zeros(2, dtype=np.uint64))
+    with pytest.raises(TypeError):
+        run(tuple(msgs))

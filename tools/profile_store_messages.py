@@ -25,10 +25,14 @@ class Dist(object):
 
 
 class Msg(object):
-    database_id = 1
+    """As the reference's Message.Implementation: .meta, and database_id read through it (message.py:265-266)."""
 
-    def __init__(self, gt, packet):
-        self.distribution, self.packet, self.candidate = Dist(gt), packet, None
+    def __init__(self, gt, packet, meta):
+        self.meta, self.distribution, self.packet, self.candidate = meta, Dist(gt), packet, None
+
+    @property
+    def database_id(self):
+        return self.meta.database_id
 
 
 def main():
@@ -40,13 +44,14 @@ def main():
     rows = [(i + 1, i + 1, 1, 0, blob[int(cuts[i]):int(cuts[i + 1])]) for i in range(n0)]
     store = SyncStore.from_rows(rows)
     store.handle  # noqa: B018
-    com = SyncCommunity(store, [MetaMessage("bench", 1, SyncDistribution("ASC", 128))], global_time=n0)
+    meta = MetaMessage("bench", 1, SyncDistribution("ASC", 128))
+    com = SyncCommunity(store, [meta], global_time=n0)
     work = []
     for b in range(12):
         bl = rng.integers(100, 1501, size=batch)
         data = rng.bytes(int(bl.sum()))
         c = np.concatenate([[0], np.cumsum(bl)])
-        work.append([Msg(n0 + b * batch + j + 1, data[int(c[j]):int(c[j + 1])]) for j in range(batch)])
+        work.append([Msg(n0 + b * batch + j + 1, data[int(c[j]):int(c[j + 1])], meta) for j in range(batch)])
     com.store_messages(work[0])
     times = []
     for msgs in work[1:6]:
