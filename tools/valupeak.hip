@@ -18,11 +18,11 @@
         }                                                                                          \
     } while (0)
 
-enum Op { kAdd = 0, kXor, kAlign, kAdd3, kBfi, kBitop3, kXad, kMix, kAlignConst, kRotConst, kAddLit, kAdd3S, kPerm, kLshlOr, kNOps };
+enum Op { kAdd = 0, kXor, kAlign, kAdd3, kBfi, kBitop3, kXad, kMix, kAlignConst, kRotConst, kAddLit, kAdd3S, kPerm, kLshlOr, kLshl64, kLshlAdd64, kMov64, kCndmask, kNOps };
 static const char* kNames[] = {"v_add_u32", "v_xor_b32", "v_alignbit_b32", "v_add3_u32", "v_bfi_b32",
                                "v_bitop3_b32", "v_xad_u32", "mix(add3,align,bfi,xor)", "v_alignbit x,y,5",
                                "v_alignbit x,x,5 (rotate)", "v_add_u32 literal", "v_add3_u32 x,y,sgpr", "v_perm_b32",
-                               "v_lshl_or_b32"};
+                               "v_lshl_or_b32", "v_lshlrev_b64", "v_lshl_add_u64", "v_mov_b64", "v_cndmask_b32 (sgpr mask)"};
 
 #define STEP3(OPSTR, X, Y, Z) asm volatile(OPSTR : "+v"(X) : "v"(Y), "v"(Z))
 #define STEP2(OPSTR, X, Y) asm volatile(OPSTR : "+v"(X) : "v"(Y))
@@ -44,6 +44,21 @@ __device__ __forceinline__ void step8(uint32_t* a, uint32_t y, uint32_t z) {
         else if (OP == kAdd3S) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(a[c]) : "v"(y), "s"(z));
         else if (OP == kPerm) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a[c]) : "v"(y), "v"(z));
         else if (OP == kLshlOr) asm volatile("v_lshl_or_b32 %0, %0, 5, %1" : "+v"(a[c]) : "v"(y));
+        else if (OP == kLshl64 || OP == kLshlAdd64 || OP == kMov64) {
+            // 64-bit operands: the chain's register and the next one as a pair (c even), counted as one lane-op
+            if ((c & 1) == 0) {
+                uint64_t v = ((uint64_t)a[c + 1] << 32) | a[c];
+                const uint64_t w = ((uint64_t)y << 32) | z;
+                if (OP == kLshl64) asm volatile("v_lshlrev_b64 %0, 1, %0" : "+v"(v));
+                else if (OP == kLshlAdd64) asm volatile("v_lshl_add_u64 %0, %0, 7, %1" : "+v"(v) : "v"(w));
+                else asm volatile("v_mov_b64 %0, %1" : "+v"(v) : "v"(w));
+                a[c] = (uint32_t)v;
+                a[c + 1] = (uint32_t)(v >> 32);
+            }
+        } else if (OP == kCndmask) {
+            const uint64_t m = 0x5555555555555555ull ^ z;
+            asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[c]) : "v"(y), "s"(m));
+        }
         else {
             if ((c & 3) == 0) STEP3("v_add3_u32 %0, %0, %1, %2", a[c], y, z);
             else if ((c & 3) == 1) STEP3("v_alignbit_b32 %0, %0, %1, %2", a[c], y, z);
@@ -112,9 +127,17 @@ int main(int argc, char** argv) {
         r[11] = run<kAdd3S>(d_out, cus, iters, wg);
         r[12] = run<kPerm>(d_out, cus, iters, wg);
         r[13] = run<kLshlOr>(d_out, cus, iters, wg);
-        for (int i = 0; i < kNOps; ++i)
+        r[14] = run<kLshl64>(d_out, cus, iters, wg);
+        r[15] = run<kLshlAdd64>(d_out, cus, iters, wg);
+        r[16] = run<kMov64>(d_out, cus, iters, wg);
+        r[17] = run<kCndmask>(d_out, cus, iters, wg);
+        for (int i = 0; i < kNOps; ++i) {
+            // the 64-bit rows issue 4 instructions per 8 chains: report instructions x lanes
+            const double f = (i == kLshl64 || i == kLshlAdd64 || i == kMov64) ? 0.5 : 1.0;
+            r[i] *= f;
             printf("wg/CU=%d %-26s %7.2f T lane-ops/s  = %6.1f lane-ops/CU/clk @2.4GHz\n", wg, kNames[i], r[i] / 1e12,
                    r[i] / cus / 2.4e9);
+        }
     }
     return 0;
 }
