@@ -17,10 +17,8 @@ Launch:  python bench.py [--gpus N --steps K --warmup W]
 """
 import argparse
 import ctypes
-import itertools
 import json
 import math
-import operator
 import os
 import sys
 import time
@@ -667,10 +665,8 @@ def dropin_bench(args, ctx, lib, store, offsets, N, claims, reps=5, batch=10_000
         t0 = time.perf_counter()
         got = com.respond(reqs, byte_limit=args.byte_limit, random_seed=99)
         times.append(time.perf_counter() - t0)
-        t0 = time.perf_counter()  # respond()'s Python part: the claims' ranges and their filters' addresses
-        np.fromiter(itertools.chain.from_iterable(map(operator.itemgetter(0, 1, 2, 3), reqs)), dtype=np.uint64,
-                    count=4 * len(reqs))
-        b"".join(map(operator.attrgetter("_refs"), map(operator.itemgetter(4), reqs)))
+        t0 = time.perf_counter()  # respond()'s host part: the claims' ranges and their filters' addresses
+        SyncCommunity._claim_columns(reqs)
         rec_t.append(time.perf_counter() - t0)
         rows = sum(len(g) for g in got)
     ms = sorted(times)[len(times) // 2] * 1e3
@@ -678,7 +674,7 @@ def dropin_bench(args, ctx, lib, store, offsets, N, claims, reps=5, batch=10_000
     respond = {"call": "SyncCommunity.respond(1024 ClaimRequests) -> dsy_sync_respond_refs (host buffers)",
                "median_ms_per_batch": round(ms, 3), "claims_per_s": round(len(reqs) / (ms / 1e3), 1),
                "rows_returned": rows,
-               "host_phases_ms": {"claim ranges + (record, filter) addresses (Python)": round(rec_ms, 3),
+               "host_phases_ms": {"claim ranges + (record, filter) addresses (SyncCommunity._claim_columns)": round(rec_ms, 3),
                                   "dsy_sync_respond_refs (filter gather + upload behind the selection, device step, "
                                   "result download)": round(ms - rec_ms, 3)}}
 

@@ -29,7 +29,7 @@ from . import _native
 from .bloomfilter import BloomFilter
 from .distribution import FullSyncDistribution, GlobalTimePruning, LastSyncDistribution, SyncDistribution
 
-try:  # store_messages' column reader in C (csrc/dsy_host.c, built beside libdsybloom.so); same results as the Python path
+try:  # store_messages' / respond's column reads in C (csrc/dsy_host.c, built beside libdsybloom.so; = the Python path)
     from . import _dsyhost
 except ImportError:  # an unbuilt tree
     _dsyhost = None
@@ -759,14 +759,29 @@ class SyncCommunity(object):
         if not R:
             return self._respond_requests(np.zeros(1, dtype=_REQUEST_DTYPE), 0, b"", include_inactive, byte_limit,
                                           random_seed)
-        try:
-            ranges = np.fromiter(itertools.chain.from_iterable(map(_RANGE_OF, requests)), dtype=np.uint64, count=4 * R)
-        except OverflowError:  # a bound past 2^64: clamp in Python first (the library clamps to 2^63-1)
-            ranges = np.fromiter(itertools.chain.from_iterable((min(q.time_low, MAX_GT), min(q.time_high, MAX_GT),
-                                                                q.modulo, q.offset) for q in requests),
-                                 dtype=np.uint64, count=4 * R)
-        refs = b"".join(map(_REFS_OF, map(_BLOOM_OF, requests)))
+        ranges, refs = self._claim_columns(requests)
         return self._respond_requests(None, R, None, include_inactive, byte_limit, random_seed, (ranges, refs))
+
+    @staticmethod
+    def _claim_columns(requests):
+        """respond()'s per-claim columns: the four range fields (uint64 x 4R) and the BloomFilters' (record, filter)
+        address pairs (16 B each)."""
+        R = len(requests)
+        if _dsyhost is not None and type(requests) in (list, tuple):
+            # one C pass (dsy_host.c claim_columns): the ranges (time bounds past 2^64 stored as 2^63-1) and addresses
+            ranges, ref_words = np.empty(4 * R, dtype=np.uint64), np.empty(2 * R, dtype=np.uint64)
+            _dsyhost.claim_columns(requests, ranges, ref_words)
+            refs = ref_words.tobytes()
+        else:
+            try:
+                ranges = np.fromiter(itertools.chain.from_iterable(map(_RANGE_OF, requests)), dtype=np.uint64,
+                                     count=4 * R)
+            except OverflowError:  # a bound past 2^64: clamp in Python first (the library clamps to 2^63-1)
+                ranges = np.fromiter(itertools.chain.from_iterable((min(q.time_low, MAX_GT), min(q.time_high, MAX_GT),
+                                                                    q.modulo, q.offset) for q in requests),
+                                     dtype=np.uint64, count=4 * R)
+            refs = b"".join(map(_REFS_OF, map(_BLOOM_OF, requests)))
+        return ranges, refs
 
     @staticmethod
     def _request_table(requests):

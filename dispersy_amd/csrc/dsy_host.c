@@ -1,4 +1,4 @@
-/* _dsyhost: the columns SyncCommunity.store_messages reads from a batch of received messages, in one C pass.
+/* _dsyhost: the columns the drop-in host path reads from Python objects, in one C pass each (store_messages, respond).
  *
  * Dispersy._store (dispersy.py:1475-1533) walks its messages one by one for the INSERT's values: the packet, the
  * distribution's global time and the meta's database id.  The Python mirror (dispersy_amd/community.py
@@ -14,21 +14,102 @@
  *                bytes; all_bytes says whether they all were (else the caller takes its byte-joining path)
  *     packets  = [m.packet for m in messages] (new list, the packets' references: they keep the bytes alive)
  *     one_meta = every message's .meta (None when it has none) is the first message's object; first_meta = that.
+ *
+ * SyncCommunity.respond (community.py:2531-2572 in the reference) hands the library, per claim, the four range fields
+ * of its ClaimRequest and the 16-byte (record, filter) address pair its BloomFilter keeps (BloomFilter._refs):
+ *
+ *   claim_columns(requests, ranges, refs) -> None
+ *     requests: a list or tuple of ClaimRequests (tuples: time_low, time_high, modulo, offset, bloom, ...);
+ *     ranges: writable uint64 buffer of 4 x len(requests); refs: writable buffer of 16 x len(requests) bytes.
+ *     A time bound past 2^64 - 1 is stored as 2^63 - 1 (the library clamps every bound there, community.py:2545-2548);
+ *     a negative value, or a modulo / offset past 2^64 - 1, raises OverflowError, as numpy's conversion does.
  */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 #include <stdint.h>
+#include <string.h>
 
-static PyObject *s_distribution, *s_global_time, *s_packet, *s_meta;
+static PyObject *s_distribution, *s_global_time, *s_packet, *s_meta, *s_refs;
 
 static int get_u64_buffer(PyObject *obj, Py_buffer *view, Py_ssize_t n, const char *name) {
     if (PyObject_GetBuffer(obj, view, PyBUF_WRITABLE | PyBUF_C_CONTIGUOUS) < 0) return -1;
     if (view->len < n * (Py_ssize_t)sizeof(uint64_t)) {
         PyBuffer_Release(view);
-        PyErr_Format(PyExc_ValueError, "message_columns: %s holds fewer than %zd uint64", name, n);
+        PyErr_Format(PyExc_ValueError, "%s holds fewer than %zd uint64", name, n);
         return -1;
     }
     return 0;
+}
+
+/* an integer (int or an __index__ type) as uint64; clamp: a value past 2^64 - 1 becomes 2^63 - 1 instead of raising */
+static int as_u64(PyObject *v, int clamp, uint64_t *out) {
+    PyObject *i = PyNumber_Index(v);
+    if (!i) return -1;
+    const unsigned long long x = PyLong_AsUnsignedLongLong(i);
+    if (x == (unsigned long long)-1 && PyErr_Occurred()) {
+        if (clamp && PyErr_ExceptionMatches(PyExc_OverflowError) && _PyLong_Sign(i) > 0) {
+            PyErr_Clear();
+            Py_DECREF(i);
+            *out = (uint64_t)INT64_MAX;
+            return 0;
+        }
+        Py_DECREF(i);
+        return -1;
+    }
+    Py_DECREF(i);
+    *out = (uint64_t)x;
+    return 0;
+}
+
+static PyObject *claim_columns(PyObject *self, PyObject *args) {
+    PyObject *requests, *o_ranges, *o_refs;
+    (void)self;
+    if (!PyArg_ParseTuple(args, "OOO", &requests, &o_ranges, &o_refs)) return NULL;
+    if (!PyList_Check(requests) && !PyTuple_Check(requests)) {
+        PyErr_SetString(PyExc_TypeError, "claim_columns: requests must be a list or tuple");
+        return NULL;
+    }
+    PyObject *seq = PySequence_Fast(requests, "claim_columns: requests must be a sequence");
+    if (!seq) return NULL;
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+    PyObject **items = PySequence_Fast_ITEMS(seq);
+    Py_buffer vr, vf;
+    if (get_u64_buffer(o_ranges, &vr, 4 * n, "ranges") < 0) {
+        Py_DECREF(seq);
+        return NULL;
+    }
+    if (get_u64_buffer(o_refs, &vf, 2 * n, "refs") < 0) {
+        PyBuffer_Release(&vr);
+        Py_DECREF(seq);
+        return NULL;
+    }
+    uint64_t *ranges = (uint64_t *)vr.buf;
+    char *refs = (char *)vf.buf;
+    PyObject *ret = NULL;
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        PyObject *q = items[i];
+        if (!PyTuple_Check(q) || PyTuple_GET_SIZE(q) < 5) {
+            PyErr_SetString(PyExc_TypeError, "claim_columns: a request is a ClaimRequest tuple");
+            goto done;
+        }
+        for (int f = 0; f < 4; ++f)
+            if (as_u64(PyTuple_GET_ITEM(q, f), f < 2, &ranges[4 * i + f]) < 0) goto done;
+        PyObject *r = PyObject_GetAttr(PyTuple_GET_ITEM(q, 4), s_refs);
+        if (!r) goto done;
+        if (!PyBytes_Check(r) || PyBytes_GET_SIZE(r) != 16) {
+            Py_DECREF(r);
+            PyErr_SetString(PyExc_ValueError, "claim_columns: BloomFilter._refs is not 16 bytes");
+            goto done;
+        }
+        memcpy(refs + 16 * i, PyBytes_AS_STRING(r), 16);
+        Py_DECREF(r);
+    }
+    ret = Py_NewRef(Py_None);
+done:
+    PyBuffer_Release(&vr);
+    PyBuffer_Release(&vf);
+    Py_DECREF(seq);
+    return ret;
 }
 
 static PyObject *message_columns(PyObject *self, PyObject *args) {
@@ -117,9 +198,10 @@ done:
 static PyMethodDef methods[] = {
     {"message_columns", message_columns, METH_VARARGS,
      "message_columns(messages, gts, lens, addrs) -> (packets, one_meta, first_meta, all_bytes)"},
+    {"claim_columns", claim_columns, METH_VARARGS, "claim_columns(requests, ranges, refs) -> None"},
     {NULL, NULL, 0, NULL}};
 
-static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_dsyhost", "store_messages' column reads in C", -1,
+static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_dsyhost", "the drop-in host path's column reads in C (store_messages, respond)", -1,
                                     methods, NULL, NULL, NULL, NULL};
 
 PyMODINIT_FUNC PyInit__dsyhost(void) {
@@ -127,6 +209,7 @@ PyMODINIT_FUNC PyInit__dsyhost(void) {
     s_global_time = PyUnicode_InternFromString("global_time");
     s_packet = PyUnicode_InternFromString("packet");
     s_meta = PyUnicode_InternFromString("meta");
-    if (!s_distribution || !s_global_time || !s_packet || !s_meta) return NULL;
+    s_refs = PyUnicode_InternFromString("_refs");
+    if (!s_distribution || !s_global_time || !s_packet || !s_meta || !s_refs) return NULL;
     return PyModule_Create(&module);
 }
