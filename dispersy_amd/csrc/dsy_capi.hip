@@ -2023,6 +2023,15 @@ static int job_window(dsy_ctx* c, RespondSlot& sl) {
         for (uint32_t k = 0; k < chunks; ++k) {
             const uint32_t r0 = (uint32_t)((uint64_t)fg.R * k / chunks), r1 = (uint32_t)((uint64_t)fg.R * (k + 1) / chunks);
             for (uint32_t r = r0; r < r1; ++r) {
+                // two scattered objects per claim (its record, its filter bytes): touch those of the claim
+                // kPrefetch ahead so their misses overlap this claim's copy
+                constexpr uint32_t kPrefetch = 6;
+                if (r + kPrefetch < fg.R) {
+                    const uint8_t* nf = (const uint8_t*)(uintptr_t)fg.refs[2 * (size_t)(r + kPrefetch) + 1];
+                    __builtin_prefetch((const void*)(uintptr_t)fg.refs[2 * (size_t)(r + kPrefetch)]);
+                    __builtin_prefetch(nf);
+                    __builtin_prefetch(nf + 64);
+                }
                 const uint64_t n = ((const dsy_request*)(uintptr_t)fg.refs[2 * (size_t)r])->m_bits / 8;
                 uint8_t* dst = h + fg.foff[r];
                 memcpy(dst, (const void*)(uintptr_t)fg.refs[2 * (size_t)r + 1], n);
