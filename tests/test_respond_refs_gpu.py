@@ -57,6 +57,30 @@ def test_gather_equals_blob_and_oracle(shapes):
             assert store.rowid[g].tolist() == want, (q.time_low, q.time_high, q.modulo, q.offset, limit)
 
 
+def test_gather_of_many_claims_on_two_threads():
+    """>= 256 claims: the library gathers the filters in four chunks, each uploaded while the next is copied -- the
+    answers equal the caller-packed blob path's for every claim (no gather there) and the oracle's for a sample."""
+    rows, conn = build(12, 6_000, 30_000, False)
+    store = SyncStore.from_rows(rows)
+    gt_now = 30_100
+    chosen = [m for m in METAS if m[0] in ("a", "d")]
+    com = SyncCommunity(store, [MetaMessage(n, i, SyncDistribution(d, p, None)) for n, i, d, p, _ in chosen],
+                        global_time=gt_now)
+    served_oracle = [dict(name=n, id=i, direction=d, priority=p, pruning=None) for n, i, d, p, _ in chosen]
+    shapes = [(10160, 0.01), (4096, 0.001), (1 << 15, 0.01), (8, 0.5), (10168, 0.01)]
+    reqs, blooms = _claims(rows, gt_now, np.random.Generator(np.random.PCG64(9)), shapes, 300)
+    for rep in range(3):  # the ctx's staging and filters workspace are reused call after call
+        got = com.respond(reqs, byte_limit=4096, random_seed=11 + rep)
+        packed, R, blob = com.request_records(reqs)
+        want_blob = com._respond_requests(packed, R, blob, False, 4096, 11 + rep)
+        assert [g.tolist() for g in got] == [b.tolist() for b in want_blob]
+    for i in range(0, 300, 15):
+        q = reqs[i]
+        want = sync_ref.respond_lists(conn, served_oracle, (q.time_low, q.time_high, q.offset, q.modulo), blooms[i],
+                                      gt_now, 4096, False)
+        assert store.rowid[got[i]].tolist() == want, i
+
+
 def test_refs_layout_and_argument_checks():
     rows, _ = build(12, 2_000, 9_000, False)
     store = SyncStore.from_rows(rows)
