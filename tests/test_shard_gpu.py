@@ -100,3 +100,19 @@ def test_cfg4_one_rank_add_sharded_equals_single_build():
         whole = BloomFilter(m, f, prefix)
         whole.add_packed(blob, offs)
         assert union.cpu().numpy().tobytes()[:m // 8] == whole.bytes
+
+
+def test_rccl_collectives_one_rank():
+    """The collectives Collectives issues over RCCL ("nccl"), with the dtypes the jobs pass -- int64 / float64
+    scalars (all-reduce SUM / MAX), int32 and int64 all-gathers, a uint8 all-to-all(v) with byte splits -- in a
+    one-rank torchrun job on cuda:0 (tools/rccl_probe.py).  Two ranks cannot share one GPU under RCCL ("Duplicate GPU
+    detected"), so the two-rank exchanges above run over gloo; this pins the RCCL calls themselves."""
+    port = str(_free_port())
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", port, os.path.join(os.path.dirname(HERE), "tools", "rccl_probe.py")]
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=120)
+    log = p.stdout.decode(errors="replace")
+    assert p.returncode == 0, log[-3000:]
+    row = json.loads([ln for ln in log.splitlines() if ln.startswith("{")][-1])
+    assert row == {"rank": 0, "world": 1, "backend": "nccl", "sum_i64": 1, "max_f64": 0.5, "gather_i32": [0, 10, 20],
+                   "gather_i64": [2 ** 40], "a2av_ok": True}
