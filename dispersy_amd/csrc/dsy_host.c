@@ -87,6 +87,11 @@ static PyObject *claim_columns(PyObject *self, PyObject *args) {
     char *refs = (char *)vf.buf;
     PyObject *ret = NULL;
     for (Py_ssize_t i = 0; i < n; ++i) {
+        /* (a getter may run Python code: the sequence must keep its length) */
+        if (PySequence_Fast_GET_SIZE(seq) != n) {
+            PyErr_SetString(PyExc_RuntimeError, "claim_columns: the request list changed size");
+            goto done;
+        }
         PyObject *q = items[i];
         if (!PyTuple_Check(q) || PyTuple_GET_SIZE(q) < 5) {
             PyErr_SetString(PyExc_TypeError, "claim_columns: a request is a ClaimRequest tuple");
@@ -94,7 +99,9 @@ static PyObject *claim_columns(PyObject *self, PyObject *args) {
         }
         for (int f = 0; f < 4; ++f)
             if (as_u64(PyTuple_GET_ITEM(q, f), f < 2, &ranges[4 * i + f]) < 0) goto done;
+        Py_INCREF(q); /* (held while its filter's getter runs) */
         PyObject *r = PyObject_GetAttr(PyTuple_GET_ITEM(q, 4), s_refs);
+        Py_DECREF(q);
         if (!r) goto done;
         if (!PyBytes_Check(r) || PyBytes_GET_SIZE(r) != 16) {
             Py_DECREF(r);
@@ -110,6 +117,52 @@ done:
     PyBuffer_Release(&vf);
     Py_DECREF(seq);
     return ret;
+}
+
+/* message i's columns (message_columns); 0, or -1 with the exception set */
+static int read_message(PyObject *m, Py_ssize_t i, uint64_t *gts, uint64_t *lens, uint64_t *addrs, PyObject *packets,
+                        PyObject **first, int *one_meta, int *all_bytes) {
+    /* global time: m.distribution.global_time, any integer (int or an __index__ type such as numpy's) */
+    PyObject *dist = PyObject_GetAttr(m, s_distribution);
+    if (!dist) return -1;
+    PyObject *gt = PyObject_GetAttr(dist, s_global_time);
+    Py_DECREF(dist);
+    if (!gt) return -1;
+    PyObject *gti = PyNumber_Index(gt);
+    Py_DECREF(gt);
+    if (!gti) return -1;
+    const unsigned long long g = PyLong_AsUnsignedLongLong(gti);
+    Py_DECREF(gti);
+    if (g == (unsigned long long)-1 && PyErr_Occurred()) return -1;
+    gts[i] = (uint64_t)g;
+    /* packet (the list keeps the reference, and with it the bytes the gather list points into) */
+    PyObject *p = PyObject_GetAttr(m, s_packet);
+    if (!p) return -1;
+    PyList_SET_ITEM(packets, i, p); /* steals the reference */
+    if (*all_bytes) {
+        if (PyBytes_CheckExact(p)) {
+            lens[i] = (uint64_t)PyBytes_GET_SIZE(p);
+            addrs[i] = (uint64_t)(uintptr_t)PyBytes_AS_STRING(p);
+        } else {
+            *all_bytes = 0;
+        }
+    }
+    /* meta: getattr(m, "meta", None) compared by identity with the first message's */
+    if (*one_meta) {
+        PyObject *meta = PyObject_GetAttr(m, s_meta);
+        if (!meta) {
+            if (!PyErr_ExceptionMatches(PyExc_AttributeError)) return -1;
+            PyErr_Clear();
+            meta = Py_NewRef(Py_None);
+        }
+        if (i == 0) {
+            *first = meta; /* keeps the reference */
+        } else {
+            if (meta != *first) *one_meta = 0;
+            Py_DECREF(meta);
+        }
+    }
+    return 0;
 }
 
 static PyObject *message_columns(PyObject *self, PyObject *args) {
@@ -133,48 +186,17 @@ static PyObject *message_columns(PyObject *self, PyObject *args) {
     int one_meta = 1, all_bytes = 1;
     if (!packets) goto done;
     for (Py_ssize_t i = 0; i < n; ++i) {
+        /* (the getters may run Python code -- properties --: the list must keep its length, and the message is held
+           for the duration) */
+        if (PyList_GET_SIZE(messages) != n) {
+            PyErr_SetString(PyExc_RuntimeError, "message_columns: the message list changed size");
+            goto fail;
+        }
         PyObject *m = PyList_GET_ITEM(messages, i);
-        /* global time: m.distribution.global_time, any integer (int or an __index__ type such as numpy's) */
-        PyObject *dist = PyObject_GetAttr(m, s_distribution);
-        if (!dist) goto fail;
-        PyObject *gt = PyObject_GetAttr(dist, s_global_time);
-        Py_DECREF(dist);
-        if (!gt) goto fail;
-        PyObject *gti = PyNumber_Index(gt);
-        Py_DECREF(gt);
-        if (!gti) goto fail;
-        const unsigned long long g = PyLong_AsUnsignedLongLong(gti);
-        Py_DECREF(gti);
-        if (g == (unsigned long long)-1 && PyErr_Occurred()) goto fail;
-        gts[i] = (uint64_t)g;
-        /* packet */
-        PyObject *p = PyObject_GetAttr(m, s_packet);
-        if (!p) goto fail;
-        PyList_SET_ITEM(packets, i, p); /* steals the reference */
-        if (all_bytes) {
-            if (PyBytes_CheckExact(p)) {
-                lens[i] = (uint64_t)PyBytes_GET_SIZE(p);
-                addrs[i] = (uint64_t)(uintptr_t)PyBytes_AS_STRING(p);
-            } else {
-                all_bytes = 0;
-            }
-        }
-        /* meta: getattr(m, "meta", None) compared by identity with the first message's */
-        if (one_meta) {
-            PyObject *meta = PyObject_GetAttr(m, s_meta);
-            if (!meta) {
-                if (!PyErr_ExceptionMatches(PyExc_AttributeError)) goto fail;
-                PyErr_Clear();
-                meta = Py_None;
-                Py_INCREF(meta);
-            }
-            if (i == 0) {
-                first = meta; /* keeps the reference */
-            } else {
-                if (meta != first) one_meta = 0;
-                Py_DECREF(meta);
-            }
-        }
+        Py_INCREF(m);
+        const int ok = read_message(m, i, gts, lens, addrs, packets, &first, &one_meta, &all_bytes);
+        Py_DECREF(m);
+        if (ok < 0) goto fail;
     }
     if (!first) {
         first = Py_None;
