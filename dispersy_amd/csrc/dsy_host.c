@@ -97,10 +97,10 @@ static PyObject *claim_columns(PyObject *self, PyObject *args) {
             PyErr_SetString(PyExc_TypeError, "claim_columns: a request is a ClaimRequest tuple");
             goto done;
         }
-        for (int f = 0; f < 4; ++f)
-            if (as_u64(PyTuple_GET_ITEM(q, f), f < 2, &ranges[4 * i + f]) < 0) goto done;
-        Py_INCREF(q); /* (held while its filter's getter runs) */
-        PyObject *r = PyObject_GetAttr(PyTuple_GET_ITEM(q, 4), s_refs);
+        Py_INCREF(q); /* (held while its fields' __index__ and its filter's getter run) */
+        int bad = 0;
+        for (int f = 0; f < 4 && !bad; ++f) bad = as_u64(PyTuple_GET_ITEM(q, f), f < 2, &ranges[4 * i + f]) < 0;
+        PyObject *r = bad ? NULL : PyObject_GetAttr(PyTuple_GET_ITEM(q, 4), s_refs);
         Py_DECREF(q);
         if (!r) goto done;
         if (!PyBytes_Check(r) || PyBytes_GET_SIZE(r) != 16) {
