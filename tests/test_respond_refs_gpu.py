@@ -57,7 +57,7 @@ def test_gather_equals_blob_and_oracle(shapes):
             assert store.rowid[g].tolist() == want, (q.time_low, q.time_high, q.modulo, q.offset, limit)
 
 
-def test_gather_of_many_claims_on_two_threads():
+def test_gather_of_many_claims_in_chunks():
     """>= 256 claims: the library gathers the filters in four chunks, each uploaded while the next is copied -- the
     answers equal the caller-packed blob path's for every claim (no gather there) and the oracle's for a sample."""
     rows, conn = build(12, 6_000, 30_000, False)
