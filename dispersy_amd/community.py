@@ -514,7 +514,9 @@ class SyncCommunity(object):
         members = list(map(_member_id, messages)) if has_member else None
         double = ([i for i, meta in enumerate(meta_objs) if per_meta[id(meta)][2]]
                   if any(info[2] for info in per_meta.values()) else [])
-        pairs = [[int(x.database_id) for x in messages[i].authentication.members] for i in double]
+        # members[0] and members[1] (dispersy.py:1537-1538)
+        pairs = [(int(ms[0].database_id), int(ms[1].database_id))
+                 for ms in (messages[i].authentication.members for i in double)]
         rows = self._store.append(packets, gts, metas, member=members, sequence=seqs, _gather=cols)
         if double:  # INSERT INTO double_signed_sync (dispersy.py:1537-1541)
             p = np.asarray(pairs, dtype=np.int64).reshape(-1, 2)
@@ -537,6 +539,11 @@ class SyncCommunity(object):
         if self._store.member is None and (history or seq or double):
             raise ValueError("store_messages: meta %s keeps per-member history; the store needs its member column"
                              % getattr(meta, "name", "?"))
+        if history and double and not dist.custom_callback and not self._store.pairs_exported(meta.database_id):
+            # the per-pair history (:1567-1578) joins double_signed_sync: rows stored without it would be missed
+            raise ValueError("store_messages: meta %s keeps its history per member pair, but the store's rows of it "
+                             "were exported without their double_signed_sync table (SyncStore.from_rows / attach: "
+                             "pass pairs=)" % getattr(meta, "name", "?"))
         return seq, history, double
 
     def _last_sync_history(self, messages):
@@ -557,8 +564,9 @@ class SyncCommunity(object):
                         pass
                 continue
             if getattr(meta, "double_signed", False):  # per member pair, through double_signed_sync (:1567-1578)
-                for pair in OrderedDict.fromkeys(tuple(sorted(int(x.database_id) for x in m.authentication.members))
-                                                 for m in msgs):
+                for pair in OrderedDict.fromkeys(
+                        tuple(sorted((int(m.authentication.members[0].database_id),
+                                      int(m.authentication.members[1].database_id)))) for m in msgs):
                     rows = st.pair_rows(meta.database_id, *pair)
                     if len(rows) > dist.history_size:
                         drop.extend(rows[:len(rows) - dist.history_size].tolist())

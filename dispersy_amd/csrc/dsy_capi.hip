@@ -147,6 +147,7 @@ struct dsy_ctx {
     int pool_queue = 0;
     int pool_deal = 0;   // DSY_POOL_DEAL: the pooled hashing's resident-grid deal (k_pair_test<POOL>)
     int pair_prio = 1;   // DSY_PAIR_PRIO: k_pair_test raises the wave priority of long wave-tasks (0 off)
+    int pair_pipe = 1;   // DSY_PAIR_PIPE=0: the responder's line-staged hashing walks task after task (k_pair_test)
     int bulk_zero = 1;   // DSY_BULK_ZERO=0: the calls do not zero their split-window sort state (diagnostic)
     uint32_t direct_kinds = 0;  // DSY_PAIR_DIRECT: bit k = hash kind k's responder hashing uses direct loads
     uint32_t timing = 0;  // bit i: bracket class i with events
@@ -536,6 +537,7 @@ int dsy_ctx_create(int device, dsy_ctx** out) {
     if (const char* v = getenv("DSY_POOL_QUEUE")) c->pool_queue = atoi(v);
     if (const char* v = getenv("DSY_POOL_DEAL")) c->pool_deal = atoi(v);
     if (const char* v = getenv("DSY_PAIR_PRIO")) c->pair_prio = atoi(v);
+    if (const char* v = getenv("DSY_PAIR_PIPE")) c->pair_pipe = atoi(v);
     if (const char* v = getenv("DSY_BULK_ZERO")) c->bulk_zero = atoi(v);
     if (const char* v = getenv("DSY_PAIR_DIRECT")) c->direct_kinds = (uint32_t)strtoul(v, nullptr, 0);
     c->pool_kinds &= (1u << DSY_MD5) | (1u << DSY_SHA1) | (1u << DSY_SHA256);
@@ -1380,6 +1382,9 @@ static int store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, const uin
     HIP_TRY(hipMemcpyAsync(s->d_pend_meta + s->pend_n, up_meta, a * 4, hipMemcpyDeviceToDevice, c->stream));
     HIP_TRY(launch_store_lines(up, (const uint64_t*)up_off, s->d_rec + n0, a, const_cast<uint8_t*>(s->d_lines),
                                c->stream));
+    // the duplicate table first: if it cannot take the rows (DSY_ENOMEM growing it), nothing below is committed -- the
+    // queued index entries past pend_n are never read, and the store keeps its n rows
+    if (s->dup && (rc = dup_insert_dev(c, s, (const uint64_t*)up_mem, (const uint64_t*)up_gt, n0, a))) return rc;
     if (!s->pend_n) {
         s->pend_base = n0;
         s->pend_glo = ~0ull;
@@ -1396,7 +1401,6 @@ static int store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, const uin
         j = e;
     }
     s->pend_n += a;
-    if (s->dup && (rc = dup_insert_dev(c, s, (const uint64_t*)up_mem, (const uint64_t*)up_gt, n0, a))) return rc;
     s->min_len = n0 ? std::min(s->min_len, minlen) : minlen;
     s->n += a;
     s->blob_len += add;
@@ -2350,6 +2354,7 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const Clai
     L.pool_queue = c->pool_queue;
     L.pool_deal = c->pool_deal;
     L.pair_prio = c->pair_prio;
+    L.pair_pipe = c->pair_pipe;
     L.bulk_zero = c->bulk_zero;
     L.pool_counts = (PoolCounts*)d_pool_counts;
     if ((rc = job_pair_buffers(sl, pool))) return rc;

@@ -69,10 +69,11 @@ static PyObject *claim_columns(PyObject *self, PyObject *args) {
         PyErr_SetString(PyExc_TypeError, "claim_columns: requests must be a list or tuple");
         return NULL;
     }
-    PyObject *seq = PySequence_Fast(requests, "claim_columns: requests must be a sequence");
+    /* a tuple snapshot: it holds a reference to every request, so a getter that mutates the caller's list (even
+       keeping its length, which may reallocate a list's item array) cannot leave this loop reading freed memory */
+    PyObject *seq = PySequence_Tuple(requests);
     if (!seq) return NULL;
-    const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
-    PyObject **items = PySequence_Fast_ITEMS(seq);
+    const Py_ssize_t n = PyTuple_GET_SIZE(seq);
     Py_buffer vr, vf;
     if (get_u64_buffer(o_ranges, &vr, 4 * n, "ranges") < 0) {
         Py_DECREF(seq);
@@ -87,21 +88,14 @@ static PyObject *claim_columns(PyObject *self, PyObject *args) {
     char *refs = (char *)vf.buf;
     PyObject *ret = NULL;
     for (Py_ssize_t i = 0; i < n; ++i) {
-        /* (a getter may run Python code: the sequence must keep its length) */
-        if (PySequence_Fast_GET_SIZE(seq) != n) {
-            PyErr_SetString(PyExc_RuntimeError, "claim_columns: the request list changed size");
-            goto done;
-        }
-        PyObject *q = items[i];
+        PyObject *q = PyTuple_GET_ITEM(seq, i);
         if (!PyTuple_Check(q) || PyTuple_GET_SIZE(q) < 5) {
             PyErr_SetString(PyExc_TypeError, "claim_columns: a request is a ClaimRequest tuple");
             goto done;
         }
-        Py_INCREF(q); /* (held while its fields' __index__ and its filter's getter run) */
         int bad = 0;
         for (int f = 0; f < 4 && !bad; ++f) bad = as_u64(PyTuple_GET_ITEM(q, f), f < 2, &ranges[4 * i + f]) < 0;
         PyObject *r = bad ? NULL : PyObject_GetAttr(PyTuple_GET_ITEM(q, 4), s_refs);
-        Py_DECREF(q);
         if (!r) goto done;
         if (!PyBytes_Check(r) || PyBytes_GET_SIZE(r) != 16) {
             Py_DECREF(r);

@@ -1354,6 +1354,11 @@ static hipError_t pair_test_family(const RespondLaunch& L, bool long_prefix, con
     if constexpr (dma) {
         if (!long_prefix && !((L.direct_kinds >> H::kind) & 1u)) {
             const size_t lds = 4 * DmaGeometry<2, 1>::kWaveBytes;
+            if (CHUNK <= 4 && L.pair_pipe && !pooled && (uint64_t)n_list * (L.window / 64) < (1ull << 32) &&
+                L.st.lines_bytes < (1ull << 36)) {
+                launch_pair_pipe(L, H::kind, CHUNK, list, n_list, (uint32_t)blocks, lds);
+                return hipGetLastError();
+            }
             auto kern = pooled ? k_pair_test<H, CHUNK, true, 0, true> : k_pair_test<H, CHUNK, true>;
             if constexpr (CHUNK == 2) {  // (respond_core pools no family while a diagnostic build is asked for)
                 if (L.diag == 1) kern = k_pair_test<H, CHUNK, true, 1>;

@@ -59,6 +59,126 @@ _BYTES_DATA = _bytes_data_offset()
 _ONLY_BYTES = {bytes}
 
 
+class _LiveRows(object):
+    """One meta's live rows (undone == 0, not deleted) in the index order (global_time, row): a sorted base array
+    (its global times beside it) whose removed rows are tombstones, and the rows added since (appended, or live again
+    after a redo), merged on read.  Every change is O(its rows) -- a DELETE or an undo of 100 rows does not copy a
+    10 M-row segment, a GlobalTimePruning cut is a binary search and a slice (round-4 verdict); rows() materialises
+    the order (O(segment), only when a host-side reader asks for it)."""
+    __slots__ = ("base", "gbase", "dead_base", "added", "dead_added", "n")
+
+    def __init__(self, base, gbase):
+        self.base = base
+        self.gbase = gbase         # global_time of base's rows (ascending)
+        self.dead_base = set()     # tombstones: rows of base no longer live
+        self.added = []            # arrays of rows added since base was built
+        self.dead_added = set()    # rows of `added` no longer live
+        self.n = len(base)
+
+    def _in_base(self, rows, gt):
+        """Whether each of `rows` sits in base (else: in added): its global time's run of base, searched."""
+        g = gt[rows]
+        lo = np.searchsorted(self.gbase, g, side="left")
+        hi = np.searchsorted(self.gbase, g, side="right")
+        out = np.zeros(len(rows), dtype=bool)
+        for j in np.flatnonzero(hi > lo).tolist():
+            run = self.base[lo[j]:hi[j]]  # rows of one global time, ascending
+            i = int(np.searchsorted(run, rows[j]))
+            out[j] = i < len(run) and run[i] == rows[j]
+        return out
+
+    def add(self, rows, gt):
+        if self.dead_base or self.dead_added:  # live again where they still sit (a redo of a row undone earlier)
+            back_b = [r for r in rows.tolist() if r in self.dead_base]
+            back_a = [r for r in rows.tolist() if r in self.dead_added]
+            if back_b or back_a:
+                self.dead_base.difference_update(back_b)
+                self.dead_added.difference_update(back_a)
+                self.n += len(back_b) + len(back_a)
+                rows = rows[~np.isin(rows, back_b + back_a)]
+        if len(rows):
+            self.added.append(rows)
+            self.n += len(rows)
+
+    def remove(self, rows, gt):
+        where = self._in_base(rows, gt)
+        self.dead_base.update(rows[where].tolist())
+        self.dead_added.update(rows[~where].tolist())
+        self.n -= len(rows)
+
+    @staticmethod
+    def _arr(s):
+        return np.fromiter(s, dtype=np.int64, count=len(s))
+
+    def rows(self, gt):
+        """The live rows in (global_time, row) order."""
+        if self.dead_base:
+            keep = ~np.isin(self.base, self._arr(self.dead_base))
+            self.base, self.gbase = self.base[keep], self.gbase[keep]
+            self.dead_base = set()
+        if self.added:
+            new = np.concatenate(self.added)
+            if self.dead_added:
+                new = new[~np.isin(new, self._arr(self.dead_added))]
+                self.dead_added = set()
+            new = new[np.lexsort((new, gt[new]))]
+            base, g, gn = self.base, self.gbase, gt[new]
+            lo = np.searchsorted(g, gn, side="left")
+            at = np.searchsorted(g, gn, side="right")
+            # a row added among stored rows of its global time (a redone one) goes by row; an appended row's is larger
+            # than every stored row's, so `at` (after them) is its place
+            tie = np.flatnonzero(at > lo)  # (at > lo: base is not empty there)
+            for j in tie[new[tie] < base[at[tie] - 1]].tolist():
+                at[j] = lo[j] + int(np.searchsorted(base[lo[j]:at[j]], new[j]))
+            self.base = np.insert(base, at, new)
+            self.gbase = np.insert(g, at, gn)
+            self.added = []
+        return self.base
+
+    def count_upto(self, gt, max_gt):
+        """Live rows with global_time <= max_gt: O(log segment + tombstones + rows added since the last merge)."""
+        mg = np.uint64(max_gt)
+        k = int(np.searchsorted(self.gbase, mg, side="right"))
+        if self.dead_base:
+            k -= int((gt[self._arr(self.dead_base)] <= mg).sum())
+        for a in self.added:
+            k += int((gt[a] <= mg).sum())
+        if self.dead_added:
+            k -= int((gt[self._arr(self.dead_added)] <= mg).sum())
+        return k
+
+    def cut(self, gt, max_gt):
+        """Remove and return the live rows with global_time <= max_gt (a GlobalTimePruning DELETE): O(log segment +
+        rows cut + tombstones + rows added since the last merge)."""
+        mg = np.uint64(max_gt)
+        pos = int(np.searchsorted(self.gbase, mg, side="right"))
+        gone = self.base[:pos]
+        self.base, self.gbase = self.base[pos:], self.gbase[pos:]
+        if self.dead_base:
+            d = self._arr(self.dead_base)
+            d = d[gt[d] <= mg]
+            if len(d):
+                gone = gone[~np.isin(gone, d)]
+                self.dead_base.difference_update(d.tolist())
+        if self.added:
+            parts, keep = [gone], []
+            for a in self.added:
+                low = gt[a] <= mg
+                parts.append(a[low])
+                if not low.all():
+                    keep.append(a[~low])
+            self.added = keep
+            gone = np.concatenate(parts)
+            if self.dead_added:
+                d = self._arr(self.dead_added)
+                d = d[gt[d] <= mg]
+                if len(d):
+                    gone = gone[~np.isin(gone, d)]
+                    self.dead_added.difference_update(d.tolist())
+        self.n -= len(gone)
+        return gone
+
+
 class SyncStore(object):
     def __init__(self, blob, offsets, global_time, meta, undone=None, rowid=None, ctx=None, member=None,
                  communities=None, sequence=None):
@@ -92,16 +212,19 @@ class SyncStore(object):
         self._replaced = {}  # row -> packet after an UPDATE (dsy_store_replace); the packed blob keeps the original
         self._dup_indexed = False
         self._ops = []  # ("prune", meta, max_gt, n_at) / ("delete", rows, n_at): replayed on the device after a lazy upload
-        # live (undone == 0, not deleted) rows per meta, in (global_time, row) order, plus appended rows not merged yet
+        # live (undone == 0, not deleted) rows per meta (_LiveRows), and the undone rows per meta (a DELETE reaches
+        # them too; the index does not hold them)
+        self._live = {}
+        self._undone_rows = {}
         live = np.flatnonzero(self.undone == 0)
-        self._live, self._pending = {}, {}
-        self._nlive = {}
         if len(live):
             lm = self.meta[live]
             cuts = np.flatnonzero(lm[1:] != lm[:-1]) + 1
             for seg in np.split(live, cuts):
-                self._live[int(self.meta[seg[0]])] = seg
-                self._nlive[int(self.meta[seg[0]])] = len(seg)
+                self._live[int(self.meta[seg[0]])] = _LiveRows(seg, self.global_time[seg])
+        und = np.flatnonzero(self.undone != 0)
+        for r, m in zip(und.tolist(), self.meta[und].tolist()):
+            self._undone_rows.setdefault(int(m), set()).add(r)
         self._empty = np.zeros(0, dtype=np.int64)
         self._groups = None  # (meta, member) -> rows, built on first use (member_rows)
         self._keys = None    # (member, global_time) -> row, built on first use (rows_of_keys)
@@ -112,6 +235,8 @@ class SyncStore(object):
         # packets); _tail_at[i] = offsets[] of batch i's first byte, _tail_row[i] = its first row
         self._tail, self._tail_at, self._tail_row = [], [], []
         self._pair_groups = {}  # (meta, member1, member2) -> rows: the double_signed_sync table (set_pairs)
+        # whether the constructor's rows came with their double_signed_sync table (an empty store trivially did)
+        self._pairs_exported = n == 0
         self._owns_handle = True
 
     # ------------------------------------------------------------------------------------------ columns
@@ -130,8 +255,11 @@ class SyncStore(object):
 
     # ------------------------------------------------------------------------------------ constructors
     @classmethod
-    def from_rows(cls, rows, ctx=None, communities=None):
-        """rows: iterable of (rowid, global_time, meta_message, undone, packet[, member[, sequence]])."""
+    def from_rows(cls, rows, ctx=None, communities=None, pairs=None):
+        """rows: iterable of (rowid, global_time, meta_message, undone, packet[, member[, sequence]]).
+        pairs: the double_signed_sync table of these rows, (sync id, member1, member2) each (dispersy.py:1537-1541);
+        None: not exported (a double-member-signed meta with stored rows then cannot keep its history, see
+        pairs_exported)."""
         rows = sorted(rows, key=lambda r: (r[2], r[1], r[0]))
         n = len(rows)
         offsets = np.zeros(n + 1, dtype=np.uint64)
@@ -139,13 +267,17 @@ class SyncStore(object):
             np.cumsum([len(r[4]) for r in rows], out=offsets[1:])
         member = [r[5] for r in rows] if rows and len(rows[0]) > 5 else None
         sequence = [r[6] for r in rows] if rows and len(rows[0]) > 6 else None
-        return cls(b"".join(bytes(r[4]) for r in rows), offsets, [r[1] for r in rows], [r[2] for r in rows],
-                   [r[3] for r in rows], [r[0] for r in rows], ctx=ctx, member=member, communities=communities,
-                   sequence=sequence)
+        st = cls(b"".join(bytes(r[4]) for r in rows), offsets, [r[1] for r in rows], [r[2] for r in rows],
+                 [r[3] for r in rows], [r[0] for r in rows], ctx=ctx, member=member, communities=communities,
+                 sequence=sequence)
+        if pairs is not None:
+            st._load_pairs(pairs)
+        return st
 
     @classmethod
     def from_sqlite(cls, conn, community=None, ctx=None):
-        """Export a Dispersy database's `sync` table (optionally one community) in index order."""
+        """Export a Dispersy database's `sync` table (optionally one community) in index order, with its
+        double_signed_sync rows (the member pairs of double-member-signed messages) when the database has that table."""
         sql = "SELECT id, global_time, meta_message, undone, packet, member, community, sequence FROM sync"
         args = ()
         if community is not None:
@@ -153,23 +285,46 @@ class SyncStore(object):
             args = (community,)
         sql += " ORDER BY meta_message, global_time, id"
         rows = list(conn.execute(sql, args))
+        pairs = None
+        if conn.execute("SELECT name FROM sqlite_master WHERE type = 'table' AND name = 'double_signed_sync'").fetchone():
+            psql = "SELECT double_signed_sync.sync, member1, member2 FROM double_signed_sync"
+            if community is not None:
+                psql += " JOIN sync ON sync.id = double_signed_sync.sync WHERE sync.community = ?"
+            pairs = list(conn.execute(psql, args))
         return cls.from_rows([(i, g, m, u, bytes(p), mb, sq) for i, g, m, u, p, mb, _, sq in rows], ctx=ctx,
-                             communities={r[6] for r in rows} if rows else ({community} if community is not None else None))
+                             communities={r[6] for r in rows} if rows else ({community} if community is not None else None),
+                             pairs=pairs)
 
     @classmethod
-    def attach(cls, ctx, handle, global_time, meta, lengths, member=None, undone=None):
+    def attach(cls, ctx, handle, global_time, meta, lengths, member=None, undone=None, pairs=None, rowid=None):
         """A store exported straight into HBM (dsy_store_attach / dsy_store_upload made by the caller): the host keeps
         the small columns only (rows in index order), the packets of these rows stay on the device -- packet() serves
         only rows appended later.  `handle` is the dsy_store* (the caller keeps ownership); `undone` must be the
-        column the device index was built from (None: every row live), so host and device agree on the live rows."""
+        column the device index was built from (None: every row live), so host and device agree on the live rows.
+        pairs / rowid: as from_rows (the rows' sync ids default to 1..n)."""
         lengths = np.ascontiguousarray(lengths, dtype=np.uint64)
         offsets = np.zeros(len(lengths) + 1, dtype=np.uint64)
         np.cumsum(lengths, out=offsets[1:])
-        st = cls(bytearray(), offsets, global_time, meta, ctx=ctx, member=member, undone=undone)
+        st = cls(bytearray(), offsets, global_time, meta, ctx=ctx, member=member, undone=undone, rowid=rowid)
         st._blob_base = int(offsets[-1])
         st._handle = handle if isinstance(handle, ctypes.c_void_p) else ctypes.c_void_p(handle)
         st._owns_handle = False
+        if pairs is not None:
+            st._load_pairs(pairs)
         return st
+
+    def _load_pairs(self, pairs):
+        """The exported double_signed_sync rows (sync id, member1, member2) as the pair groups set_pairs keeps."""
+        rows, a, b = [], [], []
+        for sync_id, m1, m2 in pairs:
+            try:
+                rows.append(self.row_of_id(sync_id))
+            except KeyError:  # a pair row whose sync row is gone (or of another community): the JOIN drops it
+                continue
+            a.append(int(m1))
+            b.append(int(m2))
+        self.set_pairs(np.asarray(rows, dtype=np.int64), a, b)
+        self._pairs_exported = True
 
     # --------------------------------------------------------------------------------------- accessors
     def packet(self, i):
@@ -231,25 +386,24 @@ class SyncStore(object):
 
     def live_rows(self, meta_id):
         """Store rows of one meta with undone == 0 (not deleted), in (global_time, rowid) order."""
-        m = int(meta_id)
-        pend = self._pending.pop(m, None)
-        if pend:
-            new = np.concatenate(pend)
-            new = new[np.argsort(self.global_time[new], kind="stable")]  # ties: insertion (rowid) order
-            seg = self._live.get(m, self._empty)
-            # old rows first on equal global times (smaller rowid): insert after every old row with gt <= new gt
-            at = np.searchsorted(self.global_time[seg], self.global_time[new], side="right")
-            self._live[m] = np.insert(seg, at, new)
-        return self._live.get(m, self._empty)
+        lv = self._live.get(int(meta_id))
+        return self._empty if lv is None else lv.rows(self.global_time)
 
     def live_count(self, meta_id):
-        return self._nlive.get(int(meta_id), 0)
+        lv = self._live.get(int(meta_id))
+        return 0 if lv is None else lv.n
 
     def count_live(self, meta_ids):
         return int(sum(self.live_count(m) for m in set(int(x) for x in meta_ids)))
 
     def meta_ids(self):
-        return sorted(set(self._nlive) | set(self._live))
+        return sorted(m for m, lv in self._live.items() if lv.n or len(lv.base))
+
+    def _live_of(self, m):
+        lv = self._live.get(m)
+        if lv is None:
+            lv = self._live[m] = _LiveRows(self._empty, np.zeros(0, dtype=np.uint64))
+        return lv
 
     def member_rows(self, meta_id, member):
         """Rows of one (meta_message, member) -- undone ones included, deleted ones not -- in global_time order (unique
@@ -282,6 +436,17 @@ class SyncStore(object):
         for r, a, b in zip(np.asarray(rows).tolist(), np.asarray(member_a).tolist(), np.asarray(member_b).tolist()):
             pair = (a, b) if a < b else (b, a)
             self._pair_groups.setdefault((int(self.meta[r]),) + pair, []).append(r)
+
+    def pairs_exported(self, meta_id):
+        """Whether pair_rows can see every stored row of this meta: the store's initial rows came with their
+        double_signed_sync table, or none of them is of this meta (rows appended later record their pairs)."""
+        if self._pairs_exported:
+            return True
+        known = self.__dict__.setdefault("_pairless_metas", {})
+        m = int(meta_id)
+        if m not in known:
+            known[m] = not bool(np.any(self._buf["meta"][:self._n_sorted] == m))
+        return known[m]
 
     def pair_rows(self, meta_id, member1, member2):
         """Rows of one meta signed by the member pair (member1 < member2), deleted ones not, in the order of
@@ -374,13 +539,14 @@ class SyncStore(object):
             for r, m, b_ in zip(rows.tolist(), metas.tolist(), mem.tolist()):
                 self._gpending.setdefault((m, b_), []).append(np.asarray([r], dtype=np.int64))
         # per-meta live rows: merged lazily (live_rows)
-        order = np.argsort(metas, kind="stable")
-        sm = metas[order]
-        cuts = np.flatnonzero(sm[1:] != sm[:-1]) + 1
-        for part in np.split(order, cuts):
-            m = int(metas[part[0]])
-            self._pending.setdefault(m, []).append(rows[part])
-            self._nlive[m] = self._nlive.get(m, 0) + len(part)
+        if a and metas[0] == metas[-1] and (metas == metas[0]).all():  # one meta (the usual batch)
+            self._live_of(int(metas[0])).add(rows, self.global_time)
+        else:
+            order = np.argsort(metas, kind="stable")
+            sm = metas[order]
+            cuts = np.flatnonzero(sm[1:] != sm[:-1]) + 1
+            for part in np.split(order, cuts):
+                self._live_of(int(metas[part[0]])).add(rows[part], self.global_time)
         return rows
 
     def _top_rowid(self):
@@ -394,12 +560,14 @@ class SyncStore(object):
         the rows -- live and undone alike, as the SQL DELETE does -- leave the store: the live ones the index (host and
         device), all of them the duplicate table and row_of_id.  Returns the number of rows deleted."""
         m = int(meta_id)
-        seg = self.live_rows(m)
         if max_global_time < 0:
             return 0
-        k = int(np.searchsorted(self.global_time[seg], np.uint64(max_global_time), side="right")) if len(seg) else 0
-        gone = np.flatnonzero((self.meta == m) & (self.undone != 0) & ~self.deleted &
-                              (self.global_time <= np.uint64(max_global_time)))
+        lv = self._live.get(m)
+        gt = self.global_time
+        # the live rows the DELETE reaches: a prefix of the meta's index order (plus rows added since its last merge)
+        k = lv.count_upto(gt, max_global_time) if lv is not None else 0
+        und = self._undone_rows.get(m)
+        gone = np.asarray(sorted(r for r in und if gt[r] <= max_global_time), dtype=np.int64) if und else self._empty
         # the device first: a refused call (e.g. DSY_EINVAL while responder batches are in flight) leaves the host
         # bookkeeping untouched, so host and device never drift apart
         if k:
@@ -410,9 +578,9 @@ class SyncStore(object):
                 if out.value != k:
                     raise RuntimeError("device and host stores disagree: the device pruned %d rows, the host %d"
                                        % (out.value, k))
-            self._mark_deleted(seg[:k])
-            self._live[m] = seg[k:]
-            self._nlive[m] -= k
+            cut = lv.cut(gt, max_global_time)
+            assert len(cut) == k
+            self._mark_deleted(cut)
             self._ops.append(("prune", m, int(max_global_time), self.n))
         if len(gone):  # undone rows are outside the index: only their duplicate-table slots go
             if self._handle is not None:
@@ -420,6 +588,7 @@ class SyncStore(object):
                 rws = gone.astype(np.uint64)
                 _native.check(self.ctx.lib.dsy_store_delete(self.ctx.handle, self._handle, rws.ctypes.data, len(rws),
                                                             ctypes.byref(out)))
+            und.difference_update(gone.tolist())
             self._mark_deleted(gone)
             self._ops.append(("delete", gone, self.n))
         return k + len(gone)
@@ -445,11 +614,12 @@ class SyncStore(object):
             if out.value != len(live):
                 raise RuntimeError("device and host stores disagree: the device removed %d index entries, the host "
                                    "counts %d live rows" % (out.value, len(live)))
-        for m in np.unique(self.meta[live]).tolist():
-            seg = self.live_rows(m)
-            drop = live[self.meta[live] == m]
-            self._live[m] = seg[~np.isin(seg, drop, assume_unique=True)]
-            self._nlive[m] -= len(drop)
+        lm = self.meta[live]
+        for m in np.unique(lm).tolist():
+            self._live[m].remove(live[lm == m], self.global_time)
+        und = rows[self.undone[rows] != 0]
+        for r, m in zip(und.tolist(), self.meta[und].tolist()):
+            self._undone_rows[int(m)].discard(r)
         self._mark_deleted(rows)
         self._ops.append(("delete", rows, self.n))
         return len(rows)
@@ -479,15 +649,16 @@ class SyncStore(object):
         if self._handle is not None:  # the device first (see prune)
             self._set_undone_device(undo, redo)
         self._buf["undone"][rows] = vals
-        for m in np.unique(self.meta[undo]).tolist():
-            seg = self.live_rows(m)
-            drop = undo[self.meta[undo] == m]
-            self._live[m] = seg[~np.isin(seg, drop, assume_unique=True)]
-            self._nlive[m] -= len(drop)
-        for m in np.unique(self.meta[redo]).tolist():
-            seg = np.concatenate([self.live_rows(m), redo[self.meta[redo] == m]])
-            self._live[m] = seg[np.lexsort((seg, self.global_time[seg]))]
-            self._nlive[m] = self._nlive.get(m, 0) + int((self.meta[redo] == m).sum())
+        um = self.meta[undo]
+        for m in np.unique(um).tolist():
+            part = undo[um == m]
+            self._live[m].remove(part, self.global_time)
+            self._undone_rows.setdefault(m, set()).update(part.tolist())
+        rm = self.meta[redo]
+        for m in np.unique(rm).tolist():
+            part = redo[rm == m]
+            self._undone_rows[m].difference_update(part.tolist())
+            self._live_of(m).add(part, self.global_time)
         return len(undo) + len(redo)
 
     def _set_undone_device(self, undo, redo):

@@ -82,3 +82,25 @@ def test_respond_python_and_c_paths_build_the_same_call(monkeypatch):
     monkeypatch.setattr(community, "_dsyhost", reader)
     com.respond(list(itertools.islice(reqs, 10)))
     assert seen[0] == seen[1] and seen[2][1] == seen[0][1][:160]
+
+
+def test_claim_columns_getter_that_mutates_the_list():
+    """A `_refs` getter that pops and re-appends the caller's list (same length, possibly a reallocated item array)
+    while claim_columns reads it: the reader works from its own snapshot of the requests (dsy_host.c)."""
+    real = BloomFilter(1024, 0.01, b"\x01")
+    reqs = []
+
+    class Mutating:
+        @property
+        def _refs(self):
+            for _ in range(64):          # grow and shrink: a list reallocates its item array as it goes
+                reqs.extend([None] * 1000)
+                del reqs[-1000:]
+            reqs.append(reqs.pop(0))     # pop-then-append keeps the length
+            return real._refs
+
+    reqs[:] = [ClaimRequest(i + 1, i + 10, 1, 0, Mutating()) for i in range(50)]
+    want = [[i + 1, i + 10, 1, 0] for i in range(50)]
+    ranges, words = c_columns(reqs)
+    assert [ranges[4 * i:4 * i + 4] for i in range(50)] == want
+    assert words == real._refs * 50

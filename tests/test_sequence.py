@@ -107,9 +107,9 @@ class _Msg(object):
         self.packet, self.index, self.candidate = packet, index, "c%d" % index
 
 
-def store_of(table):
+def store_of(table, pairs=None):
     return SyncStore.from_rows([(i, gt, meta, und, bytes.fromhex(p), mem, sq or 0)
-                                for i, mem, gt, meta, und, p, sq in table])
+                                for i, mem, gt, meta, und, p, sq in table], pairs=pairs)
 
 
 def alive(store):
@@ -240,14 +240,46 @@ def _double_replay(store, com, meta):
         assert sorted([k] + v for k, v in pairs.items()) == step["double"]
 
 
-def _double_store():
-    store = store_of(DOUBLE["initial_table"])
-    rid = {int(store.rowid[r]): r for r in range(store.n)}
-    d = DOUBLE["initial_double"]
-    store.set_pairs([rid[s] for s, _, _ in d], [a for _, a, _ in d], [b for _, _, b in d])
-    meta = MetaMessage("double", DOUBLE["meta"], LastSyncDistribution("ASC", 128, DOUBLE["history_size"]),
+def _double_meta():
+    return MetaMessage("double", DOUBLE["meta"], LastSyncDistribution("ASC", 128, DOUBLE["history_size"]),
                        double_signed=True)
-    return store, meta
+
+
+def _double_store():
+    return store_of(DOUBLE["initial_table"], pairs=[tuple(r) for r in DOUBLE["initial_double"]]), _double_meta()
+
+
+def test_double_signed_history_from_a_sqlite_export():
+    """A store exported from a Dispersy database (SyncStore.from_sqlite) brings its double_signed_sync rows along, so
+    the per-pair LastSync history sees the pairs' older rows (before, the export dropped the table and the
+    store silently kept more than history_size rows per pair).  CPU: the host copy."""
+    conn = sqlite_of(DOUBLE["initial_table"])
+    conn.executemany("INSERT INTO double_signed_sync (sync, member1, member2) VALUES (?, ?, ?)",
+                     [tuple(r) for r in DOUBLE["initial_double"]])
+    store = SyncStore.from_sqlite(conn)
+    store._ctx = object()  # never uploaded
+    meta = _double_meta()
+    _double_replay(store, SyncCommunity(store, [meta], global_time=1), meta)
+
+
+def test_double_signed_history_needs_the_pairs_of_stored_rows():
+    """A store whose rows of a double-member-signed meta came without their double_signed_sync table cannot apply the
+    per-pair history (pair_rows would miss the older rows): store_messages refuses the batch before storing any of
+    it.  Rows of other metas do not matter, and an empty store records every pair itself."""
+    meta = _double_meta()
+    bare = store_of(DOUBLE["initial_table"])
+    bare._ctx = object()
+    step = DOUBLE["steps"][0]
+    msgs = [_DoubleMsg(meta, m["members"][0], m["members"][1], m["gt"], bytes.fromhex(m["packet"]), m["index"])
+            for m in step["messages"]]
+    n0 = bare.n
+    with pytest.raises(ValueError):
+        SyncCommunity(bare, [meta], global_time=1).store_messages(msgs)
+    assert bare.n == n0
+    other = store_of([r[:3] + [r[3] + 1] + r[4:] for r in DOUBLE["initial_table"]])  # the rows under another meta
+    other._ctx = object()
+    assert other.pairs_exported(DOUBLE["meta"])
+    SyncCommunity(other, [meta], global_time=1).store_messages(msgs)
 
 
 def test_double_signed_history_matches_reference_host():

@@ -1,0 +1,83 @@
+"""SyncStore's host mirror of the live index (store.py _LiveRows): appends, DELETEs, undo / redo and GlobalTimePruning
+cuts kept O(their rows) -- tombstones and pending rows merged on read -- checked against a brute-force recomputation
+from the columns after every operation (the reference's SQL over the sync table: `WHERE meta_message = ? AND undone
+= 0 ORDER BY global_time` with rowid ties, dispersydatabase.py:63; DELETE community.py:1094-1096; UPDATE undone
+community.py:3479-3480).  CPU only: the store never goes to the device (its ctx is a placeholder)."""
+import time
+
+import numpy as np
+import pytest
+
+from dispersy_amd.store import SyncStore
+
+
+def brute_live(st, m):
+    r = np.flatnonzero((st.meta == m) & (st.undone == 0) & ~st.deleted)
+    return r[np.lexsort((r, st.global_time[r]))]
+
+
+def brute_prune_count(st, m, max_gt):
+    return int(((st.meta == m) & ~st.deleted & (st.global_time <= np.uint64(max_gt))).sum())
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4])
+def test_host_live_index_against_brute_force(seed):
+    rng = np.random.default_rng(seed)
+    n0 = 3000
+    meta = np.sort(rng.integers(1, 4, n0)).astype(np.uint32)
+    gt = np.concatenate([np.sort(rng.integers(1, 400, (meta == m).sum())) for m in (1, 2, 3)]).astype(np.uint64)
+    undone = np.where(rng.random(n0) < 0.05, 7, 0)
+    st = SyncStore(b"\x00" * n0, np.arange(n0 + 1, dtype=np.uint64), gt, meta, undone=undone, ctx=object(),
+                   member=rng.integers(1, 50, n0).astype(np.uint64))
+    for step in range(300):
+        op = rng.integers(0, 6)
+        if op == 0:  # append a batch (one or several metas, global times anywhere in the history or above)
+            a = int(rng.integers(1, 60))
+            ms = np.full(a, rng.integers(1, 5)) if rng.random() < 0.5 else rng.integers(1, 5, a)
+            g = rng.integers(1, 600, a).astype(np.uint64)
+            st.append([b"p"] * a, g, ms, member=rng.integers(1, 50, a).astype(np.uint64))
+        elif op == 1:  # DELETE of arbitrary rows (live, undone, already deleted, appended)
+            st.delete_rows(rng.integers(0, st.n, int(rng.integers(1, 40))))
+        elif op == 2:  # undo
+            st.set_undone(rng.integers(0, st.n, int(rng.integers(1, 30))), 1)
+        elif op == 3:  # redo
+            st.set_undone(rng.integers(0, st.n, int(rng.integers(1, 30))), 0)
+        elif op == 4:  # GlobalTimePruning
+            m = int(rng.integers(1, 5))
+            cut = int(rng.integers(0, 120)) + step // 3
+            want = brute_prune_count(st, m, cut)
+            assert st.prune(m, cut) == want
+        else:  # a host-side reader materialises the order
+            m = int(rng.integers(1, 5))
+            assert st.live_rows(m).tolist() == brute_live(st, m).tolist()
+        for m in (1, 2, 3, 4):
+            assert st.live_count(m) == len(brute_live(st, m))
+    for m in (1, 2, 3, 4):
+        assert st.live_rows(m).tolist() == brute_live(st, m).tolist()
+
+
+def test_host_deletes_at_10m_rows_are_o_batch():
+    """Round-4 verdict: prune + delete_rows of 100 rows on a 10 M-row store in <= 2 ms (they used to build N-length
+    masks and np.isin / np.insert over the whole segment: tens of ms)."""
+    n = 10_000_000
+    gt = np.arange(1, n + 1, dtype=np.uint64)
+    meta = np.ones(n, dtype=np.uint32)
+    undone = np.zeros(n, dtype=np.int64)
+    undone[::100_000] = 5  # some undone rows (the prune's second DELETE target)
+    st = SyncStore(b"", np.zeros(n + 1, dtype=np.uint64), gt, meta, undone=undone, ctx=object())
+    rng = np.random.default_rng(9)
+    st.append([b""] * 1000, rng.integers(n // 2, n, 1000).astype(np.uint64), np.ones(1000, dtype=np.uint32))
+    times, cut = [], 0
+    for _ in range(7):
+        rows = rng.integers(n // 4, n, 100)
+        t0 = time.perf_counter()
+        cut += 100
+        pruned = st.prune(1, cut)
+        deleted = st.delete_rows(rows)
+        st.set_undone(rows[:10], 1)
+        times.append(time.perf_counter() - t0)
+        assert pruned >= 99 and deleted > 0
+    med = sorted(times)[len(times) // 2]
+    print("prune(100) + delete_rows(100) + set_undone(10) at 10 M rows: median %.3f ms" % (med * 1e3))
+    assert med <= 2e-3
+    assert st.live_count(1) == n + 1000 - int(st.deleted.sum()) - int(((st.undone != 0) & ~st.deleted).sum())
