@@ -104,6 +104,12 @@ def _pool_task(payload):
     return r if isinstance(r, tuple) else (r, time.perf_counter() - t0)
 
 
+def _pool_call(payload):
+    import cloudpickle
+    fn, item = cloudpickle.loads(payload)
+    return fn(item)
+
+
 class CpuPool(object):
     """The N-core CPU legs' workers.  They are forked at start-up, before torch is imported or HIP is touched, so
     no worker inherits device files or GPU runtime state; tasks reach them as cloudpickle payloads (large arrays as
@@ -122,6 +128,11 @@ class CpuPool(object):
             raise ValueError("%d shards for %d workers" % (len(shards), self.n))
         res = self.pool.map(_pool_task, [cloudpickle.dumps((fn, s)) for s in shards], chunksize=1)
         return sum(u for u, _ in res), max(t for _, t in res)
+
+    def map(self, fn, items):
+        """[fn(item) for item in items] on the workers (the heaviest items first is the caller's choice)."""
+        import cloudpickle
+        return self.pool.map(_pool_call, [cloudpickle.dumps((fn, it)) for it in items], chunksize=1)
 
     def close(self):
         self.pool.close()
@@ -1546,7 +1557,7 @@ def heavy_tail(args, ctx, lib, dev, rank, world, dist):
     cpu = None
     if rank == 0 and world == 1 and args.cpu_claims > 0:
         cpu = responder_cpu(args, ctx, lib, store, reqs, claims, fblob, blob, offsets, h_gt.astype(np.uint64), G_MAX,
-                            dev, "cfg5 heavy tail")
+                            dev, "cfg5 heavy tail", check=[i for i in range(R) if i % 16 in (0, 1)])
     lib.dsy_store_free(store)
     secs = kt["ms"] / 1e3
     out = {"metric": "packets hashed+tested/sec", "value": round(useful / dt, 1), "unit": "packets/s", "n_gpus": world,
@@ -1574,7 +1585,7 @@ def heavy_tail(args, ctx, lib, dev, rank, world, dist):
 
 
 def responder_cpu(args, ctx, lib, store, reqs, claims, fblob, blob, offsets, h_gts, g_time, dev, label,
-                  max_claims=1024):
+                  max_claims=1024, check=None):
     """The responder's CPU baseline (configs 2 and 5, the SHA-1 leg): oracle/sync_ref.respond_arrays -- numpy for
     the range / modulo predicate (faster than the reference's sqlite scan, so generous to the CPU), hashlib + Python
     for the lazy not_filter / byte-limit loop exactly as the reference (community.py:2555-2567) -- over the first
@@ -1597,8 +1608,7 @@ def responder_cpu(args, ctx, lib, store, reqs, claims, fblob, blob, offsets, h_g
                                        99, out.ctypes.data, len(out), out_off.ctypes.data))
     gpu = [out[int(out_off[j]):int(out_off[j + 1])].tolist() for j in range(n_try)]
     h_off = offsets.cpu().numpy()
-    touched, sample, pairs = [], [], 0
-    for i in range(n_try):  # the rows the reference's lazy loop hashes for claim i (ASC meta, gt sorted by row)
+    def walked(i):  # the rows the reference's lazy loop hashes for claim i (ASC meta, gt sorted by row)
         lo, hi, offset, modulo = claims[i][:4]
         a = int(np.searchsorted(h_gts, lo, side="left"))
         b = int(np.searchsorted(h_gts, hi, side="right"))
@@ -1608,11 +1618,24 @@ def responder_cpu(args, ctx, lib, store, reqs, claims, fblob, blob, offsets, h_g
         sent = gpu[i]
         if sent and int((h_off[np.asarray(sent) + 1] - h_off[np.asarray(sent)]).sum()) >= args.byte_limit:
             sel = sel[:int(np.searchsorted(sel, sent[-1])) + 1]
+        return sel
+
+    touched, sample, pairs = [], [], 0
+    for i in range(n_try):
+        sel = walked(i)
         touched.append(sel)
         sample.append(i)
         pairs += len(sel)
         if pairs >= args.cpu_pairs:
             break
+    work = {}
+    if check:  # the claims the pool checks against the oracle as well (not timed)
+        check = [i for i in check if i < n_try]
+        for i in check:
+            sel = walked(i)
+            work[i] = len(sel)
+            if i not in sample:
+                touched.append(sel)
     rows = np.unique(np.concatenate(touched)) if touched else np.zeros(0, np.int64)
     d_rows = torch.from_numpy(rows).to(dev)
     st = offsets[d_rows]
@@ -1657,7 +1680,30 @@ def responder_cpu(args, ctx, lib, store, reqs, claims, fblob, blob, offsets, h_g
     ncore = n_core_leg(shard, list(range(cores)), "packets/s",
                        "the same %d claims in every process (rotated), one process per core, same port"
                        % len(sample)) if match else None
+    oracle_check = None
+    if check and POOL is not None:
+        # every checked claim through the oracle, one claim per worker task (heaviest first), against the GPU's answer
+        def one(i):
+            cb, co_, rw, gts = s_blob.a, s_off.a, s_rows.a, s_gts.a
+            mv = memoryview(cb)
+
+            def p_of(r):  # (the rows are sorted: a binary search, no per-task dict over millions of rows)
+                j = int(np.searchsorted(rw, r))
+                return mv[int(co_[j]):int(co_[j + 1])]
+
+            class Rows(object):  # the store's rows are its index order
+                def __getitem__(self, k):
+                    return k
+            cnt = [0]
+            return i, run([i], p_of, {1: (Rows(), gts)}, cnt)[0], cnt[0]
+        t1 = time.perf_counter()
+        res = POOL.map(one, sorted(check, key=lambda i: -work[i]))
+        oracle_check = {"claims": len(res), "pairs_hashed": int(sum(c for _, _, c in res)),
+                        "gpu_matches_oracle": all(ans == gpu[i] for i, ans, _ in res),
+                        "seconds": round(time.perf_counter() - t1, 2),
+                        "how": "oracle/sync_ref.respond_arrays (hashlib) on the CpuPool workers, one claim per task"}
     return {"value": round(counter[0] / dt, 1), "unit": "packets/s", "cores": 1, "kind": "port", "cpu_model": model,
+            "oracle_check": oracle_check,
             "sample": "%s: the first %d of the step's claims, %d (claim, packet) pairs hashed lazily as the reference "
                       "does (it stops at the packet that spends the %d B budget), through oracle/sync_ref.respond_arrays "
                       "+ oracle/bloom_ref (hashlib), %.1f s" % (label, len(sample), counter[0], byte_limit, dt),

@@ -147,7 +147,6 @@ struct dsy_ctx {
     int pool_queue = 0;
     int pool_deal = 0;   // DSY_POOL_DEAL: the pooled hashing's resident-grid deal (k_pair_test<POOL>)
     int pair_prio = 1;   // DSY_PAIR_PRIO: k_pair_test raises the wave priority of long wave-tasks (0 off)
-    int pair_pipe = 1;   // DSY_PAIR_PIPE=0: the responder's line-staged hashing walks task after task (k_pair_test)
     int bulk_zero = 1;   // DSY_BULK_ZERO=0: the calls do not zero their split-window sort state (diagnostic)
     uint32_t direct_kinds = 0;  // DSY_PAIR_DIRECT: bit k = hash kind k's responder hashing uses direct loads
     uint32_t timing = 0;  // bit i: bracket class i with events
@@ -537,7 +536,6 @@ int dsy_ctx_create(int device, dsy_ctx** out) {
     if (const char* v = getenv("DSY_POOL_QUEUE")) c->pool_queue = atoi(v);
     if (const char* v = getenv("DSY_POOL_DEAL")) c->pool_deal = atoi(v);
     if (const char* v = getenv("DSY_PAIR_PRIO")) c->pair_prio = atoi(v);
-    if (const char* v = getenv("DSY_PAIR_PIPE")) c->pair_pipe = atoi(v);
     if (const char* v = getenv("DSY_BULK_ZERO")) c->bulk_zero = atoi(v);
     if (const char* v = getenv("DSY_PAIR_DIRECT")) c->direct_kinds = (uint32_t)strtoul(v, nullptr, 0);
     c->pool_kinds &= (1u << DSY_MD5) | (1u << DSY_SHA1) | (1u << DSY_SHA256);
@@ -2354,7 +2352,6 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const Clai
     L.pool_queue = c->pool_queue;
     L.pool_deal = c->pool_deal;
     L.pair_prio = c->pair_prio;
-    L.pair_pipe = c->pair_pipe;
     L.bulk_zero = c->bulk_zero;
     L.pool_counts = (PoolCounts*)d_pool_counts;
     if ((rc = job_pair_buffers(sl, pool))) return rc;

@@ -148,6 +148,11 @@ enum { kGuardSortPos = 0, kGuardTask = 1, kGuardPack = 2, kGuardWindow = 3 };
 __device__ __forceinline__ void guard_trip(uint64_t* h_status, int which) {
     ((volatile uint8_t*)&h_status[kStatusGuard])[which] = 1;
 }
+// a task record's packet lies inside the line copy with its guard bytes on both sides; overflow-safe, so a record
+// the fill did not write this window (say 0xFF.. in recycled memory) cannot wrap around the check
+__device__ __forceinline__ bool packet_in_lines(uint64_t off, uint64_t len, uint64_t lines_bytes) {
+    return off >= DSY_BLOB_GUARD && len + 2 * DSY_BLOB_GUARD <= lines_bytes && off <= lines_bytes - DSY_BLOB_GUARD - len;
+}
 static constexpr uint32_t kCntSpread = 64;
 __device__ __forceinline__ unsigned long long* counter(uint64_t* counters, uint32_t which) {
     return (unsigned long long*)&counters[(blockIdx.x % kCntSpread) * kCntN + which];
@@ -243,7 +248,6 @@ struct RespondLaunch {
     int pool_queue;           // k_pair_test<POOL>: waves take wave-tasks from a queue instead of a grid stride
     int pool_deal;            // k_pair_test<POOL>: resident grid, wave-tasks dealt so each SIMD's waves sum to the mean
     int pair_prio;            // k_pair_test: wave priority by the wave-task's length (s_setprio)
-    int pair_pipe;            // line-staged MD5 / SHA-1 hashing by k_pair_pipe (software-pipelined walk), not k_pair_test
     int bulk_zero;            // k_setup / k_fill_first zero the call's bulk_hist / bulk_cur rows (DSY_BULK_ZERO=0: not,
                               // a diagnostic of the state k_compact leaves between calls)
     PoolCounts* pool_counts;  // device, zero outside a window (k_pair_test<POOL> clears its family's)
@@ -274,10 +278,6 @@ hipError_t launch_pair_test_list(const RespondLaunch& L, int kind, uint32_t chun
 // (k_pool_scatter), then one hashing launch over the pool (k_pair_test<POOL>)
 hipError_t launch_pair_test_pooled(const RespondLaunch& L, int kind, uint32_t chunk, bool long_prefix, uint32_t fam,
                                    const uint32_t* d_list, uint32_t n);
-// the line-staged MD5 / SHA-1 (2- or 4-byte chunks, prefixes of 1..4 bytes) hashing of the listed window slots as one
-// software pipeline per wave (dsy_pipe_kernels.hip); blocks workgroups of 256, lds bytes of dynamic LDS
-hipError_t launch_pair_pipe(const RespondLaunch& L, int kind, uint32_t chunk, const uint32_t* list, uint32_t n_list,
-                            uint32_t blocks, size_t lds);
 hipError_t launch_compact(const RespondLaunch& L);
 // done (optional): an event the last pack kernel's dispatch records when it completes
 hipError_t launch_pack(const RespondLaunch& L, uint64_t* packed, uint64_t* packed_offsets, uint64_t* d_scan_tmp,

@@ -1208,7 +1208,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
             r = L.act[a_slot];
             if (active) {
                 const uint64_t off = ((uint64_t)pt.line << 7) + kLineBias;
-                if (off < DSY_BLOB_GUARD || off + pt.len + DSY_BLOB_GUARD > L.st.lines_bytes || pt.slot >= W) {
+                if (!packet_in_lines(off, pt.len, L.st.lines_bytes) || pt.slot >= W) {
                     guard_trip(L.h_status, kGuardTask);
                     active = false;
                 } else {
@@ -1235,7 +1235,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
                 const PairTask tk = L.task[(uint64_t)a_slot * W + i];
                 // bounds check of the packet the record names (a record the fill did not write this window would
                 // address another store's line copy): skipped and reported, never dereferenced
-                if (tk.off < DSY_BLOB_GUARD || tk.off + tk.len + DSY_BLOB_GUARD > L.st.lines_bytes ||
+                if (!packet_in_lines(tk.off, tk.len, L.st.lines_bytes) ||
                     tk.slot >= n) {
                     guard_trip(L.h_status, kGuardTask);
                     active = false;
@@ -1354,11 +1354,6 @@ static hipError_t pair_test_family(const RespondLaunch& L, bool long_prefix, con
     if constexpr (dma) {
         if (!long_prefix && !((L.direct_kinds >> H::kind) & 1u)) {
             const size_t lds = 4 * DmaGeometry<2, 1>::kWaveBytes;
-            if (CHUNK <= 4 && L.pair_pipe && !pooled && (uint64_t)n_list * (L.window / 64) < (1ull << 32) &&
-                L.st.lines_bytes < (1ull << 36)) {
-                launch_pair_pipe(L, H::kind, CHUNK, list, n_list, (uint32_t)blocks, lds);
-                return hipGetLastError();
-            }
             auto kern = pooled ? k_pair_test<H, CHUNK, true, 0, true> : k_pair_test<H, CHUNK, true>;
             if constexpr (CHUNK == 2) {  // (respond_core pools no family while a diagnostic build is asked for)
                 if (L.diag == 1) kern = k_pair_test<H, CHUNK, true, 1>;

@@ -1,15 +1,13 @@
 """BASELINE configs[1] at its full size: one responder with 10 M stored packets (100-1500 B, global_time 1..N) answers
 1024 claims (half largest-style, half modulo-style, as bench.py's headline) through dsy_sync_respond, and EVERY
-claim's answer is checked.
+claim's answer is checked against the CPU oracle.
 
-The reference's answer (community.py:2746-2811 + the byte-limited loop :2555-2567) is recomputed per claim from
-scratch: the claim's candidates in send order (rows with time_low <= global_time <= time_high and
-(global_time + offset) % modulo == 0, ascending), each candidate's membership in the claim's filter, and the budget
-walk -- send the missing packets until the one whose length makes the running total reach the byte limit.  The
-membership of all 1.08 M candidates comes from the single-filter kernel (dsy_bloom_test_dev, k_bloom: a different
-kernel from the responder's k_pair_test, pinned to the reference's bloomfilter.py by the golden vectors), and for a
-sample of claims from hashlib (oracle/bloom_ref.py) as well.  MD5 MTU filters (m = 10160, f = 0.01) and the SHA-1
-test-harness filters of node.py:617 (m = 4096, f = 0.001)."""
+The oracle is oracle/sync_ref.respond_arrays -- the reference's responder (community.py:2746-2811 + the byte-limited
+loop :2555-2567) over in-memory columns: the claim's candidates in send order, each hashed with hashlib through
+oracle/bloom_ref's lazy not_filter (bloomfilter.py:214-237), the walk stopping at the packet that spends the budget.
+It runs for every claim, fanned out over 16 spawned worker processes (tests/oracle_pool.py), on the packets of the
+claims' candidate rows gathered from HBM.  MD5 MTU filters (m = 10160, f = 0.01) and the SHA-1 test-harness filters of
+node.py:617 (m = 4096, f = 0.001); config 5 (heavy tail) checks 256 of its 1024 claims the same way."""
 import ctypes
 import math
 
@@ -18,7 +16,7 @@ import pytest
 
 from dispersy_amd import _native
 from dispersy_amd.bloomfilter import BloomFilter
-from oracle.bloom_ref import OracleBloom
+from oracle_pool import check_claims
 
 pytestmark = pytest.mark.gpu
 
@@ -89,24 +87,12 @@ def claims_of(ctx, store, rng, bits, f):
     return reqs, out, b"".join(raws)
 
 
-def expected(rows, present, lens):
-    """The reference's walk over candidates `rows` (send order) with their membership and lengths."""
-    miss = ~present
-    mrows, mlens = rows[miss], lens[rows[miss]]
-    if not len(mrows):
-        return mrows
-    spent = np.cumsum(mlens)
-    stop = np.flatnonzero(spent >= LIMIT)
-    return mrows if not len(stop) else mrows[:stop[0] + 1]
-
-
 @pytest.mark.parametrize("bits,f", [(10160, 0.01), (4096, 0.001)])
 def test_full_size_every_claim(world, bits, f):
     torch, ctx, dev, store, blob, offsets, lens = world
     lib = ctx.lib
     rng = np.random.Generator(np.random.PCG64(7 if bits == 10160 else 8))
     reqs, claims, fblob = claims_of(ctx, store, rng, bits, f)
-    d_filters = torch.frombuffer(bytearray(fblob + bytes(64)), dtype=torch.uint8).to(dev)
     metas = (_native.Meta * 1)()
     metas[0].meta_id, metas[0].direction = 1, _native.DSY_ASC
     h_off = np.zeros(R + 1, dtype=np.uint64)
@@ -115,45 +101,44 @@ def test_full_size_every_claim(world, bits, f):
     # the host-buffer entry point: the filters go up the bus, the answers come back
     _native.check(lib.dsy_sync_respond(ctx.handle, store, reqs, R, fblob, len(fblob), metas, 1, N, 0, LIMIT, 99,
                                        h_idx.ctypes.data, len(h_idx), h_off.ctypes.data))
-    # membership of every candidate of every claim through k_bloom: the candidates' packets gathered into one
-    # contiguous device blob (largest-style claims' candidates are consecutive rows already)
-    all_rows = np.concatenate([c[0] for c in claims])
-    starts = np.concatenate([[0], np.cumsum([len(c[0]) for c in claims])])
-    d_rows = torch.from_numpy(all_rows).to(dev)
-    G = _native.BLOB_GUARD
-    beg, ln = offsets[d_rows], offsets[d_rows + 1] - offsets[d_rows]
-    koff = torch.zeros(len(all_rows) + 1, device=dev, dtype=torch.int64)
-    torch.cumsum(ln, 0, out=koff[1:])
-    nbytes = int(koff[-1].item())
-    pos = torch.arange(nbytes, device=dev, dtype=torch.int64)
-    seg = torch.repeat_interleave(torch.arange(len(all_rows), device=dev), ln)
-    gathered = torch.zeros(nbytes + 2 * G, device=dev, dtype=torch.uint8)
-    gathered[G:G + nbytes] = blob[beg[seg] + (pos - koff[seg])]
-    present = torch.zeros(len(all_rows), device=dev, dtype=torch.uint8)
-    torch.cuda.synchronize()
-    for i, (rows, bf, pre, raw, foff) in enumerate(claims):
-        a, b = int(starts[i]), int(starts[i + 1])
-        _native.check(lib.dsy_bloom_test_dev(ctx.handle, ctypes.byref(bf.params), gathered.data_ptr() + G,
-                                             koff.data_ptr() + 8 * a, b - a, d_filters.data_ptr() + foff,
-                                             present.data_ptr() + a))
-    ctx.synchronize()
-    h_present = present.cpu().numpy().astype(bool)
-    checked_hashlib = 0
-    for i, (rows, bf, pre, raw, foff) in enumerate(claims):
-        a, b = int(starts[i]), int(starts[i + 1])
-        got = h_idx[h_off[i]:h_off[i + 1]].astype(np.int64)
-        want = expected(rows, h_present[a:b], lens)
-        assert np.array_equal(got, want), (i, len(got), len(want))
-        if i % 32 in (0, 1):  # hashlib on a sample: k_bloom's membership == bloomfilter.py's at full size
-            ob = OracleBloom.from_bytes(raw, bf.functions, pre)
-            kb = gathered[G + int(koff[a].item()):G + int(koff[b].item())].cpu().numpy().tobytes()
-            ko = koff[a:b + 1].cpu().numpy() - int(koff[a].item())
-            ref = np.array([kb[ko[j]:ko[j + 1]] in ob for j in range(b - a)])
-            assert np.array_equal(ref, h_present[a:b]), i
-            checked_hashlib += 1
-    assert checked_hashlib == 64
-    assert int(h_off[-1]) > R  # most claims send several packets
+    # the oracle over every claim: the packets of all candidate rows, gathered from HBM, in worker processes
+    rows = np.unique(np.concatenate([c[0] for c in claims]))
+    packets, poff = gather_rows(torch, dev, blob, offsets, rows)
+    want = check_claims([oracle_claim(reqs[i], c) for i, c in enumerate(claims)], packets, poff, rows,
+                        np.arange(1, N + 1, dtype=np.uint64), N, LIMIT, work=[len(c[0]) for c in claims])
+    sent = 0
+    for i in range(R):
+        got = h_idx[h_off[i]:h_off[i + 1]].astype(np.int64).tolist()
+        assert got == want[i], (i, len(got), len(want[i]))
+        sent += len(got)
+    assert sent > R  # most claims send several packets
 
+
+def gather_rows(torch, dev, blob, offsets, rows, chunk=1 << 18):
+    """The packets of store rows `rows` (sorted), back to back, copied from the device blob in chunks: (bytes as
+    a uint8 array, offsets)."""
+    d_off = offsets
+    lens = (d_off[torch.from_numpy(rows + 1).to(dev)] - d_off[torch.from_numpy(rows).to(dev)]).cpu().numpy()
+    poff = np.zeros(len(rows) + 1, dtype=np.int64)
+    np.cumsum(lens, out=poff[1:])
+    out = np.empty(int(poff[-1]), dtype=np.uint8)
+    for a in range(0, len(rows), chunk):
+        b = min(len(rows), a + chunk)
+        d_rows = torch.from_numpy(rows[a:b]).to(dev)
+        beg, ln = d_off[d_rows], d_off[d_rows + 1] - d_off[d_rows]
+        koff = torch.zeros(b - a + 1, device=dev, dtype=torch.int64)
+        torch.cumsum(ln, 0, out=koff[1:])
+        n = int(koff[-1].item())
+        seg = torch.repeat_interleave(torch.arange(b - a, device=dev), ln)
+        pos = torch.arange(n, device=dev, dtype=torch.int64)
+        out[int(poff[a]):int(poff[b])] = blob[beg[seg] + (pos - koff[seg])].cpu().numpy()
+        del d_rows, beg, ln, koff, seg, pos
+    return out, poff
+
+
+def oracle_claim(q, c):
+    """(time_low, time_high, offset, modulo, filter bytes, k, prefix) of claim q (its claims_of tuple c)."""
+    return (int(q.time_low), int(q.time_high), int(q.offset), int(q.modulo), c[3], c[1].functions, c[2])
 
 
 def heavy_tail_world(torch, ctx, dev):
@@ -184,8 +169,7 @@ def heavy_tail_world(torch, ctx, dev):
 
 def test_heavy_tail_full_size_sample(world):
     """Config 5 at its full size: the 1024 claims of bench.py's heavy_tail leg in one call (claims whose filters
-    saturate walk 10^5-10^6 rows over many windows), every 16th claim checked completely -- its candidates in send
-    order through k_bloom's membership and the budget walk, as above."""
+    saturate walk 10^5-10^6 rows over many windows), 256 of them checked completely against the oracle, as above."""
     torch, ctx, dev = world[0], world[1], world[2]
     lib = ctx.lib
     store, blob_full, offsets, lens, h_gt = heavy_tail_world(torch, ctx, dev)
@@ -223,7 +207,7 @@ def test_heavy_tail_full_size_sample(world):
             q.hash_kind, q.chunk_bytes = _native.HASH_KINDS[bf.hash_name], bf.chunk_bytes
             q.prefix_len = 1
             q.prefix[0] = pre[0]
-            claims.append((rows, bf, off))
+            claims.append((rows, bf, off, buf.raw, pre))
             raws.append(raw)
             off += len(raw)
         fblob = b"".join(raws)
@@ -233,36 +217,21 @@ def test_heavy_tail_full_size_sample(world):
         h_idx = np.zeros(1 << 24, dtype=np.uint64)
         _native.check(lib.dsy_sync_respond(ctx.handle, store, reqs, R, fblob, len(fblob), metas, 1, 1_000_000, 0,
                                            LIMIT, 99, h_idx.ctypes.data, len(h_idx), h_off.ctypes.data))
-        d_filters = torch.frombuffer(bytearray(fblob + bytes(64)), dtype=torch.uint8).to(dev)
-        d_off64 = offsets
+        # the oracle over 256 of the claims (both styles: i % 8 in {0, 1}); the saturated largest-style ones walk
+        # 10^5-10^6 rows with hashlib
+        pick = [i for i in range(R) if i % 8 in (0, 1)]
+        rows = np.unique(np.concatenate([claims[i][0] for i in pick]))
+        packets, poff = gather_rows(torch, dev, blob_full[G:], offsets, rows)
+        want = check_claims([(int(reqs[i].time_low), int(reqs[i].time_high), int(reqs[i].offset), int(reqs[i].modulo),
+                              claims[i][3], claims[i][1].functions, claims[i][4]) for i in pick], packets, poff, rows,
+                            h_gt.astype(np.uint64), 1_000_000, LIMIT, work=[len(claims[i][0]) for i in pick])
+        del packets
         sent = 0
-        for i in range(0, R, 16):
-            rows, bf, foff = claims[i]
-            got = h_idx[h_off[i]:h_off[i + 1]].astype(np.int64)
-            if len(rows):
-                d_rows = torch.from_numpy(rows).to(dev)
-                beg, ln = d_off64[d_rows], d_off64[d_rows + 1] - d_off64[d_rows]
-                koff = torch.zeros(len(rows) + 1, device=dev, dtype=torch.int64)
-                torch.cumsum(ln, 0, out=koff[1:])
-                nbytes = int(koff[-1].item())
-                seg = torch.repeat_interleave(torch.arange(len(rows), device=dev), ln)
-                pos = torch.arange(nbytes, device=dev, dtype=torch.int64)
-                gathered = torch.zeros(nbytes + 2 * G, device=dev, dtype=torch.uint8)
-                gathered[G:G + nbytes] = blob_full[G + beg[seg] + (pos - koff[seg])]
-                present = torch.zeros(len(rows), device=dev, dtype=torch.uint8)
-                del seg, pos, beg, ln
-                torch.cuda.synchronize()
-                _native.check(lib.dsy_bloom_test_dev(ctx.handle, ctypes.byref(bf.params), gathered.data_ptr() + G,
-                                                     koff.data_ptr(), len(rows), d_filters.data_ptr() + foff,
-                                                     present.data_ptr()))
-                ctx.synchronize()
-                want = expected(rows, present.cpu().numpy().astype(bool), lens)
-                del gathered, koff, present
-            else:
-                want = rows
-            assert np.array_equal(got, want), (i, len(got), len(want))
+        for j, i in enumerate(pick):
+            got = h_idx[h_off[i]:h_off[i + 1]].astype(np.int64).tolist()
+            assert got == want[j], (i, len(got), len(want[j]))
             sent += len(got)
-        assert sent > 0
+        assert sent > 0 and len(pick) == 256
     finally:
         lib.dsy_store_free(store)
         del blob_full, offsets
