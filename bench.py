@@ -1375,7 +1375,7 @@ def large_filter(args, ctx, lib, dev, rank, world, dist=None):
                                                             present.data_ptr()))
         filt.zero_()
         ctx.wait_torch(dev)  # torch's zeroing before the ctx stream's build
-        k_add, _ = _timed_bloom(ctx, add, 1)
+        k_add, wall_add = _timed_bloom(ctx, add, 1)
         union = None
         if dist is not None and world > 1:
             # the whole build as a job: every rank adds its shard, then all-gather + OR of the partial filters
@@ -1390,7 +1390,7 @@ def large_filter(args, ctx, lib, dev, rank, world, dist=None):
             t_job = coll.scalar(time.perf_counter() - t0, "max", device=dev)
             filt.copy_(union)
             torch.cuda.synchronize()
-        k_test, _ = _timed_bloom(ctx, test, 3)
+        k_test, wall_test = _timed_bloom(ctx, test, 3)
         ones = int(np.unpackbits(filt.cpu().numpy().view(np.uint8)[:m // 8]).sum())
         if union is not None:
             out.setdefault("sharded_build", {})["2^%d" % bits] = {
@@ -1401,9 +1401,11 @@ def large_filter(args, ctx, lib, dev, rank, world, dist=None):
         out["filters"]["2^%d" % bits] = {
             "hash": "%s k=%d chunk=%d" % (bf.hash_name, bf.functions, bf.chunk_bytes),
             "add_keys_per_s": round(n_add / k_add, 1), "add_ms": round(k_add * 1e3, 2),
+            "add_wall_keys_per_s": round(n_add / wall_add, 1),
             "add_gblocks_per_s": round(add_blocks / k_add / 1e9, 2),
             "add_valu_frac": round(add_blocks * OPS_PER_BLOCK["sha256"] / k_add / 1e12 / PEAK_INT32_TOPS, 4),
             "test_keys_per_s": round(n_test / k_test, 1), "test_ms": round(k_test * 1e3, 2),
+            "test_wall_keys_per_s": round(n_test / wall_test, 1),
             "test_gblocks_per_s": round(test_blocks / k_test / 1e9, 2),
             "bits_set": ones, "present_fraction": round(float(present.float().mean().item()), 4),
         }

@@ -149,6 +149,7 @@ class SyncCommunity(object):
         the module-level random()/randint() draws (prefix, skip, modulo offset).  Both default to `random`.
         clock: the time() acceptable_global_time's 5-second cache reads (default time.time)."""
         self._store = store
+        self._respond_out = None  # _respond_requests' reusable output buffer
         self._meta_messages = OrderedDict((m.name, m) for m in meta_messages)
         self._global_time = global_time
         self._signature_length = signature_length
@@ -879,9 +880,13 @@ class SyncCommunity(object):
         ctx = st.ctx
         mt, n_metas = self.meta_records()
         out_off = np.zeros(R + 1, dtype=np.uint64)
-        cap = 1 << 16
+        # one output buffer per community, grown on demand and reused by every call (the answer is copied out of it:
+        # RowLists handed to callers never alias the next call's output)
+        out = self._respond_out
+        if out is None:
+            out = self._respond_out = np.empty(1 << 16, dtype=np.uint64)
         while True:
-            out = np.empty(cap, dtype=np.uint64)
+            cap = len(out)
             if refs is None:
                 rc = ctx.lib.dsy_sync_respond(ctx.handle, st.handle,
                                               reqs.ctypes.data_as(ctypes.POINTER(_native.Request)), R, blob, len(blob),
@@ -892,11 +897,11 @@ class SyncCommunity(object):
                                                    self.global_time, 1 if include_inactive else 0, int(byte_limit),
                                                    seed, out.ctypes.data, cap, out_off.ctypes.data)
             if rc == _native.DSY_ECAPACITY and int(out_off[R]) > cap:
-                cap = int(out_off[R])
+                out = self._respond_out = np.empty(int(out_off[R]), dtype=np.uint64)
                 continue
             _native.check(rc)
             break
-        return RowLists(out[:int(out_off[R])].view(np.int64), out_off.view(np.int64))
+        return RowLists(out[:int(out_off[R])].view(np.int64).copy(), out_off.view(np.int64))
 
     def on_introduction_request_sync(self, messages, include_inactive=False):
         """The sync half of on_introduction_request (community.py:2531-2572) for a receive batch.
