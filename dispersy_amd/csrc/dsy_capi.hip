@@ -76,6 +76,7 @@ struct RespondJob {
     const dsy_store* s = nullptr;
     std::vector<std::vector<uint32_t>> fam_active;  // per family: its active claims
     std::vector<int> fam_id;
+    std::vector<uint8_t> pad1;  // per claim: a 1-byte prefix (the line copy's padded messages, hash_key_dma_lines)
     RespondLaunch L{};
     uint64_t pool = 0;
     uint8_t* h_in = nullptr;   // pinned staging (upload region, then host-mapped status)
@@ -816,7 +817,8 @@ static int store_finish(dsy_ctx* c, dsy_store* s, const uint64_t* h_gt_or_null, 
 
 // The responder's line copy: row i's packet at rec[i].off, kLineBias bytes past a multiple of 128, so every LDS-DMA
 // piece of the hashing kernel is one whole line and a 1-byte-prefixed message is line-aligned (dsy_message.h
-// hash_key_dma_lines).  Costs <= 128 bytes per row.
+// hash_key_dma_lines); 0x80 and zeros after the packet up to its padded message's bit length (line_bytes_for).
+// Costs < 192 bytes per row.
 static int store_build_lines(dsy_ctx* c, dsy_store* s, const uint64_t* h_off) {
     const uint64_t n = s->n;
     std::vector<RowRec> rec(std::max<uint64_t>(n, 1));
@@ -824,7 +826,7 @@ static int store_build_lines(dsy_ctx* c, dsy_store* s, const uint64_t* h_off) {
     for (uint64_t i = 0; i < n; ++i) {
         const uint64_t len = h_off[i + 1] - h_off[i];
         rec[i] = RowRec{at + kLineBias, (uint32_t)len, 0u};
-        at += (len + kLineBias + 127) & ~127ull;
+        at += line_bytes_for(len);
     }
     const uint64_t bytes = at + DSY_BLOB_GUARD;
     void *pl, *pr;
@@ -1321,7 +1323,7 @@ static int store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, const uin
     for (uint64_t j = 0; j < a; ++j) {
         const uint64_t len = offsets[j + 1] - offsets[j];
         h_rec[j] = RowRec{at + kLineBias, (uint32_t)len, 0u};
-        at += (len + kLineBias + 127) & ~127ull;
+        at += line_bytes_for(len);
     }
     for (uint64_t j = 0; j <= a; ++j) h_off[j] = offsets[j] - base0;
     std::memcpy(c->in_stage + b_off + b_rec, gt, a * 8);
@@ -1630,7 +1632,7 @@ int dsy_store_replace(dsy_ctx* c, dsy_store* s, const uint64_t* rows, const uint
     for (uint64_t i = 0; i < k; ++i) {
         const uint64_t len = offsets[i + 1] - offsets[i];
         nrec[i] = RowRec{at + kLineBias, (uint32_t)len, 0u};
-        at += (len + kLineBias + 127) & ~127ull;
+        at += line_bytes_for(len);
         minlen = std::min(minlen, len);
     }
     for (uint64_t i = 0; i <= k; ++i) noff[i] = offsets[i] - base0;
@@ -2087,17 +2089,30 @@ static int job_window(dsy_ctx* c, RespondSlot& sl) {
     for (size_t f = 0; f < jb.fam_active.size(); ++f) {
         if (!runs[f].second) continue;
         const int fid = jb.fam_id[f];
-        timer_dispatch(c, &t, kTimePairTest, &L.ev_start, &L.ev_stop);
         const int kc = fid / 2;
         const uint32_t chunk = kc % 3 == 0 ? 2 : kc % 3 == 1 ? 4 : 8;
-        if ((L.pool_mask >> fid) & 1u)
+        if ((L.pool_mask >> fid) & 1u) {
+            timer_dispatch(c, &t, kTimePairTest, &L.ev_start, &L.ev_stop);
             HIP_TRY(launch_pair_test_pooled(L, kc / 3, chunk, fid % 2 == 1, (uint32_t)fid, jb.d_slots + runs[f].first,
                                             (uint32_t)runs[f].second));
-        else
-            HIP_TRY(launch_pair_test_list(L, kc / 3, chunk, fid % 2 == 1, jb.d_slots + runs[f].first,
-                                          (uint32_t)runs[f].second));
-        timer_dispatched(c, &t);
-        L.ev_start = L.ev_stop = nullptr;
+            timer_dispatched(c, &t);
+            L.ev_start = L.ev_stop = nullptr;
+            continue;
+        }
+        // the family's 1-byte-prefix claims lead its run (job_start): one launch over the padded messages, one over
+        // the rest
+        size_t n1 = 0;
+        if (fid % 2 == 0)
+            for (uint32_t r : jb.fam_active[f]) n1 += jb.pad1[r];
+        const size_t part[2] = {n1, runs[f].second - n1};
+        for (int k = 0; k < 2; ++k) {
+            if (!part[k]) continue;
+            timer_dispatch(c, &t, kTimePairTest, &L.ev_start, &L.ev_stop);
+            HIP_TRY(launch_pair_test_list(L, kc / 3, chunk, fid % 2 == 1, k == 0,
+                                          jb.d_slots + runs[f].first + (k ? n1 : 0), (uint32_t)part[k]));
+            timer_dispatched(c, &t);
+            L.ev_start = L.ev_stop = nullptr;
+        }
     }
     if (trace_path) {
         uint32_t n = 0;
@@ -2193,6 +2208,12 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const Clai
         if (fm.empty()) fm.reserve(R);
         fm.push_back(r);
     }
+    // within a line-staged family, the claims of 1-byte prefixes (every reference claim) come first: their run hashes
+    // the line copy's padded messages (one launch), the 2-4-byte prefixes' run shifts and masks (another)
+    jb.pad1.assign(R, 0);
+    for (uint32_t r = 0; r < R; ++r) jb.pad1[r] = cl.shape(r).prefix_len == 1;
+    for (int f = 0; f < kFamilies; f += 2)
+        std::stable_partition(fam_members[f].begin(), fam_members[f].end(), [&](uint32_t r) { return jb.pad1[r] != 0; });
     for (uint32_t j = 0; j < J; ++j)
         if (metas[j].direction < DSY_ASC || metas[j].direction > DSY_RANDOM)
             return fail(DSY_EINVAL, "meta %u: unknown synchronization direction %d", j, metas[j].direction);

@@ -271,8 +271,9 @@ hipError_t launch_fill(const RespondLaunch& L);
 hipError_t launch_fill_first(const RespondLaunch& L, const void* h_src, void* d_dst, size_t in_bytes, void* d_counters,
                              size_t counter_bytes, uint64_t per_claim_cap, const uint32_t* h_act);
 // hash + test the window's pairs of the listed window slots, all of one (hash kind, chunk) family
-// long_prefix: the listed claims' prefixes are longer than 4 bytes (hashed without the LDS-DMA staging)
-hipError_t launch_pair_test_list(const RespondLaunch& L, int kind, uint32_t chunk, bool long_prefix,
+// long_prefix: the listed claims' prefixes are longer than 4 bytes (hashed without the LDS-DMA staging); padded: their
+// prefixes are 1 byte (the line copy's padded messages, dsy_message.h line_bytes_for)
+hipError_t launch_pair_test_list(const RespondLaunch& L, int kind, uint32_t chunk, bool long_prefix, bool padded,
                                  const uint32_t* d_list, uint32_t n);
 // a pooled family (bit fam of L.pool_mask): its listed claims' window pairs into L.pool in block-count order
 // (k_pool_scatter), then one hashing launch over the pool (k_pair_test<POOL>)

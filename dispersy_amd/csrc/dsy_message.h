@@ -242,6 +242,15 @@ __device__ __forceinline__ uint32_t lds_local(uint8_t* p) {
 // :911) starts exactly on the line, and the responder's blocks need no byte shift.
 static constexpr uint64_t kLineBias = 1;
 
+// Bytes of line copy a packet of `len` bytes takes: its 1-byte-prefixed message padded to whole 64-byte blocks
+// (MD5 / SHA-1 / SHA-256: 0x80, zeros, the 8-byte bit length), in whole lines.  The copy holds the 0x80 after every
+// packet and zeros up to the end of the final block (k_store_lines), so a 1-byte-prefixed message's blocks come out of
+// the line copy already padded and the hashing kernel only writes the bit length (hash_key_dma_lines).
+__host__ __device__ __forceinline__ uint64_t line_bytes_for(uint64_t len) {
+    const uint64_t padded = 64 * ((len + kLineBias + 8) / 64 + 1);
+    return (padded + 127) & ~127ull;
+}
+
 // DmaLanes for line-aligned keys (hash_key_dma_lines): each piece is named by its 128-byte line index relative to a
 // wave-uniform base (u32: 512 GB of lines) and the lengths of two keys share a register, so the per-key list costs
 // 12 VGPRs instead of 24 -- the responder kernel sits at its 128-VGPR cap.
@@ -249,11 +258,12 @@ struct DmaLinePieces {
     using G = DmaGeometry<2, 1>;
     uint32_t line[G::kInsts];      // key p_i's first line, in lines from the base
     uint32_t len2[G::kInsts / 2];  // end of keys p_2j (low half) / p_2j+1 (high half) in their first line, < 65536
-    // key = base + line * 128 + kLineBias; a piece is live when it holds a byte of [line start, key + len)
-    __device__ __forceinline__ void init(const uint8_t* base, const uint8_t* key, uint32_t len) {
+    // key = base + line * 128 + kLineBias; a piece is live when it holds a byte of [line start, line start + end)
+    // (end < 65536: the packet's bytes, or its padded message's up to the bit length)
+    __device__ __forceinline__ void init(const uint8_t* base, const uint8_t* key, uint32_t end) {
         const uint32_t lane = threadIdx.x & 63;
         const uint32_t my_line = (uint32_t)((uint64_t)(key - base) >> 7);
-        const uint32_t my_end = len + (uint32_t)kLineBias;
+        const uint32_t my_end = end;
 #pragma unroll
         for (int i = 0; i < G::kInsts; ++i) {
             const int p = G::kKeysPerInst * i + (int)(lane / G::kChunks);
@@ -316,6 +326,24 @@ __device__ __forceinline__ void finish_block(uint32_t* x, uint32_t o0, uint32_t 
             x[14] = last ? (uint32_t)bits : x[14];
             x[15] = last ? (uint32_t)(bits >> 32) : x[15];
         }
+    }
+}
+
+// finish_block for a block read from the line copy's padded message (line_bytes_for): the terminator and the zeros are
+// in place already; only the byte swap and, in the final block, the bit length remain.
+template <class H>
+__device__ __forceinline__ void finish_block_padded(uint32_t* x, uint32_t total, bool last) {
+    if (H::big_endian) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[i] = bswap32(x[i]);
+    }
+    const uint64_t bits = (uint64_t)total * 8u;
+    if (H::big_endian) {
+        x[14] = last ? (uint32_t)(bits >> 32) : x[14];
+        x[15] = last ? (uint32_t)bits : x[15];
+    } else {
+        x[14] = last ? (uint32_t)bits : x[14];
+        x[15] = last ? (uint32_t)(bits >> 32) : x[15];
     }
 }
 
@@ -465,10 +493,12 @@ __device__ __forceinline__ void hash_key_dma_reg(const KeyView& kv, H& st, uint8
 // (wave-uniform: one claim per wave): a uniform alignbyte funnel with a one-dword carry from the previous stage.
 // Single 8 KiB buffer per wave, like hash_key_dma_reg<H, 2>.  Requires 1 <= r <= 4 (the responder routes other
 // prefixes to the byte-wise path), kv.key = lines + 128 * line + kLineBias, at most 2^32 lines past `lines` (the
-// copy's base, wave-uniform); line bytes past the packet are not loaded (their words are masked by finish_block).
+// copy's base, wave-uniform); line bytes past the packet are not loaded (their words are masked by finish_block) --
+// except with PADDED (every lane's prefix is 1 byte, the message is line-aligned): the line copy holds the padded
+// message (line_bytes_for), its pieces are loaded up to the bit length and the blocks need no masking.
 // preword: the r prefix bytes, little-endian (wave-uniform: read once per claim).  MODE as in hash_key_dma_reg
 // (k_pair_test DIAG diagnostics only).
-template <class H, int MODE = 0>
+template <class H, int MODE = 0, bool PADDED = false>
 __device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uint8_t* lds_wave, uint32_t preword,
                                                    const uint8_t* lines) {
     static_assert(H::block_bytes == 64, "LDS-DMA staging is for 64-byte blocks");
@@ -483,14 +513,14 @@ __device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uin
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, d, 64));
     const uint32_t nst = (nbmax + 1) / 2;
-    const uint32_t tmin = wave_min_u32(total);
+    const uint32_t tmin = PADDED ? 0u : wave_min_u32(total);
     DmaLinePieces dl;
-    dl.init(lines, kv.key, len);  // stage s is line s of the packet
+    dl.init(lines, kv.key, PADDED ? 64 * nb - 8 : len + (uint32_t)kLineBias);  // stage s is line s of the packet
     st.init();
     // message byte j is line byte j - rr (rr = r - 1): the carry is the dword before the stage's first one, its top
     // rr bytes the message bytes before the stage (at stage 0 the first rr prefix bytes); the slack byte, line byte 0
     // of stage 0, becomes the last prefix byte
-    const uint32_t rr = r - 1;
+    const uint32_t rr = PADDED ? 0u : r - 1;
     uint32_t carry = rr ? (preword & low_bytes_mask(rr)) << (8 * (4 - rr)) : 0u;
     const uint32_t slack = (preword >> (8 * rr)) & 0xffu;
     const uint32_t sh = (4 - rr) & 3;  // alignbyte shift for rr in 1..3
@@ -527,7 +557,8 @@ __device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uin
                     for (int i = 0; i < 16; ++i) x[i] = __builtin_amdgcn_alignbyte(d[1 + 16 * bb + i], d[16 * bb + i], sh);
                 }
                 const uint32_t o0 = b * 64;
-                finish_block<H>(x, o0, total, b + 1 == nb, o0 + 64 <= tmin);
+                if (PADDED) finish_block_padded<H>(x, total, b + 1 == nb);
+                else finish_block<H>(x, o0, total, b + 1 == nb, o0 + 64 <= tmin);
                 if (MODE != 2) st.compress(x);
                 else st.h[0] ^= x[0] ^ x[5] ^ x[10] ^ x[15];
             }

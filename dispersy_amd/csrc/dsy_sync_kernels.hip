@@ -1147,7 +1147,7 @@ __global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_waves_per_
 // POOL: the wave-tasks are 64 consecutive pairs of the family's pooled order (k_pool_scatter): the claim -- filter,
 // prefix, m, k -- is per lane.  pool_queue: waves take wave-tasks from a queue (longest first) instead of the grid
 // stride.
-template <class H, int CHUNK, bool DMA, int DIAG = 0, bool POOL = false>
+template <class H, int CHUNK, bool DMA, int DIAG = 0, bool POOL = false, bool PADDED = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_pair_test(RespondLaunch L, const uint32_t* __restrict__ req_list,
                                                    uint32_t n_list, uint32_t fam) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dma_lds[];
@@ -1268,7 +1268,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         H st;
         if constexpr (DMA) {
             // prefixes of 0 or > 4 bytes go to DMA = false
-            hash_key_dma_lines<H, DIAG>(kv, st, my_lds, q.prefix_word, L.st.lines);
+            hash_key_dma_lines<H, DIAG, PADDED>(kv, st, my_lds, q.prefix_word, L.st.lines);
         } else {
             hash_key<H>(kv, st);
         }
@@ -1326,7 +1326,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
 // SHA-256 only (the larger SHA-2 families take the per-claim order)
 template <class H, int CHUNK>
 static hipError_t pair_test_family(const RespondLaunch& L, bool long_prefix, const uint32_t* list, uint32_t n_list,
-                                   bool pooled = false, uint32_t fam = 0) {
+                                   bool pooled = false, uint32_t fam = 0, bool padded = false) {
     const uint64_t waves = (uint64_t)n_list * (L.window / 64);
     uint64_t blocks = (waves + 3) / 4;
     // 8 workgroups per CU (respond_core: the ctx's max_grid, DSY_PAIR_GRID overrides): the grid-stride then deals
@@ -1354,10 +1354,12 @@ static hipError_t pair_test_family(const RespondLaunch& L, bool long_prefix, con
     if constexpr (dma) {
         if (!long_prefix && !((L.direct_kinds >> H::kind) & 1u)) {
             const size_t lds = 4 * DmaGeometry<2, 1>::kWaveBytes;
-            auto kern = pooled ? k_pair_test<H, CHUNK, true, 0, true> : k_pair_test<H, CHUNK, true>;
+            // (padded: every listed claim has a 1-byte prefix -- the pooled order mixes prefixes, so it never is)
+            auto kern = pooled ? k_pair_test<H, CHUNK, true, 0, true>
+                               : padded ? k_pair_test<H, CHUNK, true, 0, false, true> : k_pair_test<H, CHUNK, true>;
             if constexpr (CHUNK == 2) {  // (respond_core pools no family while a diagnostic build is asked for)
-                if (L.diag == 1) kern = k_pair_test<H, CHUNK, true, 1>;
-                if (L.diag == 2) kern = k_pair_test<H, CHUNK, true, 2>;
+                if (L.diag == 1) kern = padded ? k_pair_test<H, CHUNK, true, 1, false, true> : k_pair_test<H, CHUNK, true, 1>;
+                if (L.diag == 2) kern = padded ? k_pair_test<H, CHUNK, true, 2, false, true> : k_pair_test<H, CHUNK, true, 2>;
             }
             launch_timed(kern, dim3((uint32_t)blocks), dim3(256), lds, L.stream, L.ev_start, L.ev_stop, L, list, n_list,
                          fam);
@@ -1373,35 +1375,35 @@ static hipError_t pair_test_family(const RespondLaunch& L, bool long_prefix, con
 
 template <class H>
 static hipError_t pair_test_chunk(const RespondLaunch& L, uint32_t chunk, bool lp, const uint32_t* list, uint32_t n,
-                                  bool pooled, uint32_t fam) {
+                                  bool pooled, uint32_t fam, bool padded) {
     switch (chunk) {
-        case 2: return pair_test_family<H, 2>(L, lp, list, n, pooled, fam);
-        case 4: return pair_test_family<H, 4>(L, lp, list, n, pooled, fam);
-        default: return pair_test_family<H, 8>(L, lp, list, n, pooled, fam);
+        case 2: return pair_test_family<H, 2>(L, lp, list, n, pooled, fam, padded);
+        case 4: return pair_test_family<H, 4>(L, lp, list, n, pooled, fam, padded);
+        default: return pair_test_family<H, 8>(L, lp, list, n, pooled, fam, padded);
     }
 }
 
 static hipError_t pair_test_kind(const RespondLaunch& L, int kind, uint32_t chunk, bool long_prefix, const uint32_t* list,
-                                 uint32_t n, bool pooled, uint32_t fam) {
+                                 uint32_t n, bool pooled, uint32_t fam, bool padded) {
     switch (kind) {
-        case DSY_MD5: return pair_test_chunk<Md5>(L, chunk, long_prefix, list, n, pooled, fam);
+        case DSY_MD5: return pair_test_chunk<Md5>(L, chunk, long_prefix, list, n, pooled, fam, padded);
         case DSY_SHA1:
-            return chunk == 2 ? pair_test_family<Sha1, 2>(L, long_prefix, list, n, pooled, fam)
-                              : pair_test_family<Sha1, 4>(L, long_prefix, list, n, pooled, fam);
-        case DSY_SHA256: return pair_test_chunk<Sha256>(L, chunk, long_prefix, list, n, pooled, fam);
-        case DSY_SHA384: return pair_test_chunk<Sha384>(L, chunk, long_prefix, list, n, false, fam);
-        default: return pair_test_chunk<Sha512>(L, chunk, long_prefix, list, n, false, fam);
+            return chunk == 2 ? pair_test_family<Sha1, 2>(L, long_prefix, list, n, pooled, fam, padded)
+                              : pair_test_family<Sha1, 4>(L, long_prefix, list, n, pooled, fam, padded);
+        case DSY_SHA256: return pair_test_chunk<Sha256>(L, chunk, long_prefix, list, n, pooled, fam, false);
+        case DSY_SHA384: return pair_test_chunk<Sha384>(L, chunk, long_prefix, list, n, false, fam, false);
+        default: return pair_test_chunk<Sha512>(L, chunk, long_prefix, list, n, false, fam, false);
     }
 }
 
-hipError_t launch_pair_test_list(const RespondLaunch& L, int kind, uint32_t chunk, bool long_prefix, const uint32_t* list,
-                                 uint32_t n) {
-    return pair_test_kind(L, kind, chunk, long_prefix, list, n, false, 0);
+hipError_t launch_pair_test_list(const RespondLaunch& L, int kind, uint32_t chunk, bool long_prefix, bool padded,
+                                 const uint32_t* list, uint32_t n) {
+    return pair_test_kind(L, kind, chunk, long_prefix, list, n, false, 0, padded && !long_prefix);
 }
 
 hipError_t launch_pair_test_pooled(const RespondLaunch& L, int kind, uint32_t chunk, bool long_prefix, uint32_t fam,
                                    const uint32_t* list, uint32_t n) {
-    return pair_test_kind(L, kind, chunk, long_prefix, list, n, true, fam);
+    return pair_test_kind(L, kind, chunk, long_prefix, list, n, true, fam, false);
 }
 
 // ----------------------------------------------------------------------------------------- k_compact
@@ -1652,7 +1654,8 @@ __global__ void __launch_bounds__(256) k_pack_fused(RespondLaunch L, uint64_t* p
     if (r == 0) fold_status(L);
 }
 
-// one wave per row: bytes of the packet to its line-aligned place (coalesced 64-byte stretches)
+// one wave per row: bytes of the packet to its line-aligned place (coalesced 64-byte stretches), then the padded
+// message's terminator after it (the line copy is zeroed: the padding's zeros are there already; line_bytes_for)
 __global__ void __launch_bounds__(256) k_store_lines(const uint8_t* __restrict__ blob, const uint64_t* __restrict__ offsets,
                                                      const RowRec* __restrict__ rec, uint64_t n, uint8_t* __restrict__ lines) {
     const uint64_t row = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
@@ -1662,6 +1665,7 @@ __global__ void __launch_bounds__(256) k_store_lines(const uint8_t* __restrict__
     uint8_t* dst = lines + rec[row].off;
     const uint32_t len = rec[row].len;
     for (uint32_t k = lane; k < len; k += 64) dst[k] = src[k];
+    if (lane == 0) dst[len] = 0x80;
 }
 
 hipError_t launch_store_lines(const uint8_t* blob, const uint64_t* offsets, const RowRec* rec, uint64_t n,

@@ -66,8 +66,8 @@ def kernel_sha(lib, symbol_substring):
     return None
 
 
-# the headline kernel: k_pair_test<Md5, 2, DMA=true, DIAG=0, POOL=false>
-HEADLINE = "k_pair_testINS_3Md5ELi2ELb1ELi0ELb0E"
+# the headline kernel: k_pair_test<Md5, 2, DMA=true, DIAG=0, POOL=false, PADDED=true>
+HEADLINE = "k_pair_testINS_3Md5ELi2ELb1ELi0ELb0ELb1E"
 
 if __name__ == "__main__":
     print(kernel_sha(sys.argv[1], sys.argv[2]))
