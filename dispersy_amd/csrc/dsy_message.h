@@ -251,45 +251,52 @@ __host__ __device__ __forceinline__ uint64_t line_bytes_for(uint64_t len) {
     return (padded + 127) & ~127ull;
 }
 
-// DmaLanes for line-aligned keys (hash_key_dma_lines): each piece is named by its 128-byte line index relative to a
-// wave-uniform base (u32: 512 GB of lines) and the lengths of two keys share a register, so the per-key list costs
-// 12 VGPRs instead of 24 -- the responder kernel sits at its 128-VGPR cap.
+// DmaLanes for line-aligned keys (hash_key_dma_lines).  Piece i of a lane is 16-byte chunk c_i of key p_i = 8 i +
+// lane / 8 with an XOR swizzle, c_i = (lane % 8) ^ (p_i / 2 % 8): key k's chunk q then sits at (its LDS row) + 16 (q ^
+// (k / 2 % 8)), one XOR per read, and the 16 lanes of each ds_read_b128 bank group still hit 16 distinct 16-byte
+// bank groups.  A piece is kept as what its issue needs: idx_i = 8 x (key p_i's first line) + c_i, its stage-0
+// address in 16-byte units from the wave-uniform base (stage s: + 8 s), and the number of stages in which it holds
+// bytes to load (two per register) -- per stage and piece an add, a 64-bit shift-add and a compare.  12 VGPRs per
+// lane; needs the line copy under 64 GiB (idx < 2^32; pair_test_family checks).
 struct DmaLinePieces {
     using G = DmaGeometry<2, 1>;
-    uint32_t line[G::kInsts];      // key p_i's first line, in lines from the base
-    uint32_t len2[G::kInsts / 2];  // end of keys p_2j (low half) / p_2j+1 (high half) in their first line, < 65536
+    uint32_t idx[G::kInsts];
+    uint32_t ns2[G::kInsts / 2];  // live stages of pieces 2j (low half) / 2j+1 (high half)
     // key = base + line * 128 + kLineBias; a piece is live when it holds a byte of [line start, line start + end)
     // (end < 65536: the packet's bytes, or its padded message's up to the bit length)
     __device__ __forceinline__ void init(const uint8_t* base, const uint8_t* key, uint32_t end) {
         const uint32_t lane = threadIdx.x & 63;
         const uint32_t my_line = (uint32_t)((uint64_t)(key - base) >> 7);
-        const uint32_t my_end = end;
 #pragma unroll
         for (int i = 0; i < G::kInsts; ++i) {
-            const int p = G::kKeysPerInst * i + (int)(lane / G::kChunks);
-            line[i] = (uint32_t)__shfl((int)my_line, p, 64);
-            const uint32_t lv = (uint32_t)__shfl((int)my_end, p, 64);
-            if (i & 1) len2[i / 2] |= lv << 16;
-            else len2[i / 2] = lv;
+            const uint32_t p = G::kKeysPerInst * i + lane / G::kChunks;
+            const uint32_t c = (lane % G::kChunks) ^ ((p >> 1) & 7);
+            const uint32_t ln = (uint32_t)__shfl((int)my_line, (int)p, 64);
+            const uint32_t e = (uint32_t)__shfl((int)end, (int)p, 64);
+            idx[i] = (ln << 3) + c;
+            const uint32_t ns = e > 16 * c ? (e - 16 * c + 127) >> 7 : 0u;
+            if (i & 1) ns2[i / 2] |= ns << 16;
+            else ns2[i / 2] = ns;
         }
     }
-    // a 16-byte piece is loaded only when it holds packet bytes: the last line of a packet moves only the chunks
+    // a 16-byte piece is loaded only when it holds bytes to hash: the last line of a packet moves only the chunks
     // its bytes reach (the rest of that line is padding)
     // lds: the wave's LDS buffer as a wave-uniform local address (lds_local), so each instruction's M0 is a scalar add
     template <bool SKIP = false>
     __device__ __forceinline__ void issue(uint32_t s, const uint8_t* base, uint32_t lds) const {
         if constexpr (SKIP) return;
-        const uint32_t lane = threadIdx.x & 63;
 #pragma unroll
         for (int i = 0; i < G::kInsts; ++i) {
-            const uint32_t lv = (i & 1) ? len2[i / 2] >> 16 : len2[i / 2] & 0xffffu;
-            const int p = G::kKeysPerInst * i + (int)(lane / G::kChunks);
-            const uint32_t c = ((lane % G::kChunks) + ((uint32_t)p >> G::kShift)) % G::kChunks;
-            if (s * 128 + 16 * c < lv)
-                __builtin_amdgcn_global_load_lds((const void*)(base + ((uint64_t)(line[i] + s) << 7) + 16 * c),
+            const uint32_t ns = (i & 1) ? ns2[i / 2] >> 16 : ns2[i / 2] & 0xffffu;
+            if (s < ns)
+                __builtin_amdgcn_global_load_lds((const void*)(base + ((uint64_t)(idx[i] + (s << 3)) << 4)),
                                                  (__attribute__((address_space(3))) void*)(uintptr_t)(lds + i * 1024),
                                                  16, 0, 0);
         }
+    }
+    // key k's (this lane's) chunk q of the staged line: its LDS row, then one XOR per chunk
+    __device__ __forceinline__ static uint32_t row_of(uint32_t k) {
+        return (k >> 3) * 1024 + 128 * (k & 7) + 16 * ((k >> 1) & 7);
     }
 };
 
@@ -531,11 +538,10 @@ __device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uin
         __builtin_amdgcn_wave_barrier();
         uint32_t d[33];
         d[0] = carry;
+        const uint32_t row = DmaLinePieces::row_of(lane);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-            const uint32_t slot = (q - (lane >> G::kShift)) % G::kChunks;
-            const uint4 v = *(const uint4*)(lds_wave + (lane / G::kKeysPerInst) * 1024 +
-                                            16 * (G::kChunks * (lane % G::kKeysPerInst) + slot));
+            const uint4 v = *(const uint4*)(lds_wave + (row ^ (16u * q)));
             d[1 + 4 * q] = v.x; d[2 + 4 * q] = v.y; d[3 + 4 * q] = v.z; d[4 + 4 * q] = v.w;
         }
         if (s == 0) d[1] = (d[1] & ~0xffu) | slack;

@@ -1352,7 +1352,8 @@ static hipError_t pair_test_family(const RespondLaunch& L, bool long_prefix, con
     // tools/hashbench, profiles/hashbench_r1_dmareg.txt); SHA-2 is compute-bound enough that direct loads match it
     constexpr bool dma = H::kind == DSY_MD5 || H::kind == DSY_SHA1;
     if constexpr (dma) {
-        if (!long_prefix && !((L.direct_kinds >> H::kind) & 1u)) {
+        // (the line-staged pieces address the line copy in 16-byte units from a 32-bit index: under 64 GiB)
+        if (!long_prefix && !((L.direct_kinds >> H::kind) & 1u) && L.st.lines_bytes < (1ull << 36)) {
             const size_t lds = 4 * DmaGeometry<2, 1>::kWaveBytes;
             // (padded: every listed claim has a 1-byte prefix -- the pooled order mixes prefixes, so it never is)
             auto kern = pooled ? k_pair_test<H, CHUNK, true, 0, true>
