@@ -354,6 +354,31 @@ __device__ __forceinline__ void finish_block_padded(uint32_t* x, uint32_t total,
     }
 }
 
+// Wave-wide max / min of a lane value, wave-uniform (SGPR): DPP within each row of 16 lanes, then the four rows'
+// results by readlane -- four VALU and four readlanes instead of six ds_bpermute round trips.  Every lane active.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t wave_max_uniform(uint32_t v) {
+    v = max(v, dpp_u32<0xB1>(v));   // quad_perm [1, 0, 3, 2]
+    v = max(v, dpp_u32<0x4E>(v));   // quad_perm [2, 3, 0, 1]
+    v = max(v, dpp_u32<0x141>(v));  // row_half_mirror
+    v = max(v, dpp_u32<0x140>(v));  // row_mirror
+    const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+    const uint32_t c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+    return max(max(a, b), max(c, d));
+}
+__device__ __forceinline__ uint32_t wave_min_uniform(uint32_t v) {
+    v = min(v, dpp_u32<0xB1>(v));
+    v = min(v, dpp_u32<0x4E>(v));
+    v = min(v, dpp_u32<0x141>(v));
+    v = min(v, dpp_u32<0x140>(v));
+    const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+    const uint32_t c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+    return min(min(a, b), min(c, d));
+}
+
 // wave minimum of a lane value
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 #pragma unroll
@@ -503,24 +528,20 @@ __device__ __forceinline__ void hash_key_dma_reg(const KeyView& kv, H& st, uint8
 // copy's base, wave-uniform); line bytes past the packet are not loaded (their words are masked by finish_block) --
 // except with PADDED (every lane's prefix is 1 byte, the message is line-aligned): the line copy holds the padded
 // message (line_bytes_for), its pieces are loaded up to the bit length and the blocks need no masking.
-// preword: the r prefix bytes, little-endian (wave-uniform: read once per claim).  MODE as in hash_key_dma_reg
-// (k_pair_test DIAG diagnostics only).
+// preword: the r prefix bytes, little-endian (wave-uniform: read once per claim).  nbmax: the wave's most blocks
+// (wave-uniform; the caller has it).  MODE as in hash_key_dma_reg (k_pair_test DIAG diagnostics only).
 template <class H, int MODE = 0, bool PADDED = false>
 __device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uint8_t* lds_wave, uint32_t preword,
-                                                   const uint8_t* lines) {
+                                                   const uint8_t* lines, uint32_t nbmax) {
     static_assert(H::block_bytes == 64, "LDS-DMA staging is for 64-byte blocks");
     static_assert(kLineBias == 1, "the shift below assumes one byte of slack before every packet");
-    using G = DmaGeometry<2, 1>;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t r = kv.plen;  // wave-uniform, 1..4
     const uint32_t len = kv.len;
     const uint32_t total = r + len;
     const uint32_t nb = n_blocks(total, 64, H::len_bytes);
-    uint32_t nbmax = nb;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, d, 64));
     const uint32_t nst = (nbmax + 1) / 2;
-    const uint32_t tmin = PADDED ? 0u : wave_min_u32(total);
+    const uint32_t tmin = PADDED ? 0u : wave_min_uniform(total);
     DmaLinePieces dl;
     dl.init(lines, kv.key, PADDED ? 64 * nb - 8 : len + (uint32_t)kLineBias);  // stage s is line s of the packet
     st.init();

@@ -1184,6 +1184,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
     // consecutive wave-tasks (about equal), and the workgroups of a CU take positions c, G/2 - 1 - c, G/2 + c,
     // G - 1 - c of the G workgroup positions (snaking over the quarters), so every SIMD's four waves sum to about the
     // mean when the wave-tasks come longest first.  Later rounds snake back.
+    const uint32_t nl_recip = n_list > 1 ? mod_recip(n_list) : 0u;  // ceil(2^32 / n_list): the task -> claim split
     const bool deal = L.pool_deal && gridDim.x % 4 == 0;
     const uint64_t wend = deal ? (total_waves + wstride - 1) / wstride * wstride : total_waves;
     for (uint64_t wv = queue ? next_task() : wave0; wv < wend; wv = queue ? next_task() : wv + wstride) {
@@ -1220,9 +1221,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         } else {
             // chunk-major task order: wave-task v hashes 64-pair chunk (v / n_list) of claim (v % n_list), so the
             // non-empty chunks of every claim come first (the longest packets of each) and spread over the grid
-            a_slot = req_list[v % n_list];
+            // (v < 2^32 on every real launch: one multiply-high instead of a 64-bit division per wave-task)
+            uint64_t chunk, slot_i;
+            if (v < (1ull << 32) && (n_list == 1 || nl_recip)) {
+                uint32_t q = n_list > 1 ? __umulhi((uint32_t)v, nl_recip) : (uint32_t)v;  // floor(v / n) or one more
+                int64_t rem = (int64_t)(uint32_t)v - (int64_t)q * n_list;
+                if (rem < 0) { --q; rem += n_list; }
+                chunk = q;
+                slot_i = (uint64_t)rem;
+            } else {
+                chunk = v / n_list;
+                slot_i = v % n_list;
+            }
+            a_slot = req_list[slot_i];
             r = L.act[a_slot];
-            const uint64_t i0 = (v / n_list) * 64;
+            const uint64_t i0 = chunk * 64;
             const uint64_t n = L.state[r].n_window;
             if (i0 >= n) continue;  // wave-uniform: past this claim's window
             if (n > W) {  // wave-uniform (cannot happen: the fill never places more than W pairs)
@@ -1251,9 +1264,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         const uint64_t trace_t0 = L.trace ? __builtin_amdgcn_s_memrealtime() : 0;
         const uint32_t nb = active ? n_blocks(kv.plen + kv.len, H::block_bytes, H::len_bytes) : 0u;
         // lane-block slots this wave-task occupies: 64 x the longest lane (load-balance denominator)
-        uint32_t nbmax = nb;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, d, 64));
+        const uint32_t nbmax = wave_max_uniform(nb);
         // the SIMD's arbiter issues for the longest wave-tasks first: a heavy-tailed window's few 64 KB packets (1024
         // blocks of serial digest) set its end.  pair_prio 1 (default): tasks of >= 32 blocks (2 KB packets; config
         // 5: k_pair_test -4 %, the headline's packets never qualify); 2: every task by length (packets of 100-1500 B
@@ -1268,7 +1279,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         H st;
         if constexpr (DMA) {
             // prefixes of 0 or > 4 bytes go to DMA = false
-            hash_key_dma_lines<H, DIAG, PADDED>(kv, st, my_lds, q.prefix_word, L.st.lines);
+            // (the idle lanes' empty keys hash one block: a wave with no active lane still walks one stage)
+            hash_key_dma_lines<H, DIAG, PADDED>(kv, st, my_lds, q.prefix_word, L.st.lines, max(nbmax, 1u));
         } else {
             hash_key<H>(kv, st);
         }
