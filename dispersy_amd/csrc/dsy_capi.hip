@@ -2092,9 +2092,13 @@ static int job_window(dsy_ctx* c, RespondSlot& sl) {
         const int kc = fid / 2;
         const uint32_t chunk = kc % 3 == 0 ? 2 : kc % 3 == 1 ? 4 : 8;
         if ((L.pool_mask >> fid) & 1u) {
+            // (a pooled wave mixes claims: the padded messages only when every claim of the family has a 1-byte prefix)
+            size_t p1 = 0;
+            if (fid % 2 == 0)
+                for (uint32_t r : jb.fam_active[f]) p1 += jb.pad1[r];
             timer_dispatch(c, &t, kTimePairTest, &L.ev_start, &L.ev_stop);
-            HIP_TRY(launch_pair_test_pooled(L, kc / 3, chunk, fid % 2 == 1, (uint32_t)fid, jb.d_slots + runs[f].first,
-                                            (uint32_t)runs[f].second));
+            HIP_TRY(launch_pair_test_pooled(L, kc / 3, chunk, fid % 2 == 1, p1 == runs[f].second, (uint32_t)fid,
+                                            jb.d_slots + runs[f].first, (uint32_t)runs[f].second));
             timer_dispatched(c, &t);
             L.ev_start = L.ev_stop = nullptr;
             continue;

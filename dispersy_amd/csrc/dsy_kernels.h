@@ -277,8 +277,8 @@ hipError_t launch_pair_test_list(const RespondLaunch& L, int kind, uint32_t chun
                                  const uint32_t* d_list, uint32_t n);
 // a pooled family (bit fam of L.pool_mask): its listed claims' window pairs into L.pool in block-count order
 // (k_pool_scatter), then one hashing launch over the pool (k_pair_test<POOL>)
-hipError_t launch_pair_test_pooled(const RespondLaunch& L, int kind, uint32_t chunk, bool long_prefix, uint32_t fam,
-                                   const uint32_t* d_list, uint32_t n);
+hipError_t launch_pair_test_pooled(const RespondLaunch& L, int kind, uint32_t chunk, bool long_prefix, bool padded,
+                                   uint32_t fam, const uint32_t* d_list, uint32_t n);
 hipError_t launch_compact(const RespondLaunch& L);
 // done (optional): an event the last pack kernel's dispatch records when it completes
 hipError_t launch_pack(const RespondLaunch& L, uint64_t* packed, uint64_t* packed_offsets, uint64_t* d_scan_tmp,

@@ -1367,8 +1367,8 @@ static hipError_t pair_test_family(const RespondLaunch& L, bool long_prefix, con
         // (the line-staged pieces address the line copy in 16-byte units from a 32-bit index: under 64 GiB)
         if (!long_prefix && !((L.direct_kinds >> H::kind) & 1u) && L.st.lines_bytes < (1ull << 36)) {
             const size_t lds = 4 * DmaGeometry<2, 1>::kWaveBytes;
-            // (padded: every listed claim has a 1-byte prefix -- the pooled order mixes prefixes, so it never is)
-            auto kern = pooled ? k_pair_test<H, CHUNK, true, 0, true>
+            // (padded: every listed claim has a 1-byte prefix)
+            auto kern = pooled ? (padded ? k_pair_test<H, CHUNK, true, 0, true, true> : k_pair_test<H, CHUNK, true, 0, true>)
                                : padded ? k_pair_test<H, CHUNK, true, 0, false, true> : k_pair_test<H, CHUNK, true>;
             if constexpr (CHUNK == 2) {  // (respond_core pools no family while a diagnostic build is asked for)
                 if (L.diag == 1) kern = padded ? k_pair_test<H, CHUNK, true, 1, false, true> : k_pair_test<H, CHUNK, true, 1>;
@@ -1414,9 +1414,9 @@ hipError_t launch_pair_test_list(const RespondLaunch& L, int kind, uint32_t chun
     return pair_test_kind(L, kind, chunk, long_prefix, list, n, false, 0, padded && !long_prefix);
 }
 
-hipError_t launch_pair_test_pooled(const RespondLaunch& L, int kind, uint32_t chunk, bool long_prefix, uint32_t fam,
-                                   const uint32_t* list, uint32_t n) {
-    return pair_test_kind(L, kind, chunk, long_prefix, list, n, true, fam, false);
+hipError_t launch_pair_test_pooled(const RespondLaunch& L, int kind, uint32_t chunk, bool long_prefix, bool padded,
+                                   uint32_t fam, const uint32_t* list, uint32_t n) {
+    return pair_test_kind(L, kind, chunk, long_prefix, list, n, true, fam, padded && !long_prefix);
 }
 
 // ----------------------------------------------------------------------------------------- k_compact

@@ -28,9 +28,12 @@ def pooled_ctx(request, monkeypatch):
     ctx.close()
 
 
+@pytest.mark.parametrize("one_byte", [False, True], ids=["prefixes0-5", "prefix1"])
 @pytest.mark.parametrize("window", [0, 256])
 @pytest.mark.parametrize("skew", [False, "dense"])
-def test_pooled_families_vs_oracle(pooled_ctx, skew, window):
+def test_pooled_families_vs_oracle(pooled_ctx, skew, window, one_byte):
+    """one_byte: every claim's prefix is 1 byte (every reference claim), so the pooled MD5 / SHA-1 families hash the
+    line copy's padded messages (k_pair_test<..., POOL, PADDED>)."""
     seed = 3 if skew is False else 4
     rows, conn = build(seed, 30_000, 120_000 if skew is False else 5_000, skew)
     store = SyncStore.from_rows(rows, ctx=pooled_ctx)
@@ -50,7 +53,7 @@ def test_pooled_families_vs_oracle(pooled_ctx, skew, window):
         lo = int(rng.integers(1, gt_now // 2))
         hi = int(rng.integers(lo, gt_now + 10))
         m, f = shapes[q % len(shapes)]
-        prefix = bytes(rng.integers(0, 256, size=int(q % 6), dtype=np.uint8))
+        prefix = bytes(rng.integers(0, 256, size=1 if one_byte else int(q % 6), dtype=np.uint8))
         bf, ob = BloomFilter(m, f, prefix), OracleBloom.from_m_f(m, f, prefix)
         known = [packets[r[0]] for r in rows if rng.random() < 0.9]
         bf.add_keys(known)
