@@ -255,29 +255,35 @@ __host__ __device__ __forceinline__ uint64_t line_bytes_for(uint64_t len) {
 // lane / 8 with an XOR swizzle, c_i = (lane % 8) ^ (p_i / 2 % 8): key k's chunk q then sits at (its LDS row) + 16 (q ^
 // (k / 2 % 8)), one XOR per read, and the 16 lanes of each ds_read_b128 bank group still hit 16 distinct 16-byte
 // bank groups.  A piece is kept as what its issue needs: idx_i = 8 x (key p_i's first line) + c_i, its stage-0
-// address in 16-byte units from the wave-uniform base (stage s: + 8 s), and the number of stages in which it holds
-// bytes to load (two per register) -- per stage and piece an add, a 64-bit shift-add and a compare.  12 VGPRs per
+// address in 16-byte units from the wave-uniform base (stage s: + 8 s), and how many bytes from there it has to load
+// (two per register; stage s is live while 128 s < lim) -- per stage and piece an add, a 64-bit shift-add and a
+// compare.  12 VGPRs per
 // lane; needs the line copy under 64 GiB (idx < 2^32; pair_test_family checks).
 struct DmaLinePieces {
     using G = DmaGeometry<2, 1>;
     uint32_t idx[G::kInsts];
-    uint32_t ns2[G::kInsts / 2];  // live stages of pieces 2j (low half) / 2j+1 (high half)
+    uint32_t lim2[G::kInsts / 2];  // bytes of pieces 2j (low half) / 2j+1 (high half) from their stage-0 start to load
     // key = base + line * 128 + kLineBias; a piece is live when it holds a byte of [line start, line start + end)
-    // (end < 65536: the packet's bytes, or its padded message's up to the bit length)
-    __device__ __forceinline__ void init(const uint8_t* base, const uint8_t* key, uint32_t end) {
+    // (end < 65536: the packet's bytes, or its padded message's up to the bit length).  Every lane's (line, end) goes
+    // through the wave's LDS buffer, free until the first stage's DMA: one ds_write_b64 and eight broadcast
+    // ds_read_b64 instead of sixteen ds_bpermute.
+    __device__ __forceinline__ void init(const uint8_t* base, const uint8_t* key, uint32_t end, uint8_t* lds_wave) {
         const uint32_t lane = threadIdx.x & 63;
         const uint32_t my_line = (uint32_t)((uint64_t)(key - base) >> 7);
+        uint2* xs = (uint2*)lds_wave;
+        xs[lane] = make_uint2(my_line, end);
 #pragma unroll
         for (int i = 0; i < G::kInsts; ++i) {
             const uint32_t p = G::kKeysPerInst * i + lane / G::kChunks;
             const uint32_t c = (lane % G::kChunks) ^ ((p >> 1) & 7);
-            const uint32_t ln = (uint32_t)__shfl((int)my_line, (int)p, 64);
-            const uint32_t e = (uint32_t)__shfl((int)end, (int)p, 64);
-            idx[i] = (ln << 3) + c;
-            const uint32_t ns = e > 16 * c ? (e - 16 * c + 127) >> 7 : 0u;
-            if (i & 1) ns2[i / 2] |= ns << 16;
-            else ns2[i / 2] = ns;
+            const uint2 v = xs[p];
+            idx[i] = (v.x << 3) + c;
+            const uint32_t lim = max(v.y, 16 * c) - 16 * c;  // live while 128 s < lim
+            if (i & 1) lim2[i / 2] |= lim << 16;
+            else lim2[i / 2] = lim;
         }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the reads are done before the first stage's DMA lands
+        __builtin_amdgcn_wave_barrier();
     }
     // a 16-byte piece is loaded only when it holds bytes to hash: the last line of a packet moves only the chunks
     // its bytes reach (the rest of that line is padding)
@@ -287,8 +293,8 @@ struct DmaLinePieces {
         if constexpr (SKIP) return;
 #pragma unroll
         for (int i = 0; i < G::kInsts; ++i) {
-            const uint32_t ns = (i & 1) ? ns2[i / 2] >> 16 : ns2[i / 2] & 0xffffu;
-            if (s < ns)
+            const uint32_t lim = (i & 1) ? lim2[i / 2] >> 16 : lim2[i / 2] & 0xffffu;
+            if (s * 128 < lim)
                 __builtin_amdgcn_global_load_lds((const void*)(base + ((uint64_t)(idx[i] + (s << 3)) << 4)),
                                                  (__attribute__((address_space(3))) void*)(uintptr_t)(lds + i * 1024),
                                                  16, 0, 0);
@@ -543,7 +549,7 @@ __device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uin
     const uint32_t nst = (nbmax + 1) / 2;
     const uint32_t tmin = PADDED ? 0u : wave_min_uniform(total);
     DmaLinePieces dl;
-    dl.init(lines, kv.key, PADDED ? 64 * nb - 8 : len + (uint32_t)kLineBias);  // stage s is line s of the packet
+    dl.init(lines, kv.key, PADDED ? 64 * nb - 8 : len + (uint32_t)kLineBias, lds_wave);  // stage s: line s of the packet
     st.init();
     // message byte j is line byte j - rr (rr = r - 1): the carry is the dword before the stage's first one, its top
     // rr bytes the message bytes before the stage (at stage 0 the first rr prefix bytes); the slack byte, line byte 0

@@ -1147,8 +1147,16 @@ __global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_waves_per_
 // POOL: the wave-tasks are 64 consecutive pairs of the family's pooled order (k_pool_scatter): the claim -- filter,
 // prefix, m, k -- is per lane.  pool_queue: waves take wave-tasks from a queue (longest first) instead of the grid
 // stride.
+static constexpr uint32_t kPairRedBytes = 32;  // a wave's end-of-launch sums in LDS (direct-load kernels)
+// DSY_PAIR_WAVES5=1 builds the padded line-staged kernel for 5 waves per SIMD (<= 96 VGPRs; 5 workgroups x 4 x 8 KiB
+// fill the CU's LDS). Measured and dropped (profiles/waves5_ab_r5.json): at 96 VGPRs the task setup spills and the
+// launch ran 207-209 vs 202 us (headline), 108 vs 99 us (SHA-1 leg), 1064 vs 1050 us (config 5).
+#ifndef DSY_PAIR_WAVES5
+#define DSY_PAIR_WAVES5 0
+#endif
+static constexpr bool kPairWaves5 = DSY_PAIR_WAVES5;
 template <class H, int CHUNK, bool DMA, int DIAG = 0, bool POOL = false, bool PADDED = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))) k_pair_test(RespondLaunch L, const uint32_t* __restrict__ req_list,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kPairWaves5 && DMA && PADDED ? 5 : 4, 8))) k_pair_test(RespondLaunch L, const uint32_t* __restrict__ req_list,
                                                    uint32_t n_list, uint32_t fam) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dma_lds[];
     const uint64_t W = L.window;
@@ -1311,23 +1319,29 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8))
         }
     }
     // one set of atomics per workgroup (a contended atomic per wave-task would stall the next vmcnt wait of
-    // every wave behind it)
-    __shared__ unsigned long long red[3][4];
+    // every wave behind it); each wave's sums go through its own LDS stage buffer, free once its walk is done (no
+    // static LDS: five workgroups of 4 x 8 KiB fill a CU's 160 KiB exactly)
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
         acc_blocks += __shfl_xor(acc_blocks, d, 64);
         acc_bytes += __shfl_xor(acc_bytes, d, 64);
         acc_slots += __shfl_xor(acc_slots, d, 64);
     }
+    // (the direct-load kernels launch with kPairRedBytes of LDS per wave for this)
+    constexpr uint32_t kWaveLds = DMA ? DmaGeometry<2, 1>::kWaveBytes : kPairRedBytes;
     if (lane == 0) {
-        red[0][threadIdx.x >> 6] = acc_blocks;
-        red[1][threadIdx.x >> 6] = acc_bytes;
-        red[2][threadIdx.x >> 6] = acc_slots;
+        unsigned long long* red = (unsigned long long*)(dma_lds + (threadIdx.x >> 6) * kWaveLds);
+        red[0] = acc_blocks;
+        red[1] = acc_bytes;
+        red[2] = acc_slots;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned long long b = 0, y = 0, z = 0;
-        for (uint32_t wv = 0; wv < blockDim.x / 64; ++wv) b += red[0][wv], y += red[1][wv], z += red[2][wv];
+        for (uint32_t wv = 0; wv < blockDim.x / 64; ++wv) {
+            const unsigned long long* red = (const unsigned long long*)(dma_lds + wv * kWaveLds);
+            b += red[0], y += red[1], z += red[2];
+        }
         if (b) atomicAdd(counter(L.counters, kCntBlocks), b);
         if (y) atomicAdd(counter(L.counters, kCntBytes), y);
         if (z) atomicAdd(counter(L.counters, kCntSlots), z);
@@ -1382,7 +1396,8 @@ static hipError_t pair_test_family(const RespondLaunch& L, bool long_prefix, con
     auto kern = k_pair_test<H, CHUNK, false>;
     if constexpr (poolable)
         if (pooled) kern = k_pair_test<H, CHUNK, false, 0, true>;
-    launch_timed(kern, dim3((uint32_t)blocks), dim3(256), 0, L.stream, L.ev_start, L.ev_stop, L, list, n_list, fam);
+    launch_timed(kern, dim3((uint32_t)blocks), dim3(256), 4 * kPairRedBytes, L.stream, L.ev_start, L.ev_stop, L, list,
+                 n_list, fam);
     return hipGetLastError();
 }
 
