@@ -37,6 +37,18 @@ constexpr uint32_t kMaj = (0xF0 & 0xCC) | (0xF0 & 0xAA) | (0xCC & 0xAA);
 constexpr uint32_t kMd5G = (0xF0 & 0xAA) | (0xCC & ~0xAA & 0xFF);  // (b & d) | (c & ~d)
 constexpr uint32_t kMd5I = (0xCC ^ (0xF0 | (~0xAA & 0xFF))) & 0xFF; // c ^ (b | ~d)
 
+// x + K with K a 32-bit literal in the instruction (LIT) or left to the compiler
+template <bool LIT>
+__device__ __forceinline__ uint32_t addk(uint32_t x, uint32_t k) {
+    if constexpr (LIT) {
+        uint32_t r;
+        asm("v_add_u32_e32 %0, %1, %2" : "=v"(r) : "i"(k), "v"(x));
+        return r;
+    } else {
+        return x + k;
+    }
+}
+
 // --------------------------------------------------------------------------------------------------- MD5
 struct Md5 {
     static constexpr int kind = 0;
@@ -51,9 +63,14 @@ struct Md5 {
         h[0] = 0x67452301u; h[1] = 0xefcdab89u; h[2] = 0x98badcfeu; h[3] = 0x10325476u;
     }
 
+    // LIT: every round constant is a literal operand of one v_add_u32 (x + K) instead of an SGPR the compiler keeps
+    // for all 64 of them (and an add3 that reads it) -- the responder's wave-task loop (k_pair_test) needs those
+    // SGPRs for its task state, which otherwise spills into VGPR lanes (v_writelane / v_readlane, VALU work on every
+    // wave-task).  Same instruction count per step.
+    template <bool LIT = false>
     __device__ __forceinline__ void compress(const uint32_t* m) {
         uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
-#define DSY_MD5_STEP(f, a, b, c, d, x, k, s) a = b + rotl32(a + (f) + (x) + (k), s)
+#define DSY_MD5_STEP(f, a, b, c, d, x, k, s) a = b + rotl32(a + (f) + addk<LIT>((x), (k)), s)
         // round 1: F = (b & c) | (~b & d)
         DSY_MD5_STEP(bop3<kCh>(b, c, d), a, b, c, d, m[0], 0xd76aa478u, 7);
         DSY_MD5_STEP(bop3<kCh>(a, b, c), d, a, b, c, m[1], 0xe8c7b756u, 12);
@@ -63,6 +80,7 @@ struct Md5 {
         DSY_MD5_STEP(bop3<kCh>(a, b, c), d, a, b, c, m[5], 0x4787c62au, 12);
         DSY_MD5_STEP(bop3<kCh>(d, a, b), c, d, a, b, m[6], 0xa8304613u, 17);
         DSY_MD5_STEP(bop3<kCh>(c, d, a), b, c, d, a, m[7], 0xfd469501u, 22);
+        if constexpr (LIT) __builtin_amdgcn_sched_barrier(0);  // (no hoisting of the next x + K adds)
         DSY_MD5_STEP(bop3<kCh>(b, c, d), a, b, c, d, m[8], 0x698098d8u, 7);
         DSY_MD5_STEP(bop3<kCh>(a, b, c), d, a, b, c, m[9], 0x8b44f7afu, 12);
         DSY_MD5_STEP(bop3<kCh>(d, a, b), c, d, a, b, m[10], 0xffff5bb1u, 17);
@@ -71,6 +89,7 @@ struct Md5 {
         DSY_MD5_STEP(bop3<kCh>(a, b, c), d, a, b, c, m[13], 0xfd987193u, 12);
         DSY_MD5_STEP(bop3<kCh>(d, a, b), c, d, a, b, m[14], 0xa679438eu, 17);
         DSY_MD5_STEP(bop3<kCh>(c, d, a), b, c, d, a, m[15], 0x49b40821u, 22);
+        if constexpr (LIT) __builtin_amdgcn_sched_barrier(0);  // (no hoisting of the next x + K adds)
         // round 2: G = (b & d) | (c & ~d)
         DSY_MD5_STEP(bop3<kMd5G>(b, c, d), a, b, c, d, m[1], 0xf61e2562u, 5);
         DSY_MD5_STEP(bop3<kMd5G>(a, b, c), d, a, b, c, m[6], 0xc040b340u, 9);
@@ -80,6 +99,7 @@ struct Md5 {
         DSY_MD5_STEP(bop3<kMd5G>(a, b, c), d, a, b, c, m[10], 0x02441453u, 9);
         DSY_MD5_STEP(bop3<kMd5G>(d, a, b), c, d, a, b, m[15], 0xd8a1e681u, 14);
         DSY_MD5_STEP(bop3<kMd5G>(c, d, a), b, c, d, a, m[4], 0xe7d3fbc8u, 20);
+        if constexpr (LIT) __builtin_amdgcn_sched_barrier(0);  // (no hoisting of the next x + K adds)
         DSY_MD5_STEP(bop3<kMd5G>(b, c, d), a, b, c, d, m[9], 0x21e1cde6u, 5);
         DSY_MD5_STEP(bop3<kMd5G>(a, b, c), d, a, b, c, m[14], 0xc33707d6u, 9);
         DSY_MD5_STEP(bop3<kMd5G>(d, a, b), c, d, a, b, m[3], 0xf4d50d87u, 14);
@@ -88,6 +108,7 @@ struct Md5 {
         DSY_MD5_STEP(bop3<kMd5G>(a, b, c), d, a, b, c, m[2], 0xfcefa3f8u, 9);
         DSY_MD5_STEP(bop3<kMd5G>(d, a, b), c, d, a, b, m[7], 0x676f02d9u, 14);
         DSY_MD5_STEP(bop3<kMd5G>(c, d, a), b, c, d, a, m[12], 0x8d2a4c8au, 20);
+        if constexpr (LIT) __builtin_amdgcn_sched_barrier(0);  // (no hoisting of the next x + K adds)
         // round 3: H = b ^ c ^ d
         DSY_MD5_STEP(bop3<kXor3>(b, c, d), a, b, c, d, m[5], 0xfffa3942u, 4);
         DSY_MD5_STEP(bop3<kXor3>(a, b, c), d, a, b, c, m[8], 0x8771f681u, 11);
@@ -97,6 +118,7 @@ struct Md5 {
         DSY_MD5_STEP(bop3<kXor3>(a, b, c), d, a, b, c, m[4], 0x4bdecfa9u, 11);
         DSY_MD5_STEP(bop3<kXor3>(d, a, b), c, d, a, b, m[7], 0xf6bb4b60u, 16);
         DSY_MD5_STEP(bop3<kXor3>(c, d, a), b, c, d, a, m[10], 0xbebfbc70u, 23);
+        if constexpr (LIT) __builtin_amdgcn_sched_barrier(0);  // (no hoisting of the next x + K adds)
         DSY_MD5_STEP(bop3<kXor3>(b, c, d), a, b, c, d, m[13], 0x289b7ec6u, 4);
         DSY_MD5_STEP(bop3<kXor3>(a, b, c), d, a, b, c, m[0], 0xeaa127fau, 11);
         DSY_MD5_STEP(bop3<kXor3>(d, a, b), c, d, a, b, m[3], 0xd4ef3085u, 16);
@@ -105,6 +127,7 @@ struct Md5 {
         DSY_MD5_STEP(bop3<kXor3>(a, b, c), d, a, b, c, m[12], 0xe6db99e5u, 11);
         DSY_MD5_STEP(bop3<kXor3>(d, a, b), c, d, a, b, m[15], 0x1fa27cf8u, 16);
         DSY_MD5_STEP(bop3<kXor3>(c, d, a), b, c, d, a, m[2], 0xc4ac5665u, 23);
+        if constexpr (LIT) __builtin_amdgcn_sched_barrier(0);  // (no hoisting of the next x + K adds)
         // round 4: I = c ^ (b | ~d)
         DSY_MD5_STEP(bop3<kMd5I>(b, c, d), a, b, c, d, m[0], 0xf4292244u, 6);
         DSY_MD5_STEP(bop3<kMd5I>(a, b, c), d, a, b, c, m[7], 0x432aff97u, 10);
@@ -114,6 +137,7 @@ struct Md5 {
         DSY_MD5_STEP(bop3<kMd5I>(a, b, c), d, a, b, c, m[3], 0x8f0ccc92u, 10);
         DSY_MD5_STEP(bop3<kMd5I>(d, a, b), c, d, a, b, m[10], 0xffeff47du, 15);
         DSY_MD5_STEP(bop3<kMd5I>(c, d, a), b, c, d, a, m[1], 0x85845dd1u, 21);
+        if constexpr (LIT) __builtin_amdgcn_sched_barrier(0);  // (no hoisting of the next x + K adds)
         DSY_MD5_STEP(bop3<kMd5I>(b, c, d), a, b, c, d, m[8], 0x6fa87e4fu, 6);
         DSY_MD5_STEP(bop3<kMd5I>(a, b, c), d, a, b, c, m[15], 0xfe2ce6e0u, 10);
         DSY_MD5_STEP(bop3<kMd5I>(d, a, b), c, d, a, b, m[6], 0xa3014314u, 15);
@@ -144,6 +168,7 @@ struct Sha1 {
         h[0] = 0x67452301u; h[1] = 0xefcdab89u; h[2] = 0x98badcfeu; h[3] = 0x10325476u; h[4] = 0xc3d2e1f0u;
     }
 
+    template <bool LIT = false>
     __device__ __forceinline__ void compress(const uint32_t* m) {
         uint32_t w[16];
 #pragma unroll
@@ -197,6 +222,7 @@ struct Sha256 {
         h[4] = 0x510e527fu; h[5] = 0x9b05688cu; h[6] = 0x1f83d9abu; h[7] = 0x5be0cd19u;
     }
 
+    template <bool LIT = false>
     __device__ __forceinline__ void compress(const uint32_t* m) {
         uint32_t w[16];
 #pragma unroll

@@ -592,7 +592,7 @@ __device__ __forceinline__ void hash_key_dma_lines(const KeyView& kv, H& st, uin
                 const uint32_t o0 = b * 64;
                 if (PADDED) finish_block_padded<H>(x, total, b + 1 == nb);
                 else finish_block<H>(x, o0, total, b + 1 == nb, o0 + 64 <= tmin);
-                if (MODE != 2) st.compress(x);
+                if (MODE != 2) st.template compress<true>(x);
                 else st.h[0] ^= x[0] ^ x[5] ^ x[10] ^ x[15];
             }
             // keep block 1's message words from being formed while block 0 compresses (register pressure: the
