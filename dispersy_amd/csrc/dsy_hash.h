@@ -298,6 +298,7 @@ struct Sha512T {
     }
 
     // m: 32 big-endian-decoded 32-bit words (word 2i is the high half of 64-bit word i)
+    template <bool LIT = false>  // (no literal form: the 64-bit constants are kept by the compiler)
     __device__ __forceinline__ void compress(const uint32_t* m) {
         uint64_t w[16];
 #pragma unroll

@@ -89,7 +89,7 @@ __device__ __forceinline__ void hash_key_generic(const KeyView& kv, H& st) {
     uint32_t w[H::words];
     for (uint32_t b = 0; b < nb; ++b) {
         message_block<H>(kv, b, nb, w);
-        st.compress(w);
+        st.template compress<true>(w);
     }
 }
 
@@ -161,7 +161,7 @@ __device__ __forceinline__ void hash_key_short_prefix(const KeyView& kv, H& st) 
                 w[15] = (uint32_t)(bits >> 32);
             }
         }
-        st.compress(w);
+        st.template compress<true>(w);
     }
 }
 
@@ -457,7 +457,7 @@ __device__ __forceinline__ void hash_key_dma(const KeyView& kv, H& st, uint8_t* 
                 const uint32_t o0 = b * 64;
                 if (b == 0 && r) w[0] = (w[0] & ~low_bytes_mask(r)) | preword;
                 finish_block<H>(w, o0, total, b + 1 == nb, o0 + 64 <= tmin);
-                st.compress(w);
+                st.template compress<true>(w);
             }
         }
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this stage's reads retire before its buffer refills
@@ -516,7 +516,7 @@ __device__ __forceinline__ void hash_key_dma_reg(const KeyView& kv, H& st, uint8
                 const uint32_t o0 = b * 64;
                 if (b == 0 && r) x[0] = (x[0] & ~low_bytes_mask(r)) | preword;
                 finish_block<H>(x, o0, total, b + 1 == nb, o0 + 64 <= tmin);
-                if (MODE != 2) st.compress(x);
+                if (MODE != 2) st.template compress<true>(x);
                 else st.h[0] ^= x[0] ^ x[5] ^ x[10] ^ x[15];
             }
         }
