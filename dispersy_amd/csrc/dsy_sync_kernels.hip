@@ -824,7 +824,10 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
 // is committed by k_compact, since the other parts read it while this launch runs.  (A config 5 claim whose filter
 // covers its 10^5-10^6 rows walks them in 2^18-pair windows: one workgroup per claim left the chip idle, 1-2 ms per
 // window.)
-static constexpr uint64_t kBulkChunk = (uint64_t)kFillThreads * 8;
+#ifndef DSY_BULK_UNROLL
+#define DSY_BULK_UNROLL 16  // pairs per thread of a split window's part (8: 2048-pair parts)
+#endif
+static constexpr uint64_t kBulkChunk = (uint64_t)kFillThreads * DSY_BULK_UNROLL;
 // k_fill: an enumerating claim with at most this many candidates left fills a window of >= 2 parts part by part
 static constexpr uint64_t kSliceCands = 2048;
 
