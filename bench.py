@@ -189,6 +189,11 @@ def parse():
     ap.add_argument("--pipeline", type=int, default=3,
                     help="responder legs: batches in flight (dsy_sync_respond_submit / _wait, at most 3); 1 one at a time "
                          "(dsy_sync_respond_dev)")
+    ap.add_argument("--pipeline5", type=int, default=1,
+                    help="config 5 (heavy tail): batches in flight. Default 1: its calls walk 9 windows each, and "
+                         "batches in flight interleave their windows on the stream (each window waits for the host "
+                         "to read the previous one's flags), which measured 1-2 %% slower than one call at a time "
+                         "(profiles/bulk_parts_ab_r5.json: ms_per_step 3 in flight vs serial_ms_per_step)")
     ap.add_argument("--window", type=int, default=0, help="cap on the responder's window (pairs per claim; 0: default)")
     ap.add_argument("--sim-peers", type=int, default=1_000_000, help="config 3 gossip simulator peers (0: skip)")
     ap.add_argument("--sim-universe", type=int, default=10_000)
@@ -1528,7 +1533,7 @@ def heavy_tail(args, ctx, lib, dev, rank, world, dist):
     if args.window:
         ctx.set_window(args.window)
     batches = Batches(lib, ctx, store, reqs, R, d_filters.data_ptr(), metas, 1, G_MAX, args.byte_limit)
-    pipe = args.pipeline
+    pipe = args.pipeline5
     batches.run(2, pipe)
     steps = max(3, args.steps // 4)
     ctx.synchronize()
