@@ -146,6 +146,8 @@ struct dsy_ctx {
     // (1024 workgroups' atomics on the same ~20 bin cursors), 0.149 -> 0.157 ms per step; MD5 headline 0.28 -> 0.30
     uint32_t pool_kinds = 0;
     int pool_queue = 0;
+    int pool_scan = 0;   // DSY_POOL_SCAN=1: pooled pairs placed by the per-(claim, bin) scan (k_pool_scan), not the
+                         // scatter's atomics -- measured slower (profiles/pool_scan_ab_r5.json)
     int pool_deal = 0;   // DSY_POOL_DEAL: the pooled hashing's resident-grid deal (k_pair_test<POOL>)
     int pair_prio = 1;   // DSY_PAIR_PRIO: k_pair_test raises the wave priority of long wave-tasks (0 off)
     int bulk_zero = 1;   // DSY_BULK_ZERO=0: the calls do not zero their split-window sort state (diagnostic)
@@ -536,6 +538,7 @@ int dsy_ctx_create(int device, dsy_ctx** out) {
     if (const char* v = getenv("DSY_POOL")) c->pool_kinds = (uint32_t)strtoul(v, nullptr, 0);
     if (const char* v = getenv("DSY_POOL_QUEUE")) c->pool_queue = atoi(v);
     if (const char* v = getenv("DSY_POOL_DEAL")) c->pool_deal = atoi(v);
+    if (const char* v = getenv("DSY_POOL_SCAN")) c->pool_scan = atoi(v);
     if (const char* v = getenv("DSY_PAIR_PRIO")) c->pair_prio = atoi(v);
     if (const char* v = getenv("DSY_BULK_ZERO")) c->bulk_zero = atoi(v);
     if (const char* v = getenv("DSY_PAIR_DIRECT")) c->direct_kinds = (uint32_t)strtoul(v, nullptr, 0);
@@ -2265,8 +2268,12 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const Clai
         for (int f = 0; f < kFamilies; ++f)
             if (!fam_members[f].empty() && ((c->pool_kinds >> (f / 6)) & 1u)) pool_mask |= 1u << f;
     void* d_pool_counts = nullptr;
+    void* d_pool_tab = nullptr;
     if (pool_mask) {
         if ((rc = ws_get(w, "pool_counts", sizeof(PoolCounts), &d_pool_counts))) return rc;
+        // the per-(claim, bin) counts and offsets: every row a pooled window reads is written by that window's k_fill
+        if (c->pool_scan && (rc = ws_get(w, "pool_tab", (size_t)std::max<uint32_t>(R, 1) * 2 * kPoolBins * 4, &d_pool_tab)))
+            return rc;
         // every call starts from zero counts (k_pair_test<POOL> keeps them zero between windows; a call that ended
         // early may have left some)
         HIP_TRY(hipMemsetAsync(d_pool_counts, 0, sizeof(PoolCounts), st));
@@ -2376,6 +2383,8 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const Clai
     L.pool_mask = pool_mask;
     L.pool_queue = c->pool_queue;
     L.pool_deal = c->pool_deal;
+    L.pool_scan = c->pool_scan && d_pool_tab;
+    L.pool_tab = (uint32_t*)d_pool_tab;
     L.pair_prio = c->pair_prio;
     L.bulk_zero = c->bulk_zero;
     L.pool_counts = (PoolCounts*)d_pool_counts;

@@ -46,6 +46,7 @@ struct PoolCounts {
     uint32_t cur[kFamilies][kPoolBins];
     uint32_t total[kFamilies];  // the family's pooled pairs in this window (k_pool_scatter)
     uint32_t next[kFamilies];   // wave-task queue head (k_pair_test<POOL> with pool_queue)
+    uint32_t split[kFamilies];  // 1: a claim of the family filled a split window (its pairs have no pool_tab rows)
 };
 
 // A store row's packet in the line copy: starts kLineBias (dsy_message.h) bytes into a 128-byte line of
@@ -252,6 +253,9 @@ struct RespondLaunch {
                               // a diagnostic of the state k_compact leaves between calls)
     PoolCounts* pool_counts;  // device, zero outside a window (k_pair_test<POOL> clears its family's)
     PoolTask* pool;           // device [pool]: the pooled order of the family being hashed
+    uint32_t* pool_tab;       // device [2][R][kPoolBins] (pool_scan): k_fill's per-(claim, bin) counts and bin starts;
+                              // k_pool_scan turns the starts into offsets in the family's pooled order
+    int pool_scan;            // pooled families place pairs by the per-(claim, bin) scan, not by scatter atomics
     hipStream_t stream;
 };
 

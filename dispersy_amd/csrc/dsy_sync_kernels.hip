@@ -694,6 +694,7 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
                 if (ph) atomicAdd(&ph[i], sh[i]);
             }
         if (threadIdx.x == 0 && s0 == 0) S->sort_later = 1;
+        if (ph && threadIdx.x == 0) L.pool_counts->split[fam_s] = 1;  // no pool_tab rows: the scatter's atomics
         if (L.fill_clock && threadIdx.x == 0 && s0 == 0) {
             uint64_t* fc = L.fill_clock + (uint64_t)a_slot * 4;
             fc[0] = clk0;
@@ -745,13 +746,18 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
     }
     __syncthreads();
     const uint32_t fam = family_id(q.hash_kind, q.chunk_bytes, q.prefix_len);
-    if ((L.pool_mask >> fam) & 1u) {  // a pooled family: the window's counts go into the family's histogram too
+    const bool pooled = (L.pool_mask >> fam) & 1u;
+    if (pooled) {  // a pooled family: the window's counts go into the family's histogram too
         uint32_t* ph = L.pool_counts->hist[fam];
-        for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads)
+        uint32_t* tc = L.pool_tab + (uint64_t)a_slot * kSortBins;  // (pool_scan) the claim's counts, every bin
+        for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads) {
             if (hist[i]) atomicAdd(&ph[i], hist[i]);
+            if (L.pool_scan) tc[i] = hist[i];
+        }
         __syncthreads();
     }
     if (may_split && filled > kSplitSortMin) {
+        if (pooled && threadIdx.x == 0) L.pool_counts->split[fam] = 1;
         // a big window this one workgroup selected (a claim whose global times hold 10^4-10^5 rows each, config
         // 5's Zipf): its pairs are placed by k_fill_sort's workgroups, kBulkChunk each, from this histogram
         uint32_t* gh = L.bulk_hist + (uint64_t)a_slot * kSortBins;
@@ -784,6 +790,10 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
         }
     }
     __syncthreads();
+    if (pooled && L.pool_scan) {  // the claim's bin starts in its task order (k_pool_scan makes them offsets)
+        uint32_t* ts = L.pool_tab + ((uint64_t)L.R + a_slot) * kSortBins;
+        for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads) ts[i] = hist[i];
+    }
     PairTask* task = L.task + (uint64_t)a_slot * W;
     if (in_regs) {
 #pragma unroll
@@ -813,6 +823,12 @@ __device__ __forceinline__ void fill_claim(const RespondLaunch& L, uint32_t a_sl
         fc[2] = __builtin_amdgcn_s_memtime();
         fc[3] = clk_start;  // k_fill_first: before the claim's host reads and plan (k_fill: == clk0)
     }
+}
+
+// a pooled claim without a window this round: its pool_tab counts row reads zero in k_pool_scan
+__device__ __forceinline__ void pool_row_zero(const RespondLaunch& L, uint32_t a_slot, const DevRequest& q) {
+    if (!L.pool_scan || !((L.pool_mask >> family_id(q.hash_kind, q.chunk_bytes, q.prefix_len)) & 1u)) return;
+    for (uint32_t i = threadIdx.x; i < kSortBins; i += blockDim.x) L.pool_tab[(uint64_t)a_slot * kSortBins + i] = 0;
 }
 
 // A split window: a claim that keeps every live row of a span (a scan with modulo 1, ASC or DESC) and has at least W
@@ -889,6 +905,7 @@ __device__ __forceinline__ void fill_bulk_part(const RespondLaunch& L, uint32_t 
             if (ph) atomicAdd(&ph[i], hist[i]);
         }
     if (part == 0 && threadIdx.x == 0) {
+        if (ph) L.pool_counts->split[fam] = 1;  // no pool_tab rows: the scatter's atomics
         S->n_window = nw;
         S->cand_next = c + nw;
         S->commit = 1;
@@ -986,6 +1003,63 @@ __global__ void __launch_bounds__(kFillThreads) k_fill_sort(RespondLaunch L) {
 // bin.  Workgroup (0, 0) also publishes the total and resets the wave-task queue.
 static constexpr uint64_t kPoolPart = 1024;
 
+// The per-(claim, bin) exclusive scan (L.pool_scan): k_fill left every listed claim's block-count histogram (counts
+// row) and its bins' starts in its own task order (starts row) in L.pool_tab; here bin b's column of counts is
+// scanned over the list's claims, and every nonzero entry's starts-row word becomes (offset of the claim's first pair
+// of bin b among the family's pairs of bin b) - (its start in the claim's task order).  k_pool_scatter then places
+// task[j] at bin_start[b] + that word + j: no atomics, no cursor contention.  Workgroup g takes bins 64 g .. 64 g + 63
+// (lane = bin, coalesced 256-byte row pieces); its 16 waves take consecutive ranges of the list.  A family with a
+// split window (k_fill_sort's order, no rows) keeps the scatter's atomics: both kernels read the same flag.
+__global__ void __launch_bounds__(1024) k_pool_scan(RespondLaunch L, const uint32_t* __restrict__ list, uint32_t n_list,
+                                                    uint32_t fam) {
+    __shared__ uint32_t part[16][64];
+    if (L.pool_counts->split[fam]) return;
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t bin = blockIdx.x * 64 + lane;
+    const uint32_t per = (n_list + 15) / 16;
+    const uint32_t x0 = min(wv * per, n_list), x1 = min(x0 + per, n_list);
+    const uint32_t* tc = L.pool_tab + bin;
+    uint32_t* ts = L.pool_tab + (uint64_t)L.R * kSortBins + bin;
+    // 64 rows at a time: lane i holds row c0 + i's window slot, every row's count is one load at a wave-uniform row
+    // address, all 64 in flight together (a claim without a window this round has a zero counts row: k_fill)
+    auto load = [&](uint32_t c0, uint32_t* cnt) -> uint32_t {
+        const uint32_t my = c0 + lane < x1 ? list[c0 + lane] : ~0u;
+#pragma unroll
+        for (int k = 0; k < 64; ++k) {
+            const uint32_t a = __builtin_amdgcn_readlane(my, k);
+            cnt[k] = a != ~0u ? tc[(uint64_t)a * kSortBins] : 0u;
+        }
+        return my;
+    };
+    uint32_t cnt[64], my = ~0u, sum = 0;
+    const bool one = x1 - x0 <= 64;  // (the common case, <= 1024 claims: the counts stay in registers)
+    for (uint32_t c0 = x0; c0 < x1; c0 += 64) {
+        my = load(c0, cnt);
+#pragma unroll
+        for (int k = 0; k < 64; ++k) sum += cnt[k];
+    }
+    part[wv][lane] = sum;
+    __syncthreads();
+    uint32_t off = 0;
+    for (uint32_t v = 0; v < wv; ++v) off += part[v][lane];
+    for (uint32_t c0 = x0; c0 < x1; c0 += 64) {
+        if (!one) my = load(c0, cnt);
+#pragma unroll
+        for (int h = 0; h < 64; h += 32) {  // 32 starts loaded, then their offsets stored: no store between loads
+            uint32_t st[32];
+#pragma unroll
+            for (int k = 0; k < 32; ++k)
+                st[k] = cnt[h + k] ? ts[(uint64_t)__builtin_amdgcn_readlane(my, h + k) * kSortBins] : 0u;
+#pragma unroll
+            for (int k = 0; k < 32; ++k)
+                if (cnt[h + k]) {
+                    ts[(uint64_t)__builtin_amdgcn_readlane(my, h + k) * kSortBins] = off - st[k];
+                    off += cnt[h + k];
+                }
+        }
+    }
+}
+
 __global__ void __launch_bounds__(256) k_pool_scatter(RespondLaunch L, const uint32_t* __restrict__ list, uint32_t fam) {
     __shared__ uint32_t start[kSortBins];
     __shared__ uint32_t lh[kSortBins];
@@ -1007,6 +1081,23 @@ __global__ void __launch_bounds__(256) k_pool_scatter(RespondLaunch L, const uin
     __syncthreads();
     const DevRequest& q = L.reqs[r];
     const PairTask* task = L.task + (uint64_t)a_slot * W;
+    if (L.pool_scan && !pc->split[fam]) {  // k_pool_scan's offsets: pair j of bin b goes to start[b] + delta[b] + j
+        const uint32_t* delta = L.pool_tab + ((uint64_t)L.R + a_slot) * kSortBins;
+        const uint64_t cap = (uint64_t)L.n_act * W;
+        for (uint64_t base = base0; base < n; base += (uint64_t)gridDim.y * kPoolPart)
+            for (uint64_t j = base + threadIdx.x; j < n && j < base + kPoolPart; j += 256) {
+                const PairTask tk = task[j];
+                const uint32_t b = sort_bin(q, tk.len);
+                PoolTask p;
+                p.line = (uint32_t)(tk.off >> 7);  // off = line * 128 + kLineBias
+                p.len = tk.len;
+                p.a_slot = a_slot;
+                p.slot = tk.slot;
+                const uint32_t pos = start[b] + delta[b] + (uint32_t)j;
+                if (pos < cap) L.pool[pos] = p;  // (always: the counts are this window's pairs)
+            }
+        return;
+    }
     for (uint64_t base = base0; base < n; base += (uint64_t)gridDim.y * kPoolPart) {
         const uint64_t cnt = n - base < kPoolPart ? n - base : kPoolPart;
         constexpr int kU = (int)(kPoolPart / 256);
@@ -1052,6 +1143,7 @@ __global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_waves_per_
     ReqState* S = &L.state[r];
     if (S->done) {
         if (part == 0 && threadIdx.x == 0) S->n_window = 0;
+        if (part == 0) pool_row_zero(L, a_slot, L.reqs[r]);
         return;
     }
     const Plan* plans = L.plans + (uint64_t)r * L.J;
@@ -1133,6 +1225,7 @@ __global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_waves_per_
     ReqState* S = &L.state[r];
     if (sst.done) {
         if (threadIdx.x == 0) S[0] = sst;  // n_window = 0
+        pool_row_zero(L, a_slot, sq);
         return;
     }
     if (threadIdx.x == 0) S[0] = sst;  // the cursor fields are rewritten by fill_claim's thread 0 below
@@ -1171,6 +1264,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kPairW
         if (blockIdx.x == 0) {  // the family's histogram and cursors start the next window at zero (k_fill adds)
             for (uint32_t i = threadIdx.x; i < kSortBins; i += blockDim.x)
                 L.pool_counts->hist[fam][i] = L.pool_counts->cur[fam][i] = 0;
+            if (threadIdx.x == 0) L.pool_counts->split[fam] = 0;
         }
     } else {
         // chunks per claim: the window's longest claim (k_fill), not W / 64 -- a claim of ~1000 pairs in a 4096-pair
@@ -1371,6 +1465,8 @@ static hipError_t pair_test_family(const RespondLaunch& L, bool long_prefix, con
             // one workgroup per claim for windows of <= 16 parts (the common 4096-pair window: 1024 claims, 1024
             // workgroups), more for the big windows of a few long claims
             const uint32_t parts = (uint32_t)std::max<uint64_t>(1, L.window / (16 * kPoolPart));
+            if (L.pool_scan)
+                hipLaunchKernelGGL(k_pool_scan, dim3(kPoolBins / 64), dim3(1024), 0, L.stream, L, list, n_list, fam);
             hipLaunchKernelGGL(k_pool_scatter, dim3(n_list, parts), dim3(256), 0, L.stream, L, list, fam);
         }
     } else {

@@ -3,8 +3,10 @@ claim's block-count histogram into its family's, k_pool_scatter orders every act
 longest-first pool, and k_pair_test<POOL> reads the claim (filter, prefix, m, k) per lane.  A context created with
 DSY_POOL=7 pools the MD5, SHA-1 and SHA-256 families; its answers must equal the sqlite + hashlib oracle's
 (oracle/sync_ref.respond_lists = community.py:2746-2811 + :2555-2567) for mixed families, prefixes of 0-5 bytes,
-capped windows (the pool is rebuilt every window), a never-pooled SHA-512 family beside the pooled ones, and the
-resident-grid deal (DSY_POOL_DEAL)."""
+capped windows (the pool is rebuilt every window), a never-pooled SHA-512 family beside the pooled ones, the
+resident-grid deal (DSY_POOL_DEAL), and both placements: the scatter's atomics (the default) and the per-(claim, bin)
+scan (k_pool_scan, DSY_POOL_SCAN=1).  16384-pair windows give the modulo-1 claims split windows (k_fill_sort's order,
+no per-claim rows), for which the scan falls back to the atomics."""
 import numpy as np
 import pytest
 
@@ -19,17 +21,18 @@ from test_respond_scale_gpu import METAS, build
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["0", "1"], ids=["stride", "deal"])
+@pytest.fixture(params=[("0", "0"), ("1", "0"), ("0", "1")], ids=["stride", "deal", "scan"])
 def pooled_ctx(request, monkeypatch):
     monkeypatch.setenv("DSY_POOL", "7")
-    monkeypatch.setenv("DSY_POOL_DEAL", request.param)
+    monkeypatch.setenv("DSY_POOL_DEAL", request.param[0])
+    monkeypatch.setenv("DSY_POOL_SCAN", request.param[1])
     ctx = _native.Context(0)  # the knobs are read when a ctx is created
     yield ctx
     ctx.close()
 
 
 @pytest.mark.parametrize("one_byte", [False, True], ids=["prefixes0-5", "prefix1"])
-@pytest.mark.parametrize("window", [0, 256])
+@pytest.mark.parametrize("window", [0, 256, 16384])
 @pytest.mark.parametrize("skew", [False, "dense"])
 def test_pooled_families_vs_oracle(pooled_ctx, skew, window, one_byte):
     """one_byte: every claim's prefix is 1 byte (every reference claim), so the pooled MD5 / SHA-1 families hash the
