@@ -854,6 +854,15 @@ __device__ __forceinline__ bool bulk_window(const RespondLaunch& L, const DevReq
            p.ncand - S.cand >= 2 * kBulkChunk;
 }
 
+// A split window's pair t is candidate win_cand + t of the plan's span: its store row is arithmetic (the span's
+// candidates are consecutive live rows), so the fill writes no per-pair row / offset / length for it -- k_fill_sort
+// and k_compact recompute them from the row records.
+__device__ __forceinline__ uint64_t bulk_row(const RespondLaunch& L, const Plan& p, uint64_t c0, uint64_t t) {
+    const uint64_t ci = c0 + t;
+    const uint64_t lr = p.a + (p.dir == DSY_DESC ? p.ncand - 1 - ci : ci);
+    return L.st.live_row ? L.st.live_row[lr] : lr;
+}
+
 __device__ __forceinline__ uint32_t sort_bin(const DevRequest& q, uint32_t len) {
     const uint32_t blk = q.hash_kind >= DSY_SHA384 ? 128u : 64u, lenb = q.hash_kind >= DSY_SHA384 ? 16u : 8u;
     return (uint32_t)kSortBins - 1u - min(n_blocks(q.prefix_len + len, blk, lenb), (uint32_t)kSortBins - 1);
@@ -870,31 +879,18 @@ __device__ __forceinline__ void fill_bulk_part(const RespondLaunch& L, uint32_t 
     uint64_t* mask = L.miss_mask + (uint64_t)a_slot * (W / 64) + base / 64;
     for (uint64_t w = threadIdx.x; w < (n + 63) / 64; w += kFillThreads) mask[w] = 0;
     for (uint32_t i = threadIdx.x; i < kSortBins; i += kFillThreads) hist[i] = 0;
-    uint64_t* out = L.pair_row + (uint64_t)a_slot * W;
-    uint64_t* out_off = L.pair_off + (uint64_t)a_slot * W;
-    uint32_t* out_len = L.pair_len + (uint64_t)a_slot * W;
     const RowRec* __restrict__ rec = L.st.rec;
     constexpr int kU = (int)(kBulkChunk / kFillThreads);
-    uint64_t row[kU];
+    uint32_t len[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
         const uint64_t t = threadIdx.x + (uint64_t)kFillThreads * u;
-        const uint64_t ci = c + base + (t < n ? t : 0);
-        const uint64_t lr = p.a + (p.dir == DSY_DESC ? p.ncand - 1 - ci : ci);
-        row[u] = L.st.live_row ? L.st.live_row[lr] : lr;
+        len[u] = t < n ? rec[bulk_row(L, p, c, base + t)].len : 0u;  // (only the histogram: bulk_row)
     }
     __syncthreads();  // hist cleared
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-        const uint64_t t = threadIdx.x + (uint64_t)kFillThreads * u;
-        if (t < n) {
-            const RowRec rr = rec[row[u]];
-            out[base + t] = row[u];
-            out_off[base + t] = rr.off;
-            out_len[base + t] = rr.len;
-            atomicAdd(&hist[sort_bin(q, rr.len)], 1u);
-        }
-    }
+    for (int u = 0; u < kU; ++u)
+        if (threadIdx.x + (uint64_t)kFillThreads * u < n) atomicAdd(&hist[sort_bin(q, len[u])], 1u);
     __syncthreads();
     uint32_t* gh = L.bulk_hist + (uint64_t)a_slot * kSortBins;
     const uint32_t fam = family_id(q.hash_kind, q.chunk_bytes, q.prefix_len);
@@ -961,10 +957,15 @@ __global__ void __launch_bounds__(kFillThreads) k_fill_sort(RespondLaunch L) {
     const uint64_t* off_w = L.pair_off + (uint64_t)a_slot * W + base;
     constexpr int kU = (int)(kBulkChunk / kFillThreads);
     uint32_t len[kU];
+    // a split window (fill_bulk_part): the pairs' rows are arithmetic and their records are re-read (the offsets at
+    // placement, from L2)
+    const bool bulk = S->commit;
+    const Plan bp = bulk ? L.plans[(uint64_t)r * L.J + S->win_meta] : Plan{};
+    const uint64_t c0 = S->win_cand;
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
         const uint64_t t = threadIdx.x + (uint64_t)kFillThreads * u;
-        len[u] = t < n ? len_w[t] : 0u;
+        len[u] = t < n ? (bulk ? L.st.rec[bulk_row(L, bp, c0, base + t)].len : len_w[t]) : 0u;
     }
     __syncthreads();  // starts scanned
 #pragma unroll
@@ -981,7 +982,7 @@ __global__ void __launch_bounds__(kFillThreads) k_fill_sort(RespondLaunch L) {
         const uint64_t t = threadIdx.x + (uint64_t)kFillThreads * u;
         if (t < n) {
             PairTask tk;
-            tk.off = off_w[t];
+            tk.off = bulk ? L.st.rec[bulk_row(L, bp, c0, base + t)].off : off_w[t];
             tk.len = len[u];
             tk.slot = (uint32_t)(base + t);
             // the position lies in [0, nw) when bulk_hist holds exactly this window's counts; a stale count (state a
@@ -1602,6 +1603,8 @@ __global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
     const uint64_t* mask_w = L.miss_mask + (uint64_t)a_slot * (W / 64);
     const uint32_t* len_w = L.pair_len + (uint64_t)a_slot * W;
     const uint64_t* row_w = L.pair_row + (uint64_t)a_slot * W;
+    const bool bulk = S->commit;
+    const Plan bp = bulk ? L.plans[(uint64_t)r * L.J + S->win_meta] : Plan{};
     const uint64_t nw = (n + 63) / 64;
     constexpr uint32_t kPer = 4;  // words per lane per round
     for (uint64_t wb = 0; wb < nw && !done; wb += 64 * kPer) {
@@ -1658,8 +1661,17 @@ __global__ void __launch_bounds__(64) k_compact(RespondLaunch L) {
                 }
                 t = (wb + kPer * lo + u_sel) * 64 + (miss ? select_bit(wsel, kk) : 0u);
             }
-            const int64_t len = miss ? (int64_t)len_w[t] : 0;
-            const uint64_t row = miss ? row_w[t] : 0;
+            int64_t len = 0;
+            uint64_t row = 0;
+            if (miss) {
+                if (bulk) {  // a split window: the row is arithmetic (fill_bulk_part wrote no pair arrays)
+                    row = bulk_row(L, bp, S->win_cand, t);
+                    len = (int64_t)L.st.rec[row].len;
+                } else {
+                    len = (int64_t)len_w[t];
+                    row = row_w[t];
+                }
+            }
             int64_t inc_sum = len;
 #pragma unroll
             for (int d = 1; d < 64; d <<= 1) {

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Config 5 A/B of the split windows without per-pair arrays (arithmetic rows in k_fill_sort / k_compact): parity
+# tests of every split-window path on the new build, then the config-5 leg alone alternating base and new, twice.
+set -o pipefail
+mkdir -p gpurun_out/ab
+timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --timeout-method thread -m gpu tests/test_heavy_tail_gpu.py "tests/test_fullsize_gpu.py::test_heavy_tail_full_size_sample" tests/test_respond_scale_gpu.py tests/test_respond_order_gpu.py tests/test_sync_golden.py "tests/test_pool_gpu.py::test_pooled_families_vs_oracle" > gpurun_out/r5_ab_bulkrow_tests.txt 2>&1 || { tail -30 gpurun_out/r5_ab_bulkrow_tests.txt; exit 1; }
+tail -1 gpurun_out/r5_ab_bulkrow_tests.txt
+for i in 1 2; do
+  DSY_LIB_PATH=$PWD/dispersy_amd/libdsybloom_base.so timeout -k 10 300 python tools/leg_run.py 5 --steps 8 > gpurun_out/ab/c5b$i.json 2> gpurun_out/ab/c5b$i.err || { tail -20 gpurun_out/ab/c5b$i.err; exit 1; }
+  timeout -k 10 300 python tools/leg_run.py 5 --steps 8 > gpurun_out/ab/c5n$i.json 2> gpurun_out/ab/c5n$i.err || { tail -20 gpurun_out/ab/c5n$i.err; exit 1; }
+done
+for f in c5b1 c5n1 c5b2 c5n2; do
+  python -c "import json;d=json.loads(open('gpurun_out/ab/$f.json').read().strip().splitlines()[-1]);print('$f', d['ms_per_step'], d['serial_ms_per_step'], json.dumps(d['pair_test']))" || exit 1
+done
