@@ -115,7 +115,8 @@ struct WaveTrace {
 
 struct StoreView {
     const uint8_t* blob;
-    const uint64_t* offsets;  // [n_rows + 1] over ALL rows
+    const uint64_t* offsets;  // [n_rows + 1] over ALL rows -- nullptr once the line copy is built (store_release_raw
+                              // frees an uploaded store's packed blob and offsets): responder kernels read `rec`
     const uint8_t* lines;     // line copy of the packets (each starts on a 128-byte line)
     const RowRec* rec;        // [n_rows] where row i's packet sits in `lines`
     const uint64_t* live_gt;  // [n_live] global_time of live row i
