@@ -1274,13 +1274,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kPairW
         total_waves = (uint64_t)n_list * waves_per_req;
     }
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t wave0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    // (wave-uniform in SGPRs: readfirstlane tells the compiler, so the task decode and the claim's state loads below
+    // are scalar instructions, not 64-bit VALU arithmetic on every wave-task)
+    const uint64_t wave0 = (uint64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const bool queue = POOL && L.pool_queue;
     auto next_task = [&]() -> uint64_t {
         uint32_t v = 0;
         if (lane == 0) v = atomicAdd(&L.pool_counts->next[fam], 1u);
-        return (uint64_t)(uint32_t)__shfl((int)v, 0, 64);
+        return (uint64_t)__builtin_amdgcn_readfirstlane(__shfl((int)v, 0, 64));
     };
     uint8_t* my_lds = dma_lds + (threadIdx.x >> 6) * DmaGeometry<2, 1>::kWaveBytes;
     unsigned long long acc_blocks = 0, acc_bytes = 0, acc_slots = 0;  // this lane's work, reduced once per block
