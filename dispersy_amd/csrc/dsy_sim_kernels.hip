@@ -189,7 +189,7 @@ k_sim_build_claims(dsy_sim_config c, uint32_t round, const uint8_t* __restrict__
                    const uint32_t* __restrict__ bits, uint8_t* __restrict__ out, const uint32_t* __restrict__ slots,
                    unsigned long long* __restrict__ work) {
     extern __shared__ __attribute__((aligned(16))) uint8_t sim_lds[];
-    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // (uniform: SALU)
     const uint64_t lp = (uint64_t)blockIdx.x * 4 + wv;
     const bool live = lp < c.peer_end - c.peer_begin;  // wave-uniform; idle waves still meet the barriers
     const uint32_t nwords = (uint32_t)((c.m_bits + 31) / 32);
@@ -328,7 +328,7 @@ k_sim_respond(dsy_sim_config c, const uint8_t* __restrict__ ublob, const uint64_
     extern __shared__ __attribute__((aligned(16))) uint8_t sim_lds[];
     // MD5 / SHA-1 stage the packets through LDS with DMA (hash_key_dma_reg, one block per stage), as the claim build
     constexpr bool kDma = H::kind == DSY_MD5 || H::kind == DSY_SHA1;
-    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // (uniform: SALU)
     const uint64_t ci = (uint64_t)blockIdx.x * NW + wv;
     const bool live = ci < n_claims;  // wave-uniform; idle waves still meet the barriers
     const uint32_t nwords = (uint32_t)((c.m_bits + 31) / 32);
