@@ -128,7 +128,9 @@ __global__ void __launch_bounds__(256) k_bloom(const DevParams* __restrict__ prm
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t waves = (n + 63) / 64;
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    for (uint64_t v = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; v < waves; v += wstride) {
+    // (the wave index through readfirstlane: wave-uniform to the compiler, so the loop control is scalar)
+    const uint64_t v0 = (uint64_t)blockIdx.x * (blockDim.x >> 6) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    for (uint64_t v = v0; v < waves; v += wstride) {
         const uint64_t i = v * 64 + lane;
         const bool active = i < n;
         // idle lanes hash an empty key; the LDS-DMA path still reads its stage from key - prefix_len, so the key
