@@ -957,15 +957,21 @@ __global__ void __launch_bounds__(kFillThreads) k_fill_sort(RespondLaunch L) {
     const uint64_t* off_w = L.pair_off + (uint64_t)a_slot * W + base;
     constexpr int kU = (int)(kBulkChunk / kFillThreads);
     uint32_t len[kU];
-    // a split window (fill_bulk_part): the pairs' rows are arithmetic and their records are re-read (the offsets at
-    // placement, from L2)
+    uint64_t off[kU];
+    // a split window (fill_bulk_part): the pairs' rows are arithmetic and their records are re-read, once
     const bool bulk = S->commit;
     const Plan bp = bulk ? L.plans[(uint64_t)r * L.J + S->win_meta] : Plan{};
     const uint64_t c0 = S->win_cand;
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
         const uint64_t t = threadIdx.x + (uint64_t)kFillThreads * u;
-        len[u] = t < n ? (bulk ? L.st.rec[bulk_row(L, bp, c0, base + t)].len : len_w[t]) : 0u;
+        RowRec rr{};
+        if (t < n) {
+            if (bulk) rr = L.st.rec[bulk_row(L, bp, c0, base + t)];
+            else rr = RowRec{off_w[t], len_w[t], 0u};
+        }
+        len[u] = rr.len;
+        off[u] = rr.off;
     }
     __syncthreads();  // starts scanned
 #pragma unroll
@@ -982,7 +988,7 @@ __global__ void __launch_bounds__(kFillThreads) k_fill_sort(RespondLaunch L) {
         const uint64_t t = threadIdx.x + (uint64_t)kFillThreads * u;
         if (t < n) {
             PairTask tk;
-            tk.off = bulk ? L.st.rec[bulk_row(L, bp, c0, base + t)].off : off_w[t];
+            tk.off = off[u];
             tk.len = len[u];
             tk.slot = (uint32_t)(base + t);
             // the position lies in [0, nw) when bulk_hist holds exactly this window's counts; a stale count (state a
