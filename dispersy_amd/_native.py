@@ -73,6 +73,7 @@ SIGNATURES = {
     "dsy_ctx_stream": (_P, [_P]),
     "dsy_ctx_wait_stream": (ctypes.c_int, [_P, _P]),
     "dsy_ctx_signal_stream": (ctypes.c_int, [_P, _P]),
+    "dsy_ctx_wait_event": (ctypes.c_int, [_P, _P]),
     "dsy_ctx_set_timing": (ctypes.c_int, [_P, ctypes.c_int]),
     "dsy_ctx_kernel_time": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), _PU64, _PU64, _PU64]),
     "dsy_ctx_reset_timing": (ctypes.c_int, [_P]),
@@ -213,6 +214,14 @@ class Context(object):
     def signal_torch(self, device=None):
         """Torch's current stream waits (on the device) for what is queued on the ctx stream."""
         check(self.lib.dsy_ctx_signal_stream(self.handle, self._torch_stream(device)))
+
+    def signal_stream(self, stream):
+        """A torch.cuda.Stream waits (on the device) for what is queued on the ctx stream."""
+        check(self.lib.dsy_ctx_signal_stream(self.handle, stream.cuda_stream))
+
+    def wait_event(self, event):
+        """The ctx stream waits (on the device) for a recorded torch.cuda.Event."""
+        check(self.lib.dsy_ctx_wait_event(self.handle, event.cuda_event))
 
     def set_timing(self, on, only=None):
         """on: bracket kernel launches with HIP events; only: an iterable of TIME_* classes to bracket (default all)."""

@@ -16,9 +16,14 @@ namespace dsy {
 static constexpr uint32_t kLenBins = 1024;
 static constexpr int kDmaS = 2;
 static constexpr size_t kDmaWaveBytes = DmaGeometry<kDmaS, 1>::kWaveBytes;
+static constexpr size_t kLineWaveBytes = LineStaging::kWaveBytes;
 
-__device__ __forceinline__ uint32_t len_bin(uint64_t len, const LenSort& s) {
-    return kLenBins - 1u - min(n_blocks(s.plen + (uint32_t)len, s.blk, s.lenb), kLenBins - 1u);
+// bin of a key in the length sort, longest first: by compression blocks, or (line_mode: the line-staged hashing,
+// hash_key_dma_packed) by line stages, which also depend on where the message starts in its first line
+__device__ __forceinline__ uint32_t len_bin(uint64_t off, uint64_t len, const LenSort& s) {
+    uint32_t units = n_blocks(s.plen + (uint32_t)len, s.blk, s.lenb);
+    if (s.line_mode) units = line_stages(units, (s.base_lo + (uint32_t)off - s.plen) & 127u);
+    return kLenBins - 1u - min(units, kLenBins - 1u);
 }
 
 __device__ __forceinline__ void key_span(const uint64_t* __restrict__ offsets, const uint64_t* __restrict__ rows,
@@ -48,7 +53,7 @@ __global__ void __launch_bounds__(256) k_len_hist(LenSort s, const uint64_t* __r
         uint64_t off;
         uint32_t len;
         key_span(offsets, rows, rec, i, &off, &len);
-        atomicAdd(&h[len_bin(len, s)], 1u);
+        atomicAdd(&h[len_bin(off, len, s)], 1u);
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < kLenBins; i += blockDim.x)
@@ -86,7 +91,7 @@ __global__ void __launch_bounds__(256) k_len_scatter(LenSort s, const uint64_t* 
             uint64_t off;
             uint32_t len;
             key_span(offsets, rows, rec, i, &off, &len);
-            atomicAdd(&cnt[len_bin(len, s)], 1u);
+            atomicAdd(&cnt[len_bin(off, len, s)], 1u);
         }
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < kLenBins; i += blockDim.x) {
@@ -98,7 +103,7 @@ __global__ void __launch_bounds__(256) k_len_scatter(LenSort s, const uint64_t* 
             PairTask tk;
             key_span(offsets, rows, rec, i, &tk.off, &tk.len);
             tk.slot = (uint32_t)i;
-            const uint32_t b = len_bin(tk.len, s);
+            const uint32_t b = len_bin(tk.off, tk.len, s);
             tasks[at[b] + atomicAdd(&cnt[b], 1u)] = tk;
         }
         __syncthreads();
@@ -110,17 +115,23 @@ __global__ void __launch_bounds__(256) k_len_scatter(LenSort s, const uint64_t* 
 // LDS: the compute ceiling); 2 = packet loads without the compression (the gather ceiling).  Diagnostics only, selected
 // by the ctx's DSY_BLOOM_DIAG environment knob (tools/hash_sweep.py); results are meaningless for DIAG != 0.
 // OP 0: add (filter_set_all, OR_MODE as there), OP 1: test (present[key] = all k bits set).
-template <class H, int CHUNK, int OP, bool DMA, int DIAG = 0, int OR_MODE = 0>
-__global__ void __launch_bounds__(256) k_bloom(const DevParams* __restrict__ prm, const uint8_t* __restrict__ blob,
+// DMA 0: direct loads (hash_key); 1: LDS-DMA windows at the key's own alignment (hash_key_dma_reg); 2: line-aligned
+// LDS-DMA stages (hash_key_dma_packed: each line of a key moved once).
+template <class H, int CHUNK, int OP, int DMA, int DIAG = 0, int OR_MODE = 0>
+__global__ void __launch_bounds__(256, 3) k_bloom(const DevParams* __restrict__ prm, const uint8_t* __restrict__ blob,
                                                const uint64_t* __restrict__ offsets, const uint64_t* __restrict__ rows,
                                                const RowRec* __restrict__ rec, const PairTask* __restrict__ tasks, uint64_t n,
                                                uint32_t* __restrict__ filter, uint32_t nwords, int use_lds,
                                                uint8_t* __restrict__ present) {
     extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
-    uint8_t* my_dma = dyn_lds + (threadIdx.x >> 6) * kDmaWaveBytes;
-    uint32_t* lds_filter = (uint32_t*)(dyn_lds + (DMA ? 4 * kDmaWaveBytes : 0));
+    constexpr size_t kWaveLds = DMA == 2 ? kLineWaveBytes : DMA == 1 ? kDmaWaveBytes : 0;
+    uint8_t* my_dma = dyn_lds + (threadIdx.x >> 6) * kWaveLds;
+    uint32_t* lds_filter = (uint32_t*)(dyn_lds + 4 * kWaveLds);
     const uint64_t m = prm->m_bits;
     const uint32_t k = prm->k;
+    uint32_t preword = 0;  // the prefix's bytes, little-endian (DMA 2; <= 4 bytes)
+    if constexpr (DMA == 2)
+        for (uint32_t j = 0; j < min(prm->prefix_len, 4u); ++j) preword |= (uint32_t)prm->prefix[j] << (8 * j);
     if (use_lds) {
         for (uint32_t i = threadIdx.x; i < nwords; i += blockDim.x) lds_filter[i] = OP == 0 ? 0u : filter[i];
         __syncthreads();
@@ -151,7 +162,8 @@ __global__ void __launch_bounds__(256) k_bloom(const DevParams* __restrict__ prm
             }
         }
         H st;
-        if constexpr (DMA) hash_key_dma_reg<H, kDmaS, DIAG>(kv, st, my_dma);
+        if constexpr (DMA == 2) hash_key_dma_packed<H, DIAG>(kv, st, my_dma, preword);
+        else if constexpr (DMA == 1) hash_key_dma_reg<H, kDmaS, DIAG>(kv, st, my_dma);
         else hash_key<H>(kv, st);
         // two call sites, so each sees where its filter lives: ds_or / ds_read on the LDS copy, global atomics /
         // loads on the HBM one (one pointer picked at run time would be a flat pointer: every probe a flat atomic or
@@ -251,30 +263,42 @@ hipError_t launch_len_sort(const LenSort& s, const uint64_t* offsets, const uint
     return hipGetLastError();
 }
 
+// Which staging k_bloom uses (bloom_staging): 2 = line-aligned (hash_key_dma_packed), 1 = windows at the key's own
+// alignment (hash_key_dma_reg), 0 = direct loads.  LDS-DMA is for MD5 / SHA-1 (64-byte blocks; SHA-2 is
+// compute-bound enough that direct loads match it) with prefixes of <= 4 bytes, when the LDS filter leaves room:
+// line staging takes 12 KiB per wave, so three 4-wave workgroups per CU (the VGPR limit) fit beside filters of
+// <= 5 KiB (the MTU filter is 1.3 KiB); window staging 8 KiB per wave.
+int bloom_staging(const BloomLaunch& L) {
+    if (!(L.kind == DSY_MD5 || L.kind == DSY_SHA1) || L.prm_prefix_len > 4) return 0;
+    const uint64_t fbytes = L.use_lds ? (uint64_t)L.nwords * 4 : 0;
+    if (((L.line_kinds >> L.kind) & 1u) && fbytes <= 5 * 1024) return 2;
+    return fbytes <= 16 * 1024 ? 1 : 0;
+}
+
 template <class H, int CHUNK, int OP, int OR_MODE>
 static hipError_t launch_op(const BloomLaunch& L, uint32_t grid) {
-    // LDS-DMA staging for MD5 / SHA-1 whenever the filter is small enough to leave room for it
-    const bool dma = (H::kind == DSY_MD5 || H::kind == DSY_SHA1) && L.prm_prefix_len <= 4 &&
-                     (!L.use_lds || L.nwords * 4 <= 16 * 1024);
-    const size_t lds = (dma ? 4 * kDmaWaveBytes : 0) + (L.use_lds ? (size_t)L.nwords * 4 : 0);
-    if (dma) {
-        if constexpr (H::block_bytes == 64 && CHUNK == 2 && OR_MODE == 0) {
-            if (L.diag == 1 || L.diag == 2) {
-                auto kern = L.diag == 1 ? k_bloom<H, CHUNK, OP, true, 1> : k_bloom<H, CHUNK, OP, true, 2>;
-                launch_timed(kern, dim3(grid), dim3(256), lds, L.stream, L.ev_start, L.ev_stop, L.prm, L.blob, L.offsets,
-                             L.rows, L.rec, L.tasks, L.n, L.filter, L.nwords, L.use_lds, L.present);
-                return hipGetLastError();
+    const int dma = bloom_staging(L);
+    const size_t lds = (dma == 2 ? 4 * kLineWaveBytes : dma == 1 ? 4 * kDmaWaveBytes : 0) +
+                       (L.use_lds ? (size_t)L.nwords * 4 : 0);
+    if constexpr (H::block_bytes == 64) {
+        if (dma) {
+            if constexpr (CHUNK == 2 && OR_MODE == 0) {
+                if (L.diag == 1 || L.diag == 2) {
+                    auto kern = dma == 2 ? (L.diag == 1 ? k_bloom<H, CHUNK, OP, 2, 1> : k_bloom<H, CHUNK, OP, 2, 2>)
+                                         : (L.diag == 1 ? k_bloom<H, CHUNK, OP, 1, 1> : k_bloom<H, CHUNK, OP, 1, 2>);
+                    launch_timed(kern, dim3(grid), dim3(256), lds, L.stream, L.ev_start, L.ev_stop, L.prm, L.blob,
+                                 L.offsets, L.rows, L.rec, L.tasks, L.n, L.filter, L.nwords, L.use_lds, L.present);
+                    return hipGetLastError();
+                }
             }
+            launch_timed(dma == 2 ? k_bloom<H, CHUNK, OP, 2, 0, OR_MODE> : k_bloom<H, CHUNK, OP, 1, 0, OR_MODE>,
+                         dim3(grid), dim3(256), lds, L.stream, L.ev_start, L.ev_stop, L.prm, L.blob, L.offsets, L.rows,
+                         L.rec, L.tasks, L.n, L.filter, L.nwords, L.use_lds, L.present);
+            return hipGetLastError();
         }
-        if constexpr (H::block_bytes == 64)
-            launch_timed(k_bloom<H, CHUNK, OP, true, 0, OR_MODE>, dim3(grid), dim3(256), lds, L.stream, L.ev_start,
-                         L.ev_stop, L.prm, L.blob, L.offsets, L.rows, L.rec, L.tasks, L.n, L.filter, L.nwords, L.use_lds,
-                         L.present);
-    } else {
-        launch_timed(k_bloom<H, CHUNK, OP, false, 0, OR_MODE>, dim3(grid), dim3(256), lds, L.stream, L.ev_start,
-                     L.ev_stop, L.prm, L.blob, L.offsets, L.rows, L.rec, L.tasks, L.n, L.filter, L.nwords, L.use_lds,
-                     L.present);
     }
+    launch_timed(k_bloom<H, CHUNK, OP, 0, 0, OR_MODE>, dim3(grid), dim3(256), lds, L.stream, L.ev_start, L.ev_stop, L.prm,
+                 L.blob, L.offsets, L.rows, L.rec, L.tasks, L.n, L.filter, L.nwords, L.use_lds, L.present);
     return hipGetLastError();
 }
 

@@ -82,6 +82,7 @@ struct RespondJob {
     uint8_t* h_in = nullptr;   // pinned staging (upload region, then host-mapped status)
     uint8_t* h_io = nullptr;
     uint32_t* h_act0 = nullptr;
+    bool act0_identity = true;  // h_act0[a] == a (k_fill_first may then map slot a to claim a without the list)
     const uint32_t* d_slots = nullptr;
     uint32_t* d_act = nullptr;
     void* d_in = nullptr;
@@ -140,6 +141,9 @@ struct dsy_ctx {
     uint32_t bloom_grid = 0; // DSY_BLOOM_GRID at creation: k_bloom grid cap (0: 2 x max_grid)
     uint32_t pair_grid = 0;  // DSY_PAIR_GRID at creation: k_pair_test grid cap (0: max_grid, 8 workgroups per CU)
     int or_mode = 1;     // DSY_OR_MODE at creation: filter-build atomics (filter_set_all OR_MODE, dsy_message.h)
+    // DSY_BLOOM_LINES at creation: bit k = hash kind k's single-filter hashing (k_bloom) stages whole lines
+    // (hash_key_dma_packed); otherwise LDS-DMA windows at each key's own alignment (hash_key_dma_reg)
+    uint32_t bloom_lines = (1u << DSY_MD5) | (1u << DSY_SHA1);
     // DSY_POOL at creation: bit k = hash kind k's responder pairs are pooled across claims (k_pool_scatter) -- MD5,
     // SHA-1 and SHA-256 only; DSY_POOL_QUEUE: the pooled hashing takes its wave-tasks from a queue.  Off by default:
     // on the SHA-1 leg pooling takes k_pair_test 104 -> 95 us (lane use 0.82 -> 1.00) but k_pool_scatter costs 18 us
@@ -190,6 +194,7 @@ struct dsy_ctx {
 struct dsy_store {
     dsy_ctx* ctx = nullptr;
     uint64_t n = 0, n_live = 0, blob_len = 0, min_len = 0;
+    uint64_t max_len = 0;  // longest packet ever stored (grow-only): the line-staged hashing's 16-bit piece limits
     const uint8_t* d_blob = nullptr;
     const uint64_t* d_offsets = nullptr;
     const uint64_t* d_live_gt = nullptr;
@@ -436,6 +441,7 @@ int run_bloom(dsy_ctx* c, BloomOp op, const dsy_bloom_params* p, const uint8_t* 
     L.stream = c->stream;
     L.diag = c->bloom_diag;
     L.or_mode = c->or_mode;
+    L.line_kinds = c->bloom_lines;
     // Large batches hash in length-bucketed order (a wave's 64 lanes then run the same number of blocks); the
     // sort costs ~40 B of traffic per key next to the key bytes themselves.
     if (op != BloomOp::Indices && n >= kLenSortMin) {
@@ -445,6 +451,10 @@ int run_bloom(dsy_ctx* c, BloomOp op, const dsy_bloom_params* p, const uint8_t* 
         if ((rc2 = ws_get(c, "len_tasks", n * sizeof(PairTask), &tasks))) return rc2;
         const bool wide = p->hash_kind >= DSY_SHA384;
         LenSort ls{p->prefix_len, wide ? 128u : 64u, wide ? 16u : 8u};
+        if (bloom_staging(L) == 2) {  // the line-staged hashing's lanes run line stages, not blocks
+            ls.line_mode = 1;
+            ls.base_lo = (uint32_t)(uintptr_t)d_blob & 127u;
+        }
         HIP_TRY(launch_len_sort(ls, d_off, d_rows, d_rec, n, (uint32_t*)bins, (PairTask*)tasks, c->max_grid, c->stream));
         L.tasks = (const PairTask*)tasks;
     }
@@ -533,6 +543,7 @@ int dsy_ctx_create(int device, dsy_ctx** out) {
     if (const char* v = getenv("DSY_BLOOM_DIAG")) c->bloom_diag = atoi(v);
     if (const char* v = getenv("DSY_PAIR_DIAG")) c->pair_diag = atoi(v);
     if (const char* v = getenv("DSY_OR_MODE")) c->or_mode = atoi(v);
+    if (const char* v = getenv("DSY_BLOOM_LINES")) c->bloom_lines = (uint32_t)strtoul(v, nullptr, 0);
     if (const char* v = getenv("DSY_PAIR_GRID")) c->pair_grid = (uint32_t)atoi(v);
     if (const char* v = getenv("DSY_BLOOM_GRID")) c->bloom_grid = (uint32_t)atoi(v);
     if (const char* v = getenv("DSY_POOL")) c->pool_kinds = (uint32_t)strtoul(v, nullptr, 0);
@@ -595,6 +606,13 @@ int dsy_ctx_wait_stream(dsy_ctx* c, void* stream) {
     if (rc) return rc;
     HIP_TRY(hipEventRecord(c->xev, (hipStream_t)stream));
     HIP_TRY(hipStreamWaitEvent(c->stream, c->xev, 0));
+    return DSY_OK;
+}
+
+int dsy_ctx_wait_event(dsy_ctx* c, void* event) {
+    if (!c || !event) return fail(DSY_EINVAL, "NULL argument");
+    Guard g(c);
+    HIP_TRY(hipStreamWaitEvent(c->stream, (hipEvent_t)event, 0));
     return DSY_OK;
 }
 
@@ -759,14 +777,16 @@ static int store_index(dsy_store* s, const uint64_t* offsets, const uint64_t* gt
     // export promises (the sync_meta_message_undone_global_time_index order, dispersydatabase.py:63).
     const uint64_t n = s->n;
     *identity = true;
-    uint64_t minlen = ~0ull;
+    uint64_t minlen = ~0ull, maxlen = 0;
     for (uint64_t i = 0; i < n; ++i) {
         if (i && (meta[i] < meta[i - 1] || (meta[i] == meta[i - 1] && gt[i] < gt[i - 1])))
             return fail(DSY_EUNSORTED, "store rows not sorted by (meta, global_time) at row %llu", (unsigned long long)i);
         minlen = std::min(minlen, offsets[i + 1] - offsets[i]);
+        maxlen = std::max(maxlen, offsets[i + 1] - offsets[i]);
         if (undone && undone[i]) *identity = false;
     }
     s->min_len = n ? minlen : 0;
+    s->max_len = maxlen;
     if (!*identity) {
         live_gt->reserve(n);
         live_row->reserve(n);
@@ -1299,8 +1319,11 @@ static int store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, const uin
     Guard g(c);
     if (c->inflight()) return fail(DSY_EINVAL, "the store cannot change while submitted responder batches are in flight");
     const uint64_t n0 = s->n, base0 = offsets[0], add = offsets[a] - base0;
-    uint64_t minlen = ~0ull;
-    for (uint64_t j = 0; j < a; ++j) minlen = std::min(minlen, offsets[j + 1] - offsets[j]);
+    uint64_t minlen = ~0ull, maxlen = 0;
+    for (uint64_t j = 0; j < a; ++j) {
+        minlen = std::min(minlen, offsets[j + 1] - offsets[j]);
+        maxlen = std::max(maxlen, offsets[j + 1] - offsets[j]);
+    }
 
     HIP_TRY(hipStreamSynchronize(c->stream));  // nothing in flight reads a buffer that is about to be replaced
     // the small columns, staged in pinned memory for one upload: [offsets | row records | global times | metas |
@@ -1405,6 +1428,7 @@ static int store_append(dsy_ctx* c, dsy_store* s, const uint8_t* blob, const uin
     }
     s->pend_n += a;
     s->min_len = n0 ? std::min(s->min_len, minlen) : minlen;
+    s->max_len = std::max(s->max_len, maxlen);
     s->n += a;
     s->blob_len += add;
     s->lines_used = at;
@@ -1637,6 +1661,7 @@ int dsy_store_replace(dsy_ctx* c, dsy_store* s, const uint64_t* rows, const uint
         nrec[i] = RowRec{at + kLineBias, (uint32_t)len, 0u};
         at += line_bytes_for(len);
         minlen = std::min(minlen, len);
+        s->max_len = std::max(s->max_len, len);
     }
     for (uint64_t i = 0; i <= k; ++i) noff[i] = offsets[i] - base0;
     if ((rc = lines_reserve(c, s, at))) return rc;
@@ -2012,7 +2037,7 @@ static int job_window(dsy_ctx* c, RespondSlot& sl) {
     timer_begin(c, &t, kTimeSelect, st);
     if (jb.first_fill && jb.fused_first)
         HIP_TRY(launch_fill_first(L, jb.h_in, jb.d_in, jb.in_b, jb.d_io, jb.cnt_b, jb.per_claim,
-                                  jb.fam_active.size() == 1 ? nullptr : jb.h_act0));
+                                  jb.act0_identity ? nullptr : jb.h_act0));
     else
         HIP_TRY(launch_fill(L));
     jb.first_fill = false;
@@ -2338,14 +2363,16 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const Clai
         uint32_t a = 0;
         for (uint32_t i = 0; i < R; ++i) h_slots[i] = i;
         for (auto& fa : jb.fam_active)
-            for (uint32_t r : fa) h_act0[a++] = r;
+            for (uint32_t r : fa) {
+                jb.act0_identity &= r == a;
+                h_act0[a++] = r;
+            }
     }
     uint8_t* io = (uint8_t*)d_io;
     if (g_host_profile) jb.hp[1] = host_us();  // claims validated and staged
 
     RespondLaunch& L = jb.L;
-    L.st.blob = s->d_blob;
-    L.st.offsets = s->d_offsets;
+    L.st.max_len = s->max_len;
     L.st.lines = s->d_lines;
     L.st.rec = s->d_rec;
     L.st.live_gt = s->d_live_gt;

@@ -78,6 +78,7 @@ struct BloomLaunch {
     hipStream_t stream;
     int diag;               // k_bloom DIAG: 0 = the product kernel, 1 / 2 = compute / gather ceiling diagnostics
     int or_mode;            // filter build: filter_set_all OR_MODE (dsy_message.h)
+    uint32_t line_kinds;    // bit k: hash kind k may use the line-aligned staging (bloom_staging)
     hipEvent_t ev_start, ev_stop;  // when set: recorded by the hashing kernel's own dispatch (launch_timed)
 };
 
@@ -92,12 +93,15 @@ inline void launch_timed(F kern, dim3 grid, dim3 block, size_t lds, hipStream_t 
 }
 
 hipError_t launch_bloom(const BloomLaunch& L);
+int bloom_staging(const BloomLaunch& L);  // 2: line-aligned LDS-DMA, 1: LDS-DMA windows, 0: direct loads
 hipError_t launch_or_reduce(const uint32_t* parts, uint32_t n_parts, uint64_t words, uint32_t* out, uint32_t max_grid,
                             hipStream_t stream);
 
 // Length-bucketed order of a key batch: tasks[0..n) sorted by compression-block count, longest first.
 struct LenSort {
     uint32_t plen, blk, lenb;
+    uint32_t line_mode = 0;  // bin by line stages (hash_key_dma_packed) instead of blocks
+    uint32_t base_lo = 0;    // the blob's address mod 128 (line_mode)
 };
 hipError_t launch_len_sort(const LenSort& s, const uint64_t* offsets, const uint64_t* rows, const RowRec* rec, uint64_t n,
                            uint32_t* d_bins /* 1024 */, PairTask* d_tasks, uint32_t max_grid, hipStream_t stream);
@@ -113,17 +117,22 @@ struct WaveTrace {
 
 // Store view the responder kernels read.  `live` rows are the rows with undone == 0, in index order.
 
+// (The packed upload -- blob + offsets -- is not in the view: store_release_raw frees it once the line copy is built,
+// so no responder kernel can be handed a freed pointer; every packet is reached through `rec` into `lines`.)
 struct StoreView {
-    const uint8_t* blob;
-    const uint64_t* offsets;  // [n_rows + 1] over ALL rows -- nullptr once the line copy is built (store_release_raw
-                              // frees an uploaded store's packed blob and offsets): responder kernels read `rec`
     const uint8_t* lines;     // line copy of the packets (each starts on a 128-byte line)
     const RowRec* rec;        // [n_rows] where row i's packet sits in `lines`
     const uint64_t* live_gt;  // [n_live] global_time of live row i
     const uint64_t* live_row; // [n_live] store row of live row i (nullptr: identity)
     uint64_t n_live;
     uint64_t lines_bytes;     // bytes of `lines` (both DSY_BLOB_GUARD guards included): the hashing's bounds check
+    uint64_t max_len;         // longest packet ever stored: the line-staged pieces keep 16-bit limits (kLinePathMaxLen)
 };
+
+// DmaLinePieces packs two per-piece live-byte limits into the 16-bit halves of a word; a padded message's limit is
+// 64 x blocks - 8 of `1-byte prefix || packet`, which reaches 65536 at 65527-byte packets.  Stores holding a longer
+// packet hash every family with the direct loads (the reference's own UDP cap, 65476 bytes, stays below).
+constexpr uint64_t kLinePathMaxLen = 65526;
 
 // Per (claim, meta) selection plan.
 struct Plan {

@@ -1487,7 +1487,9 @@ static hipError_t pair_test_family(const RespondLaunch& L, bool long_prefix, con
     constexpr bool dma = H::kind == DSY_MD5 || H::kind == DSY_SHA1;
     if constexpr (dma) {
         // (the line-staged pieces address the line copy in 16-byte units from a 32-bit index: under 64 GiB)
-        if (!long_prefix && !((L.direct_kinds >> H::kind) & 1u) && L.st.lines_bytes < (1ull << 36)) {
+        // (and every packet short enough for the pieces' 16-bit limits: kLinePathMaxLen)
+        if (!long_prefix && !((L.direct_kinds >> H::kind) & 1u) && L.st.lines_bytes < (1ull << 36) &&
+            L.st.max_len <= kLinePathMaxLen) {
             const size_t lds = 4 * DmaGeometry<2, 1>::kWaveBytes;
             // (padded: every listed claim has a 1-byte prefix)
             auto kern = pooled ? (padded ? k_pair_test<H, CHUNK, true, 0, true, true> : k_pair_test<H, CHUNK, true, 0, true>)

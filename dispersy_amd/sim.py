@@ -35,10 +35,13 @@ class SimConfig(ctypes.Structure):
                 ("seed", ctypes.c_uint64), ("claim_bytes", ctypes.c_uint32), ("resp_bytes", ctypes.c_uint32)]
 
 
-def make_config(n_peers, universe, rank, world, bits=10160, error_rate=0.01, byte_limit=5120, seed=11):
-    """The claim filter is the community's MTU filter (community.py:637-666, f = 0.01 -> MD5, k = 7)."""
+def make_config(n_peers, universe, rank, world, bits=10160, error_rate=0.01, byte_limit=5120, seed=11, chunks=1):
+    """The claim filter is the community's MTU filter (community.py:637-666, f = 0.01 -> MD5, k = 7).  chunks: the
+    rank's peers split into that many equal chunks for the overlapped round (EpidemicSim.chunks), so the block size
+    is rounded up to a multiple of it (the outcome does not depend on the split)."""
     probe = BloomFilter(bits, error_rate)
     ppr = int(math.ceil(n_peers / float(world)))
+    ppr = (ppr + chunks - 1) // chunks * chunks
     c = SimConfig()
     c.n_peers, c.peers_per_rank = n_peers, ppr
     c.peer_begin, c.peer_end = min(n_peers, rank * ppr), min(n_peers, (rank + 1) * ppr)
@@ -105,7 +108,10 @@ class GpuEngine(object):
         b = self._bufs.get(name)
         if b is None or b.numel() < nbytes:
             if b is not None:
-                self.ctx.synchronize()  # queued kernels may still use the old one
+                # queued kernels -- and an overlapped round's collectives on their own stream -- may still use the
+                # old one
+                self.ctx.synchronize()
+                self.torch.cuda.synchronize(self.dev)
             b = self._bufs[name] = self.torch.empty(max(int(nbytes * 1.25), 1), dtype=self.torch.uint8, device=self.dev)
         return b[:max(nbytes, 1)]
 
@@ -130,6 +136,39 @@ class GpuEngine(object):
             self._matrix = {(rnd + i, world): out[i * world * world:(i + 1) * world * world].reshape(world, world)
                             .astype(np.int64) for i in range(n)}
         return self._matrix[key]
+
+    def chunk_cfg(self, j, cs):
+        """The config of chunk j (cs peers) of this rank's peers, as a rank of its own: its peers, and cs as the block
+        size, so the kernels group its claims by destination CHUNK (a virtual rank)."""
+        c = SimConfig.from_buffer_copy(self.cfg)
+        c.peer_begin = min(self.cfg.peer_end, self.cfg.peer_begin + j * cs)
+        c.peer_end = min(self.cfg.peer_end, c.peer_begin + cs)
+        c.peers_per_rank = cs
+        return c
+
+    def claim_matrix_v(self, rnd, nv, cs):
+        """[src, dst] claims of round rnd over virtual ranks of cs peers (nv of them), identical on every rank."""
+        key = (rnd, nv, cs)
+        if key not in self._matrix:
+            n = self.MATRIX_ROUNDS
+            c = SimConfig.from_buffer_copy(self.cfg)
+            c.peers_per_rank = cs
+            out = np.zeros(n * nv * nv, dtype=np.uint32)
+            _native.check(self.lib.dsy_sim_claim_matrix(self.ctx.handle, ctypes.byref(c), rnd, n, out.ctypes.data, nv))
+            self._matrix = {(rnd + i, nv, cs): out[i * nv * nv:(i + 1) * nv * nv].reshape(nv, nv).astype(np.int64)
+                            for i in range(n)}
+        return self._matrix[key]
+
+    def build_claims_chunk(self, rnd, j, cs, offsets, total, buf):
+        """Claims of chunk j's peers, grouped by destination chunk (offsets: one start per virtual rank)."""
+        c = self.chunk_cfg(j, cs)
+        if c.peer_end > c.peer_begin:
+            offs = (ctypes.c_uint32 * len(offsets))(*[int(x) for x in offsets])
+            bits = self.bits.data_ptr() + (c.peer_begin - self.cfg.peer_begin) * self.cfg.words * 4
+            _native.check(self.lib.dsy_sim_build_claims(self.ctx.handle, ctypes.byref(c), rnd, self.ublob,
+                                                        self.uoff_t.data_ptr(), bits, buf.data_ptr(), offs,
+                                                        len(offsets)))
+        return buf
 
     def build_claims(self, rnd, offsets, total, buf=None):
         buf = self.buffer("claims", total * self.cfg.claim_bytes) if buf is None else buf
@@ -183,6 +222,10 @@ class GpuEngine(object):
         """The ctx stream waits for torch's current stream (a collective's output)."""
         self.ctx.wait_torch(self.dev)
 
+    def wait_event(self, ev):
+        """The ctx stream waits for a recorded torch.cuda.Event (one collective on the communication stream)."""
+        self.ctx.wait_event(ev)
+
     def sync(self):
         self.ctx.synchronize()
 
@@ -193,14 +236,28 @@ class EpidemicSim(object):
     A round on rank q: the claim matrix M (computed identically on every rank, no count exchange) gives the send
     counts M[q] and receive counts M[:, q]; build -> all-to-all(v) of the claims -> respond -> all-to-all(v) of the
     responses (one per claim, so the counts reverse) -> merge.  The host never waits inside a round: the engine's
-    kernels and the collectives are ordered on the device (to_torch / from_torch events around each exchange)."""
+    kernels and the collectives are ordered on the device (to_torch / from_torch events around each exchange).
 
-    def __init__(self, engine, cfg, rank=0, world=1, dist=None, device=None):
+    chunks = C > 1 (cfg from make_config(..., chunks=C)): the round overlaps the exchanges with the kernels.  Each
+    rank's peers are C chunks of cs = peers_per_rank / C peers, treated as virtual ranks in the claim matrix (world x C
+    of them), so the counts per (source chunk, destination rank) come from the same kernel.  Chunk j's claims are built
+    and sent while chunk j - 1's received claims are answered; the exchanges run on one communication stream (in the
+    same order on every rank), the kernels on the engine's stream, each side waiting only for the one event it needs.
+    Every merge runs after the round's last respond, so every response still reads the responders' stores before any
+    merge of the round (the outcome is the unchunked round's, at any C and world)."""
+
+    def __init__(self, engine, cfg, rank=0, world=1, dist=None, device=None, chunks=1):
         self.e, self.cfg, self.rank, self.world, self.dist = engine, cfg, rank, world, dist
         self.coll = Collectives(dist) if dist is not None and world > 1 else None
         self.device = device
         self._tested = 0
-        self.exchanged_bytes = 0
+        self.exchanged_bytes = 0      # bytes this rank sent, itself included
+        self.exchanged_remote = 0     # ... to other ranks
+        if chunks > 1 and cfg.peers_per_rank % chunks:
+            raise ValueError("peers_per_rank %d is not a multiple of chunks=%d (make_config(..., chunks=%d))"
+                             % (cfg.peers_per_rank, chunks, chunks))
+        self.chunks = chunks
+        self._comm = None  # the communication stream of an overlapped round (RCCL on device buffers)
 
     @property
     def tested(self):
@@ -225,10 +282,105 @@ class EpidemicSim(object):
         self.coll.all_to_all_single(out[:total_in], buf[:sum(in_splits)], out_splits, in_splits)
         if from_torch:
             from_torch()
-        self.exchanged_bytes += sum(in_splits)
+        self._account(in_splits)
         return out
 
+    def _round_chunked(self, rnd):
+        c, e, W, C, me = self.cfg, self.e, self.world, self.chunks, self.rank
+        cs = c.peers_per_rank // C
+        nv = W * C
+        Mv = e.claim_matrix_v(rnd, nv, cs)  # [source chunk, destination chunk]
+        M4 = Mv.reshape(W, C, W, C)
+        send = M4[me].sum(axis=2)           # send[j][d]: chunk j's claims to rank d
+        recv = M4[:, :, me, :].sum(axis=2)  # recv[q][j]: claims from rank q's chunk j
+        overlap = self._overlapped()
+        if overlap:
+            import torch
+            if self._comm is None:
+                self._comm = torch.cuda.Stream(device=self.device)
+            comm = self._comm
+        got = [None] * C   # (claims received from every rank's chunk j, how many)
+        ev = [None] * C
+
+        def exchange(name, buf, s_counts, r_counts, rec):
+            in_splits = [int(x) * rec for x in s_counts]
+            out_splits = [int(x) * rec for x in r_counts]
+            self._account(in_splits)
+            if self.coll is None:
+                return buf
+            total_in = sum(out_splits)
+            out = e.buffer(name, total_in) if hasattr(e, "buffer") else self._host_buffer(total_in)
+            if not overlap:
+                if hasattr(e, "to_torch"):
+                    e.to_torch()
+                self.coll.all_to_all_single(out[:total_in], buf[:sum(in_splits)], out_splits, in_splits)
+                if hasattr(e, "from_torch"):
+                    e.from_torch()
+                return out
+            import torch
+            e.ctx.signal_stream(comm)  # comm waits for what the engine has queued (this buffer's producer)
+            with torch.cuda.stream(comm):
+                self.coll.all_to_all_single(out[:total_in], buf[:sum(in_splits)], out_splits, in_splits)
+            return out
+
+        def record():
+            import torch
+            x = torch.cuda.Event()
+            x.record(comm)
+            return x
+
+        def answer(j):
+            if overlap:
+                e.wait_event(ev[j])  # chunk j's claims have arrived (and nothing queued on comm after them)
+            claims_in, n_in = got[j]
+            rc = recv[:, j]
+            poffs = np.concatenate([[0], np.cumsum(rc)[:-1]])
+            resps, tested = e.respond(claims_in, n_in, poffs, n_in, **self._bufkw("resps%d" % j, n_in * c.resp_bytes))
+            if tested is not None:
+                self._tested += tested
+            return exchange("resps_in%d" % j, resps, rc, send[j], c.resp_bytes)
+
+        back = []
+        for j in range(C):
+            counts_v = Mv[me * C + j]
+            offs = np.concatenate([[0], np.cumsum(counts_v)[:-1]])
+            n_out = int(counts_v.sum())
+            buf = e.build_claims_chunk(rnd, j, cs, offs, n_out, self._buf("claims%d" % j, n_out * c.claim_bytes))
+            got[j] = (exchange("claims_in%d" % j, buf, send[j], recv[:, j], c.claim_bytes), int(recv[:, j].sum()))
+            if overlap:
+                ev[j] = record()
+            if j:
+                back.append(answer(j - 1))
+        back.append(answer(C - 1))
+        if overlap:
+            e.wait_event(record())  # every response has arrived
+        for j in range(C):
+            e.merge(back[j], int(send[j].sum()))
+
+    def _buf(self, name, nbytes):
+        return self.e.buffer(name, nbytes) if hasattr(self.e, "buffer") else None
+
+    def _bufkw(self, name, nbytes):
+        return {"buf": self.e.buffer(name, nbytes)} if hasattr(self.e, "buffer") else {}
+
+    def _host_buffer(self, n):
+        import torch
+        return torch.empty(max(n, 1), dtype=torch.uint8, device=self.device)
+
+    def _account(self, in_splits):
+        self.exchanged_bytes += sum(in_splits)
+        self.exchanged_remote += sum(in_splits) - in_splits[self.rank]
+
+    def _overlapped(self):
+        """Exchanges on a stream of their own (device collectives over RCCL, a GPU engine); gloo / CPU exchanges are
+        synchronous anyway."""
+        if self.coll is None or not hasattr(self.e, "wait_event"):
+            return False
+        return self.dist.get_backend() == "nccl"
+
     def round(self, rnd):
+        if self.chunks > 1:
+            return self._round_chunked(rnd)
         c = self.cfg
         M = self.e.claim_matrix(rnd, self.world)
         counts = M[self.rank]

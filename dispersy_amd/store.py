@@ -99,12 +99,31 @@ class _LiveRows(object):
         if len(rows):
             self.added.append(rows)
             self.n += len(rows)
+            self._amortise(gt)
 
     def remove(self, rows, gt):
         where = self._in_base(rows, gt)
         self.dead_base.update(rows[where].tolist())
         self.dead_added.update(rows[~where].tolist())
         self.n -= len(rows)
+        self._amortise(gt)
+
+    # count_upto / cut (every GlobalTimePruning raise) walk the added arrays and the tombstones: keep both small
+    # against the segment.  Added arrays are joined once there are kMaxParts of them (O(added rows), so O(1) per row
+    # over kMaxParts batches); rows() merges everything into base once the pending rows or tombstones reach
+    # 1/kMergeFrac of the segment (O(segment), paid once per segment/kMergeFrac changed rows: O(kMergeFrac) per row)
+    kMaxParts = 16
+    kMergeFrac = 8
+    kMergeMin = 4096
+
+    def _pending(self):
+        return sum(len(a) for a in self.added) + len(self.dead_base) + len(self.dead_added)
+
+    def _amortise(self, gt):
+        if self._pending() >= max(self.kMergeMin, len(self.base) // self.kMergeFrac):
+            self.rows(gt)
+        elif len(self.added) > self.kMaxParts:
+            self.added = [np.concatenate(self.added)]
 
     @staticmethod
     def _arr(s):

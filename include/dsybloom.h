@@ -114,6 +114,9 @@ void* dsy_ctx_stream(dsy_ctx* ctx);
  * NULL (the null stream). */
 int dsy_ctx_wait_stream(dsy_ctx* ctx, void* stream);
 int dsy_ctx_signal_stream(dsy_ctx* ctx, void* stream);
+/* The ctx stream waits (on the device) for a HIP event recorded elsewhere (hipEvent_t, e.g. a torch.cuda.Event
+ * recorded behind one collective on a communication stream that has more queued since). */
+int dsy_ctx_wait_event(dsy_ctx* ctx, void* event);
 /* Kernel timing: when enabled, HIP events bracket every launch of the hash kernels on the ctx stream.
  * dsy_ctx_kernel_time returns the accumulated milliseconds and launch count of kernel class `which`
  * (0 = hash/test of the responder, 1 = single-filter bloom kernels, 2 = selection, 3 = compaction, 4 = the

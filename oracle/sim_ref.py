@@ -86,11 +86,23 @@ class OracleEngine(object):
             out[owner(self.c, p), owner(self.c, partner(self.c, rnd, p))] += 1
         return out
 
-    def build_claims(self, rnd, offsets, total):
+    def claim_matrix_v(self, rnd, nv, cs):
+        """[src, dst] claims over virtual ranks of cs peers (dsy_sim_claim_matrix with peers_per_rank = cs)."""
+        out = np.zeros((nv, nv), dtype=np.int64)
+        for p in range(self.c.n_peers):
+            out[p // cs, partner(self.c, rnd, p) // cs] += 1
+        return out
+
+    def build_claims_chunk(self, rnd, j, cs, offsets, total, buf=None):
+        """Claims of this rank's peers [j cs, (j + 1) cs), grouped by destination chunk (the GPU engine's chunk_cfg)."""
+        return self.build_claims(rnd, offsets, total, lps=range(min(self.local, j * cs), min(self.local, (j + 1) * cs)),
+                                 owner_div=cs)
+
+    def build_claims(self, rnd, offsets, total, lps=None, owner_div=None):
         c = self.c
         buf = bytearray(max(total, 1) * c.claim_bytes)
         cursor = [int(x) for x in offsets]
-        for lp in range(self.local):
+        for lp in (range(self.local) if lps is None else lps):
             p = c.peer_begin + lp
             ids = sorted(self.stores[lp])
             time_high = 0x7fffffffffffffff
@@ -101,7 +113,7 @@ class OracleEngine(object):
             bf = OracleBloom(c.m_bits, c.k, bytes([pre]))
             bf.add_keys(self.packets[i] for i in ids)
             q = partner(c, rnd, p)
-            d = owner(c, q)
+            d = owner(c, q) if owner_div is None else q // owner_div
             at = cursor[d] * c.claim_bytes
             cursor[d] += 1
             CLAIM_HDR.pack_into(buf, at, p, q, time_high, pre, len(ids))

@@ -86,3 +86,69 @@ def test_padding_boundaries_vs_oracle(appended):
             want = sync_ref.respond_lists(conn, served_oracle, (q.time_low, q.time_high, q.offset, q.modulo), ob,
                                           GT_NOW, limit, False)
             assert store.rowid[g].tolist() == want, (i, len(q.bloom_filter.prefix), limit)
+
+
+@pytest.mark.parametrize("plens", [[2, 1, 3, 1], [4, 4, 1, 2, 1, 1, 3]], ids=["2131", "4412113"])
+def test_one_family_mixed_prefixes_first_window(plens):
+    """one hash family (MD5 m=10160) whose claims mix 1-byte and 2-4-byte prefixes, one meta (the
+    fused first window, k_fill_first).  The 1-byte claims are moved to the front of the family's run, so the first
+    active list is not the identity and k_fill_first must map its slots through it -- each claim's rows hashed against
+    its own filter and prefix, and answered in its own slot."""
+    rows = _rows(62, 3000)
+    conn = _sqlite(rows)
+    store = SyncStore.from_rows(rows)
+    served = [MetaMessage("a", 1, SyncDistribution("ASC", 128, None))]
+    served_oracle = [dict(name="a", id=1, direction="ASC", priority=128, pruning=None)]
+    com = SyncCommunity(store, served, global_time=GT_NOW)
+    rng = np.random.Generator(np.random.PCG64(11))
+    packets = [r[4] for r in rows]
+    reqs, blooms = [], []
+    for q, plen in enumerate(plens):
+        prefix = bytes(rng.integers(0, 256, size=plen, dtype=np.uint8))
+        bf, ob = BloomFilter(10160, 0.01, prefix), OracleBloom.from_m_f(10160, 0.01, prefix)
+        # claims differ in what they hold, so answering one with another's filter shows
+        known = [p for p in packets if rng.random() < (0.5 if q % 2 else 0.95)]
+        bf.add_keys(known)
+        ob.add_keys(known)
+        lo = int(rng.integers(1, GT_NOW // 4))
+        reqs.append(ClaimRequest(lo, GT_NOW, 1 + q % 2, 0, bf))
+        blooms.append(ob)
+    for limit in (5120, 1 << 40):
+        got = com.respond(reqs, byte_limit=limit)
+        for i, (q, ob, g) in enumerate(zip(reqs, blooms, got)):
+            want = sync_ref.respond_lists(conn, served_oracle, (q.time_low, q.time_high, q.offset, q.modulo), ob,
+                                          GT_NOW, limit, False)
+            assert store.rowid[g].tolist() == want, (i, plens, limit)
+
+
+def test_packets_past_the_piece_limit_take_direct_loads():
+    """the line-staged pieces keep 16-bit live-byte limits, which a padded message of a >= 65527-byte
+    packet exceeds.  A store holding such packets (longer than the reference's UDP cap, e.g. built from another
+    source) hashes through the direct loads (StoreView.max_len > kLinePathMaxLen) and still answers as the oracle."""
+    rng = np.random.Generator(np.random.PCG64(63))
+    lengths = [65525, 65526, 65527, 65528, 65534, 65535, 65536, 70001] + [int(x) for x in rng.integers(1, 3000, 200)]
+    rng.shuffle(lengths)
+    rows = [(i + 1, int(rng.integers(1, GT_NOW + 1)), 1, 0, rng.bytes(n)) for i, n in enumerate(lengths)]
+    rows.sort(key=lambda r: r[1])
+    rows = [(i + 1,) + r[1:] for i, r in enumerate(rows)]
+    conn = _sqlite(rows)
+    store = SyncStore.from_rows(rows)
+    served = [MetaMessage("a", 1, SyncDistribution("ASC", 128, None))]
+    served_oracle = [dict(name="a", id=1, direction="ASC", priority=128, pruning=None)]
+    com = SyncCommunity(store, served, global_time=GT_NOW)
+    packets = [r[4] for r in rows]
+    reqs, blooms = [], []
+    for q in range(8):
+        m, f = [(10160, 0.01), (4096, 0.001)][q % 2]
+        prefix = bytes(rng.integers(0, 256, size=[1, 2][q // 4], dtype=np.uint8))
+        bf, ob = BloomFilter(m, f, prefix), OracleBloom.from_m_f(m, f, prefix)
+        known = [p for p in packets if rng.random() < 0.7]
+        bf.add_keys(known)
+        ob.add_keys(known)
+        reqs.append(ClaimRequest(1, GT_NOW, 1, 0, bf))
+        blooms.append(ob)
+    got = com.respond(reqs, byte_limit=1 << 40)
+    for i, (q, ob, g) in enumerate(zip(reqs, blooms, got)):
+        want = sync_ref.respond_lists(conn, served_oracle, (q.time_low, q.time_high, q.offset, q.modulo), ob,
+                                      GT_NOW, 1 << 40, False)
+        assert store.rowid[g].tolist() == want, i

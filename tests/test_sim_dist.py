@@ -1,5 +1,6 @@
 """The epidemic simulator's multi-rank path (block-sharded peers, two all-to-all(v) exchanges per round) on CPU:
-world_size 2 over gloo with the oracle CPU engine must reproduce world_size 1 exactly."""
+world sizes 2, 4 and 8 (the driver's 8-GPU shape) over gloo with the oracle CPU engine must reproduce world_size 1
+exactly, with whole rounds and with the chunked round (peers in chunks as virtual ranks, EpidemicSim.chunks)."""
 import os
 import socket
 
@@ -22,44 +23,70 @@ def _free_port():
     return port
 
 
-def run_sim(rank, world, dist_mod=None, byte_limit=2000):
+def run_sim(rank, world, dist_mod=None, byte_limit=2000, chunks=1, exchanged=None):
     blob, offs = make_universe(U, seed=3)
-    cfg = make_config(P, U, rank, world, bits=2048, error_rate=0.01, byte_limit=byte_limit, seed=5)
+    cfg = make_config(P, U, rank, world, bits=2048, error_rate=0.01, byte_limit=byte_limit, seed=5, chunks=chunks)
     eng = OracleEngine(cfg, blob, offs)
     eng.seed(INITIAL)
-    sim = EpidemicSim(eng, cfg, rank, world, dist_mod, torch.device("cpu"))
+    sim = EpidemicSim(eng, cfg, rank, world, dist_mod, torch.device("cpu"), chunks=chunks)
     history = [sim.global_stats()]
     for r in range(ROUNDS):
         sim.round(r)
         history.append(sim.global_stats())
+    if exchanged is not None:
+        exchanged.append((sim.exchanged_bytes, sim.exchanged_remote))
     return history
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, chunks):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        h = run_sim(rank, world, dist)
-        if rank == 0:
-            q.put(h)
+        ex = []
+        h = run_sim(rank, world, dist, chunks=chunks, exchanged=ex)
+        q.put((rank, h, ex[0]))
     finally:
         dist.destroy_process_group()
 
 
-def test_two_ranks_equal_one():
-    single = run_sim(0, 1)
+_SINGLE = {}
+
+
+def _single():
+    if "h" not in _SINGLE:
+        _SINGLE["h"] = run_sim(0, 1)
+    return _SINGLE["h"]
+
+
+@pytest.mark.parametrize("world,chunks", [(2, 1), (4, 1), (8, 1), (2, 3), (8, 2)])
+def test_ranks_equal_one(world, chunks):
+    single = _single()
     assert single[-1][0] > single[0][0]  # packets spread
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, chunks)) for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=300)
+    got = dict((r, (h, ex)) for r, h, ex in (q.get(timeout=600) for _ in range(world)))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert got == single
+    for r in range(world):
+        assert got[r][0] == single, (world, chunks, r)
+    # every claim and response record crosses once: what the ranks sent is the whole round's records
+    sent = sum(got[r][1][0] for r in range(world))
+    blob, offs = make_universe(U, seed=3)
+    cfg = make_config(P, U, 0, 1, bits=2048, seed=5)
+    assert sent == ROUNDS * P * (cfg.claim_bytes + cfg.resp_bytes)
+    assert 0 < sum(got[r][1][1] for r in range(world)) < sent
+
+
+@pytest.mark.parametrize("chunks", [2, 4, 5])
+def test_chunked_round_one_rank_equals_whole(chunks):
+    """The chunked round at one rank (no exchange): chunk-wise builds over virtual ranks, responds and one merge at
+    the end give the whole round's stores."""
+    assert run_sim(0, 1, chunks=chunks) == _single()
 
 
 def test_sim_config_matches_community_filter():

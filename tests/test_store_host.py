@@ -81,3 +81,38 @@ def test_host_deletes_at_10m_rows_are_o_batch():
     print("prune(100) + delete_rows(100) + set_undone(10) at 10 M rows: median %.3f ms" % (med * 1e3))
     assert med <= 2e-3
     assert st.live_count(1) == n + 1000 - int(st.deleted.sum()) - int(((st.undone != 0) & ~st.deleted).sum())
+
+
+@pytest.mark.parametrize("seed", [5, 6])
+def test_host_live_index_amortised_merges_against_brute_force(seed, monkeypatch):
+    """The same random walk with the amortised merges (_LiveRows._amortise) triggered every few operations: joined
+    added arrays and merges into base mid-stream must not change any order or count."""
+    from dispersy_amd.store import _LiveRows
+    monkeypatch.setattr(_LiveRows, "kMaxParts", 2)
+    monkeypatch.setattr(_LiveRows, "kMergeMin", 16)
+    monkeypatch.setattr(_LiveRows, "kMergeFrac", 64)
+    test_host_live_index_against_brute_force(seed)
+
+
+def test_host_prune_cost_flat_over_many_single_row_appends():
+    """count_upto / cut walk the added arrays and the tombstones on every prune, and every append
+    adds an array; a long-running community (one received message, one global-time raise, one prune) must not grow a
+    per-prune cost with the number of batches seen."""
+    n = 200_000
+    gt = np.arange(1, n + 1, dtype=np.uint64)
+    st = SyncStore(b"", np.zeros(n + 1, dtype=np.uint64), gt, np.ones(n, dtype=np.uint32), ctx=object())
+    rng = np.random.default_rng(3)
+    times = []
+    for i in range(3000):
+        st.append([b""], np.asarray([int(rng.integers(n // 2, n))], dtype=np.uint64), np.ones(1, dtype=np.uint32))
+        if i % 3 == 0:
+            st.delete_rows(np.asarray([int(rng.integers(n // 2, n))]))
+        t0 = time.perf_counter()
+        st.prune(1, i // 10)
+        times.append(time.perf_counter() - t0)
+    lv = st._live[1]
+    assert len(lv.added) <= 17
+    early = sorted(times[200:700])[250]
+    late = sorted(times[-500:])[250]
+    assert late < 3 * early + 50e-6, (early, late)
+    assert st.live_rows(1).tolist() == brute_live(st, 1).tolist()
