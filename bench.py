@@ -200,6 +200,9 @@ def parse():
     ap.add_argument("--sim-initial", type=int, default=100)
     ap.add_argument("--sim-rounds", type=int, default=10)
     ap.add_argument("--sim-warmup", type=int, default=2)
+    ap.add_argument("--sim-chunks", type=int, default=0,
+                    help="config 3: each rank's peers in this many chunks, exchanges overlapped with the kernels "
+                         "(EpidemicSim.chunks); 0: 4 with more than one rank, else 1 (one rank exchanges nothing)")
     ap.add_argument("--extra", default="claim,dropin,dedup,ingest,sha1,1,3,4,5",
                     help="BASELINE configs measured beside the headline (config 2): 1 single filter, 3 gossip "
                          "simulator, 4 large filters, 5 heavy-tailed packets, ingest: received packets appended to "
@@ -384,8 +387,10 @@ def run(args, rank, world, local):
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_claims > 0:
+        # (every 8th claim of the step, both styles, also checked in full against the oracle: 128 claims; the
+        # test suite's test_fullsize_gpu.py checks all 1024)
         cpu = responder_cpu(args, ctx, lib, store, reqs, claims, fblob, blob, offsets,
-                            np.arange(1, N + 1, dtype=np.uint64), N, dev, "cfg2 md5")
+                            np.arange(1, N + 1, dtype=np.uint64), N, dev, "cfg2 md5", check=list(range(0, R, 8)))
 
     extra = set(x for x in args.extra.split(",") if x and x != "none")
 
@@ -504,12 +509,16 @@ def tail_keys(gossip, sha1=None, heavy=None, single=None, large=None, cpu=None):
         "cfg4_sha256_add_int32_frac": {k: v.get("add_valu_frac") for k, v in (_get(large, "filters") or {}).items()}
         or None,
         "cfg1_at_capacity_md5_tests_per_s": _get(single, "md5", "at_capacity", "test_keys_per_s"),
+        "cfg2_cpu_1core_pairs_per_s": _get(cpu, "value"),
+        "cfg2_cpu_ncore": {"value": _get(cpu, "n_core", "value"), "cores": _get(cpu, "n_core", "cores"),
+                           "unit": _get(cpu, "n_core", "unit")} if _get(cpu, "n_core") else None,
     }
     # every in-leg GPU == CPU-oracle check that ran (None: the leg or its check did not run)
     checks = {
         "cfg2_responder_sample": _get(cpu, "gpu_matches_cpu_on_sample"),
         "sha1_responder_sample": _get(sha1, "cpu_baseline", "gpu_matches_cpu_on_sample"),
         "cfg5_responder_sample": _get(heavy, "cpu_baseline", "gpu_matches_cpu_on_sample"),
+        "cfg2_responder_oracle_128_claims": _get(cpu, "oracle_check", "gpu_matches_oracle"),
         "cfg1_md5": _ok(_get(single, "md5", "gpu_vs_oracle")),
         "cfg1_sha1": _ok(_get(single, "sha1", "gpu_vs_oracle")),
         "cfg1_md5_at_capacity": _ok(_get(single, "md5", "at_capacity", "gpu_vs_oracle")),
@@ -1093,14 +1102,16 @@ def gossip_sim(args, ctx, dev, rank, world, dist):
     import torch
     from dispersy_amd.sim import EpidemicSim, GpuEngine, make_config, make_universe
     blob, offs = make_universe(args.sim_universe, seed=11)
-    cfg = make_config(args.sim_peers, args.sim_universe, rank, world, seed=11)
+    chunks = args.sim_chunks or (4 if world > 1 else 1)
+    cfg = make_config(args.sim_peers, args.sim_universe, rank, world, seed=11, chunks=chunks)
     eng = GpuEngine(cfg, blob, offs, dev, ctx=ctx)
     eng.seed(args.sim_initial)
-    sim = EpidemicSim(eng, cfg, rank, world, dist, dev)
+    sim = EpidemicSim(eng, cfg, rank, world, dist, dev, chunks=chunks)
     held0 = sim.global_stats()[0]
     for r in range(args.sim_warmup):
         sim.round(r)
     eng.sync()
+    ex0 = (sim.exchanged_bytes, sim.exchanged_remote)
     ctx.reset_timing()
     ctx.set_timing(True, only=[_native.TIME_SIM_BUILD, _native.TIME_SIM_RESPOND])
     if dist:
@@ -1128,8 +1139,15 @@ def gossip_sim(args, ctx, dev, rank, world, dist):
                            if secs else None},
             "lane_utilization": round(wk["blocks"] / max(wk["lane_slots"], 1), 4),
             "blocks_per_round": int(wk["blocks"] / max(args.sim_rounds, 1))}
+    # per rank and round: record bytes this rank sent (claims + responses), and the part that left the rank
+    mine = torch.tensor([(sim.exchanged_bytes - ex0[0]) // max(args.sim_rounds, 1),
+                         (sim.exchanged_remote - ex0[1]) // max(args.sim_rounds, 1)], dtype=torch.int64, device=dev)
+    per_rank = [mine.tolist()]
     if sim.coll is not None:
         dt = float(sim.coll.scalar(dt, "max", device=dev))
+        every = torch.zeros(2 * world, dtype=torch.int64, device=dev)
+        sim.coll.all_gather_into(every, mine)
+        per_rank = every.view(world, 2).tolist()
     held, chk = sim.global_stats()
     return {"metric": "gossip sync rounds/sec", "value": round(args.sim_rounds / dt, 3), "unit": "rounds/s",
             "n_gpus": world, "scaling": "strong", "rounds": args.sim_rounds, "warmup_rounds": args.sim_warmup,
@@ -1137,7 +1155,13 @@ def gossip_sim(args, ctx, dev, rank, world, dist):
             "config": {"peers": args.sim_peers, "universe": args.sim_universe, "initial_packets": args.sim_initial,
                        "filter": "m=%d k=%d md5" % (cfg.m_bits, cfg.k), "byte_limit": cfg.byte_limit},
             "packets_held_start": held0, "packets_held_end": held, "store_checksum": "%016x" % chk,
-            "exchange_bytes_rank0": sim.exchanged_bytes, "kernels": kernels,
+            "exchange_bytes_rank0": sim.exchanged_bytes, "kernels": kernels, "chunks": chunks,
+            "exchange_per_round": {"bytes_sent_per_rank": [r[0] for r in per_rank],
+                                   "bytes_to_other_ranks_per_rank": [r[1] for r in per_rank],
+                                   "how": "two all-to-all(v) per round (claims %d B, responses %d B per peer)%s"
+                                          % (cfg.claim_bytes, cfg.resp_bytes,
+                                             ", overlapped with the kernels in %d chunks" % chunks
+                                             if chunks > 1 and world > 1 else "")},
             "cpu_baseline": gossip_cpu(args, blob, offs) if rank == 0 and world == 1 and args.cpu_claims > 0 else None}
 
 

@@ -13,16 +13,182 @@
 
 namespace dsy {
 
+// ---------------------------------------------------------------------------------------------------------
+// Line-aligned staging of PACKED keys (k_bloom: config 1's add_keys / __contains__ over a caller's blob, and claim
+// filters over the store's line copy).  hash_key_dma_reg stages each key's message as windows [base + 128 s, +128)
+// with base = key - prefix at any byte alignment: a window straddles two 128-byte lines, and the line it shares with
+// the next window is requested again one stage later -- ~8 us later under load, past the XCD L2's turnover
+// (4 MiB at ~0.7 TB/s), so it is fetched twice (config 1 moved 1.5-1.6x its bytes).  Here stage s moves
+// whole LINES: line s + shift of the key (shift 0 or 1, below), 8 x 16-byte pieces, each line of the message once.
+// A block of the message then starts anywhere in a line, so each key's LDS row is [carry 64 B][line 128 B]: the carry
+// is the previous line's last 64 bytes (copied there, LDS to LDS, after a stage's reads), and the two blocks of a stage
+// are the 128 bytes at row offset e0 (1..64, per key) -- 33 dword reads at a per-lane address and one alignbyte per
+// word.
+//   a = base & 127 (where the message starts in its first line)
+//   a == 0       lag 0, shift 0: e0 = 64, stage s hashes blocks 2s, 2s + 1
+//   1 <= a <= 64 lag 1, shift 0: e0 = a, stage s hashes blocks 2s - 1, 2s (stage 0's first slot is empty)
+//   a > 64       lag 0, shift 1: e0 = a - 64; stage 0 stages line 1 and, as its carry, line 0's last 64 bytes (the
+//                message starts there), so stage s hashes blocks 2s, 2s + 1
+// A key takes line_stages(nb, a) = ceil((nb + lag) / 2) stages; the length sort (k_len_*, LenSort::line_mode) orders
+// keys by that count, so a wave's lanes run the same number of stages.
+struct LineStaging {
+    static constexpr int kRowBytes = 192;                      // [carry 64 B][line 128 B] per key
+    static constexpr int kInsts = 64 * kRowBytes / 1024;       // 12 DMA wave-instructions cover the wave's rows
+    static constexpr int kWaveBytes = 64 * kRowBytes;          // 12 KiB per wave
+};
+
+__host__ __device__ __forceinline__ uint32_t line_lag(uint32_t a) { return (a >= 1u && a <= 64u) ? 1u : 0u; }
+__host__ __device__ __forceinline__ uint32_t line_stages(uint32_t nb, uint32_t a) { return (nb + line_lag(a) + 1u) / 2u; }
+
+// The pieces one lane moves for its wave's 64 keys.  DMA wave-instruction i writes LDS bytes [1024 i, +1024) of the
+// wave's buffer, lane t the 16 bytes at 1024 i + 16 t: 16-byte slot g = 64 i + t is piece g % 12 of key g / 12's row
+// (pieces 0-3 the carry, 4-11 the line).  Per piece: idx = its stage-0 address in 16-byte units from the wave-uniform
+// base (stage s: + 8 s); lim: stage s >= 1 is live while 128 s < lim; m0: bit i = piece i is live at stage 0 (the
+// first line's pieces before the message, and the carry pieces of keys with shift 1).  25 VGPRs.
+struct DmaPackedPieces {
+    using G = LineStaging;
+    uint32_t idx[G::kInsts];
+    uint32_t lim[G::kInsts];
+    uint32_t m0;
+    // line: the key's first line (from the wave base, < 2^28); lo / hi: the bytes to load, [lo, hi) from that line's
+    // start (the prefix bytes are merged in registers, not loaded)
+    __device__ __forceinline__ void init(uint32_t line, uint32_t shift, uint32_t lo, uint32_t hi, uint8_t* lds_wave) {
+        const uint32_t lane = threadIdx.x & 63;
+        uint4* xs = (uint4*)lds_wave;
+        xs[lane] = make_uint4(line, shift, lo, hi);
+        m0 = 0;
+#pragma unroll
+        for (int i = 0; i < G::kInsts; ++i) {
+            const uint32_t g = 64u * i + lane;
+            const uint32_t p = g / 12u, k = g % 12u;
+            const uint4 v = xs[p];
+            uint32_t start0, live0;  // the piece's stage-0 byte range [start0, +16) from the key's first line
+            if (k < 4) {             // carry piece: line 0's bytes 64 + 16 k, staged only at stage 0 (shift 1)
+                start0 = 64u + 16u * k;
+                idx[i] = 8u * v.x + 4u + k;
+                lim[i] = 0u;
+                live0 = v.y;
+            } else {
+                const uint32_t c = k - 4u;
+                start0 = 128u * v.y + 16u * c;
+                idx[i] = 8u * (v.x + v.y) + c;
+                lim[i] = v.w > start0 ? v.w - start0 : 0u;
+                live0 = 1u;
+            }
+            live0 &= (start0 < v.w) & (start0 + 16u > v.z);
+            m0 |= live0 << i;
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the reads are done before the first stage's DMA lands
+        __builtin_amdgcn_wave_barrier();
+    }
+    template <bool SKIP = false>
+    __device__ __forceinline__ void issue(uint32_t s, const uint8_t* base, uint32_t lds) const {
+        if constexpr (SKIP) return;
+#pragma unroll
+        for (int i = 0; i < G::kInsts; ++i) {
+            const bool live = s ? 128u * s < lim[i] : ((m0 >> i) & 1u) != 0u;
+            if (live)
+                __builtin_amdgcn_global_load_lds((const void*)(base + ((uint64_t)(idx[i] + (s << 3)) << 4)),
+                                                 (__attribute__((address_space(3))) void*)(uintptr_t)(lds + i * 1024),
+                                                 16, 0, 0);
+        }
+    }
+};
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, d, 64);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), d, 64);
+        const uint64_t o = ((uint64_t)hi << 32) | lo;
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+// prefix || key of every lane (prefix <= 4 bytes) through line-aligned LDS stages (above); called by ALL 64 lanes of a
+// wave together (idle lanes: a zero-length key at any address).  Falls back to direct loads for a wave whose keys
+// span 32 GiB or more (the pieces' 32-bit 16-byte offsets).  MODE as in hash_key_dma_reg (DIAG builds only).
+template <class H, int MODE = 0>
+__device__ __forceinline__ void hash_key_dma_packed(const KeyView& kv, H& st, uint8_t* lds_wave, uint32_t preword) {
+    static_assert(H::block_bytes == 64, "LDS-DMA staging is for 64-byte blocks");
+    using G = LineStaging;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t r = kv.plen;
+    const uint32_t total = r + kv.len;
+    const uint32_t nb = n_blocks(total, 64, H::len_bytes);
+    const uint64_t base = (uint64_t)(uintptr_t)kv.key - r;
+    const uint64_t wline = wave_min_u64(base >> 7);  // the wave's lowest line: piece offsets are 32-bit from there
+    const uint64_t span = (base >> 7) - wline;
+    if (__builtin_amdgcn_readfirstlane((uint32_t)(__ballot(span >= (1ull << 28)) != 0))) {
+        hash_key<H>(kv, st);
+        return;
+    }
+    const uint8_t* wbase = (const uint8_t*)(uintptr_t)(wline << 7);
+    const uint32_t a = (uint32_t)base & 127u;
+    const uint32_t lag = line_lag(a), shift = a > 64u ? 1u : 0u;
+    const uint32_t e0 = a + 64u - 64u * lag - 128u * shift;  // 1..64
+    const uint32_t nst = wave_max_uniform(line_stages(nb, a));
+    const uint32_t tmin = wave_min_uniform(total);
+    const uint32_t lag_min = wave_min_uniform(lag);  // the slot's highest block is 2 s + bb - lag_min
+    DmaPackedPieces dl;
+    dl.init((uint32_t)span, shift, a + r, a + total, lds_wave);
+    st.init();
+    const uint32_t lds = lds_local(lds_wave);
+    const uint8_t* row = lds_wave + lane * G::kRowBytes;
+    const uint32_t* win = (const uint32_t*)(row + (e0 & ~3u));
+    const uint32_t sh = e0 & 3u;
+    if (nst) dl.template issue<MODE == 1>(0, wbase, lds);
+    for (uint32_t s = 0; s < nst; ++s) {
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): stage s has landed
+        __builtin_amdgcn_wave_barrier();
+        uint32_t d[33];
+#pragma unroll
+        for (int i = 0; i < 33; ++i) d[i] = win[i];
+        // the line's last 64 bytes: the next stage's carry (four named registers: an array of them was kept in
+        // scratch by the compiler)
+        const uint4 t0 = *(const uint4*)(row + 128), t1 = *(const uint4*)(row + 144);
+        const uint4 t2 = *(const uint4*)(row + 160), t3 = *(const uint4*)(row + 176);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the line slots are free again
+        __builtin_amdgcn_wave_barrier();
+        *(uint4*)(row) = t0;  // (the DMA below writes only the line slots)
+        *(uint4*)(row + 16) = t1;
+        *(uint4*)(row + 32) = t2;
+        *(uint4*)(row + 48) = t3;
+        if (s + 1 < nst) dl.template issue<MODE == 1>(s + 1, wbase, lds);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            const int b = (int)(2 * s + bb) - (int)lag;
+            if (b >= 0 && b < (int)nb) {
+                uint32_t x[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) x[i] = __builtin_amdgcn_alignbyte(d[16 * bb + i + 1], d[16 * bb + i], sh);
+                if (b == 0 && r) x[0] = (x[0] & ~low_bytes_mask(r)) | preword;
+                // (wave-uniform: every lane's block lies inside its message when the slot's highest one does)
+                finish_block<H>(x, 64u * (uint32_t)b, total, b + 1 == (int)nb, 64u * (2 * s + bb + 1 - lag_min) <= tmin);
+                if (MODE != 2) st.template compress<true>(x);
+                else st.h[0] ^= x[0] ^ x[5] ^ x[10] ^ x[15];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+
 static constexpr uint32_t kLenBins = 1024;
 static constexpr int kDmaS = 2;
 static constexpr size_t kDmaWaveBytes = DmaGeometry<kDmaS, 1>::kWaveBytes;
 static constexpr size_t kLineWaveBytes = LineStaging::kWaveBytes;
 
 // bin of a key in the length sort, longest first: by compression blocks, or (line_mode: the line-staged hashing,
-// hash_key_dma_packed) by line stages, which also depend on where the message starts in its first line
+// hash_key_dma_packed) by block slots and lag -- a lane of lag 1 fills block slots 1 .. nb, one of lag 0 slots
+// 0 .. nb - 1, so keys of equal nb + lag and equal lag run the same slots: a slot no lane of the wave needs (the empty
+// first one of a lag-1 wave, the last one of an odd count) is skipped as a whole instead of hashed for a few lanes
 __device__ __forceinline__ uint32_t len_bin(uint64_t off, uint64_t len, const LenSort& s) {
     uint32_t units = n_blocks(s.plen + (uint32_t)len, s.blk, s.lenb);
-    if (s.line_mode) units = line_stages(units, (s.base_lo + (uint32_t)off - s.plen) & 127u);
+    if (s.line_mode) {
+        const uint32_t lag = line_lag((s.base_lo + (uint32_t)off - s.plen) & 127u);
+        units = 2u * (units + lag) + lag;
+    }
     return kLenBins - 1u - min(units, kLenBins - 1u);
 }
 

@@ -1190,10 +1190,39 @@ static constexpr uint64_t kSlackMin = 16384;
 // launch_pend_order).  When every meta's new entries fit its region's slack, each meta's tail from its first new entry
 // on is merged in place -- O(batch + that tail), the common case of new global times at or near the top; otherwise one
 // merge of the whole index lays it out again with fresh slack.
+// DSY_FLUSH_PROFILE: one stderr line per flush with its phases in microseconds (each phase synchronised: diagnostics)
+struct FlushClock {
+    bool on;
+    hipStream_t st;
+    double t0, last;
+    char buf[256];
+    int at = 0;
+    explicit FlushClock(hipStream_t s) : st(s) {
+        static const bool env = getenv("DSY_FLUSH_PROFILE") != nullptr;
+        on = env;
+        t0 = last = on ? now() : 0;
+        buf[0] = 0;
+    }
+    static double now() {
+        return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
+    void mark(const char* what) {
+        if (!on) return;
+        hipStreamSynchronize(st);
+        const double t = now();
+        at += snprintf(buf + at, sizeof(buf) - at > 0 ? sizeof(buf) - at : 0, " %s=%.1f", what, t - last);
+        last = t;
+    }
+    void done(uint64_t P, const char* mode) {
+        if (on) fprintf(stderr, "flush_profile P=%llu mode=%s%s total=%.1f\n", (unsigned long long)P, mode, buf, now() - t0);
+    }
+};
+
 static int store_flush(dsy_ctx* c, const dsy_store* cs) {
     dsy_store* s = const_cast<dsy_store*>(cs);
     const uint64_t P = s->pend_n;
     if (!P) return DSY_OK;
+    FlushClock fc(c->stream);
     std::map<uint32_t, uint64_t> cntm(s->pend_cnt.begin(), s->pend_cnt.end());
     for (auto& e : s->segs) cntm.emplace(e.first, 0);
     const uint32_t nm = (uint32_t)cntm.size();
@@ -1248,9 +1277,11 @@ again:
         std::memcpy(h.data() + b_m + 4 * b_u, cnt.data(), (size_t)nm * 8);
         HIP_TRY(hipMemcpyAsync(tab, h.data(), h.size(), hipMemcpyHostToDevice, c->stream));
     }
+    fc.mark("table");
     HIP_TRY(launch_pend_order(s->d_pend_meta, s->d_pend_gt, P, s->pend_glo, s->pend_ghi, (const uint32_t*)tab, d_segs,
                               fast ? nullptr : d_gapb, nm, s->pend_base, (uint8_t*)d_rows + b_rows, b_scr, d_rows,
                               c->stream));
+    fc.mark("order");
     if (!fast) {
         std::map<uint32_t, std::pair<uint64_t, uint64_t>> cm;
         for (uint32_t r = 0; r < nm; ++r) {
@@ -1258,6 +1289,8 @@ again:
             if (cnt[r] || extra[r]) cm[metas[r]] = {cnt[r], extra[r]};
         }
         if ((rc = live_merge(c, s, d_rows, total, cm, false))) return rc;
+        fc.mark("whole_merge");
+        fc.done(P, "whole");
         s->pend_n = 0;
         s->pend_cnt.clear();
         return DSY_OK;
@@ -1268,6 +1301,7 @@ again:
     HIP_TRY(launch_first_rank(s->d_live_gt, s->d_live_row, d_rows, d_starts, d_cnt, nm, d_first, c->stream));
     HIP_TRY(hipMemcpyAsync(first.data(), d_first, (size_t)nm * 8, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    fc.mark("first_rank");
     uint64_t tail_max = 0, tail_sum = 0;
     for (uint32_t r = 0; r < nm; ++r)
         if (cnt[r]) {
@@ -1302,6 +1336,8 @@ again:
         s->segs[metas[r]].second += cnt[r];
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
+    fc.mark("tail_merge");
+    fc.done(P, "in_place");
     s->n_live += P;
     s->ix_fast += 1;
     s->ix_bytes += 16 * P + 64 * moved;  // the new entries written; each tail entry copied out and merged back

@@ -246,9 +246,10 @@ class EpidemicSim(object):
     Every merge runs after the round's last respond, so every response still reads the responders' stores before any
     merge of the round (the outcome is the unchunked round's, at any C and world)."""
 
-    def __init__(self, engine, cfg, rank=0, world=1, dist=None, device=None, chunks=1):
+    def __init__(self, engine, cfg, rank=0, world=1, dist=None, device=None, chunks=1, exchange_always=False):
         self.e, self.cfg, self.rank, self.world, self.dist = engine, cfg, rank, world, dist
-        self.coll = Collectives(dist) if dist is not None and world > 1 else None
+        # exchange_always: run the collectives even at world 1 (a one-rank RCCL job exercises the exchange path)
+        self.coll = Collectives(dist) if dist is not None and (world > 1 or exchange_always) else None
         self.device = device
         self._tested = 0
         self.exchanged_bytes = 0      # bytes this rank sent, itself included
@@ -266,7 +267,7 @@ class EpidemicSim(object):
         return self._tested
 
     def _exchange(self, name, buf, send_counts, recv_counts, rec_bytes):
-        if self.world == 1:
+        if self.coll is None:
             return buf
         in_splits = [int(c) * rec_bytes for c in send_counts]
         out_splits = [int(c) * rec_bytes for c in recv_counts]
@@ -401,7 +402,7 @@ class EpidemicSim(object):
     def global_stats(self):
         held, chk = self.e.stats()
         chk &= 0x7fffffffffffffff
-        if self.world == 1:
+        if self.coll is None:
             return held, chk
         import torch
         held = self.coll.scalar(held, "sum", device=self.device)

@@ -85,11 +85,11 @@ def cfg3(coll, dev):
     P, U, INITIAL, ROUNDS = 1500, 3000, 40, 4
     blob, offs = make_universe(U, seed=4)
 
-    def run(rank, world, d):
-        cfg = make_config(P, U, rank, world, seed=13)
+    def run(rank, world, d, chunks=1):
+        cfg = make_config(P, U, rank, world, seed=13, chunks=chunks)
         eng = GpuEngine(cfg, blob, offs, dev)
         eng.seed(INITIAL)
-        sim = EpidemicSim(eng, cfg, rank, world, d, dev)
+        sim = EpidemicSim(eng, cfg, rank, world, d, dev, chunks=chunks)
         hist = [list(sim.global_stats())]
         for r in range(ROUNDS):
             sim.round(r)
@@ -97,7 +97,8 @@ def cfg3(coll, dev):
         return hist, sim.exchanged_bytes
 
     hist, moved = run(coll.rank, coll.world, dist)
-    out = {"history": hist, "exchanged_bytes": moved}
+    chunked, _ = run(coll.rank, coll.world, dist, chunks=3)  # peers in chunks as virtual ranks (gloo: synchronous)
+    out = {"history": hist, "exchanged_bytes": moved, "chunked_equal": chunked == hist}
     if coll.rank == 0:
         single, _ = run(0, 1, None)
         out["equal_single"] = hist == single

@@ -74,6 +74,7 @@ def test_cfg3_sim_two_ranks_equal_one(two_ranks):
     assert r0["cfg3"]["history"] == r1["cfg3"]["history"]
     assert r0["cfg3"]["history"][-1][0] > r0["cfg3"]["history"][0][0]
     assert r0["cfg3"]["exchanged_bytes"] > 0 and r1["cfg3"]["exchanged_bytes"] > 0
+    assert r0["cfg3"]["chunked_equal"] and r1["cfg3"]["chunked_equal"]
 
 
 def test_cfg4_one_rank_add_sharded_equals_single_build():
@@ -100,6 +101,23 @@ def test_cfg4_one_rank_add_sharded_equals_single_build():
         whole = BloomFilter(m, f, prefix)
         whole.add_packed(blob, offs)
         assert union.cpu().numpy().tobytes()[:m // 8] == whole.bytes
+
+
+def test_sim_overlapped_round_over_rccl_one_rank():
+    """The simulator's chunked round with its exchanges on a communication stream (RCCL all-to-all(v), per-exchange
+    events the engine's kernels wait on) in a one-rank "nccl" job: every record goes through RCCL, and the per-round
+    history equals the plain round's (tools/sim_rccl_probe.py).  The driver's 8-GPU run takes this path."""
+    port = str(_free_port())
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", port, os.path.join(os.path.dirname(HERE), "tools", "sim_rccl_probe.py")]
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=180)
+    log = p.stdout.decode(errors="replace")
+    assert p.returncode == 0, log[-3000:]
+    row = json.loads([ln for ln in log.splitlines() if ln.startswith("{")][-1])
+    assert row["backend"] == "nccl" and row["whole"][-1][0] > row["whole"][0][0]
+    for key in ("chunks1", "chunks4"):
+        assert row[key]["equal"] and row[key]["exchanged_bytes"] > 0, (key, row[key])
+    assert row["chunks4"]["overlapped"]
 
 
 def test_rccl_collectives_one_rank():

@@ -81,3 +81,21 @@ def test_two_rank_routing_in_one_process():
         for e in engs:
             chk ^= e.stats()[1] & 0x7fffffffffffffff
         assert (held, chk) == ss.global_stats(), rnd
+
+
+@pytest.mark.parametrize("chunks", [2, 3])
+def test_chunked_round_gpu_equals_whole(chunks):
+    """The chunked round (EpidemicSim.chunks: chunk-wise claim builds over virtual ranks, dsy_sim_build_claims on a
+    chunk's config and bits) on the GPU engine at one rank gives the whole round's stores, round after round."""
+    blob, offs = make_universe(U, seed=5)
+    dev = torch.device("cuda", 0)
+    cw, cc = make_config(P, U, 0, 1, seed=17), make_config(P, U, 0, 1, seed=17, chunks=chunks)
+    ew, ec = GpuEngine(cw, blob, offs, dev), GpuEngine(cc, blob, offs, dev)
+    ew.seed(INITIAL)
+    ec.seed(INITIAL)
+    sw, sc = EpidemicSim(ew, cw, device=dev), EpidemicSim(ec, cc, device=dev, chunks=chunks)
+    for r in range(ROUNDS):
+        sw.round(r)
+        sc.round(r)
+        assert sc.global_stats() == sw.global_stats(), r
+    assert (ec.bits.cpu().numpy() == ew.bits.cpu().numpy()).all()

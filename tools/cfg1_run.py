@@ -47,7 +47,7 @@ def main():
     blob_full = torch.randint(0, 256, (total + 2 * _native.BLOB_GUARD,), device=dev, generator=g, dtype=torch.uint8)
     blob = blob_full[_native.BLOB_GUARD:]
     m, f, prefix = {"md5": (10160, 0.01, b"\x00\x01\x02\x03"), "sha1": (4096, 0.001, b"x")}[args.family]
-    out = {"family": args.family, "keys": N, "adds": args.adds, "key_bytes": total, "variants": {}}
+    out = {"family": args.family, "keys": N, "adds": args.adds, "key_bytes": total, "runs": []}
     blocks = bench._blocks(lengths, len(prefix), args.family)
     ref = None
     for lines in args.lines.split(","):
@@ -73,7 +73,7 @@ def main():
             ref = (got, fb)
         else:
             same = bool((got == ref[0]).all() and fb == ref[1])
-        rec = {"test_us": round(k_test * 1e6, 1), "add_us": round(k_add * 1e6, 1),
+        rec = {"lines": lines, "test_us": round(k_test * 1e6, 1), "add_us": round(k_add * 1e6, 1),
                "test_keys_per_s": round(N / k_test, 1), "test_wall_keys_per_s": round(N / wall, 1),
                "hbm_alg_tbs": round((total + 17 * N) / k_test / 1e12, 3),
                "int32_frac": round(blocks * bench.OPS_PER_BLOCK[args.family] / k_test / 1e12 / bench.PEAK_INT32_TOPS, 4),
@@ -82,7 +82,7 @@ def main():
             chk_bf = BloomFilter(m, f, prefix)
             rec["gpu_vs_oracle"] = bench.bloom_vs_oracle(ctx, lib, chk_bf, m, f, prefix, blob, offsets, args.check,
                                                          offsets, min(N, 5 * args.check), dev)
-        out["variants"][lines] = rec
+        out["runs"].append(rec)
         ctx.synchronize()
         del ctx
     print(json.dumps(out), flush=True)
