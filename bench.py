@@ -509,10 +509,11 @@ def tail_keys(gossip, sha1=None, heavy=None, single=None, large=None, cpu=None):
         "cfg4_sha256_add_int32_frac": {k: v.get("add_valu_frac") for k, v in (_get(large, "filters") or {}).items()}
         or None,
         "cfg1_at_capacity_md5_tests_per_s": _get(single, "md5", "at_capacity", "test_keys_per_s"),
-        "cfg2_cpu_1core_pairs_per_s": _get(cpu, "value"),
-        "cfg2_cpu_ncore": {"value": _get(cpu, "n_core", "value"), "cores": _get(cpu, "n_core", "cores"),
-                           "unit": _get(cpu, "n_core", "unit")} if _get(cpu, "n_core") else None,
     }
+    # (ahead of the gossip keys: the driver's tail of stdout keeps the last few hundred characters)
+    out = dict({"cfg2_cpu_1core_pairs_per_s": _get(cpu, "value"),
+                "cfg2_cpu_ncore": {"value": _get(cpu, "n_core", "value"), "cores": _get(cpu, "n_core", "cores"),
+                                   "unit": _get(cpu, "n_core", "unit")} if _get(cpu, "n_core") else None}, **out)
     # every in-leg GPU == CPU-oracle check that ran (None: the leg or its check did not run)
     checks = {
         "cfg2_responder_sample": _get(cpu, "gpu_matches_cpu_on_sample"),
@@ -1311,6 +1312,28 @@ def single_filter(args, ctx, lib, blob, offsets, N, dev, rank, world):
             "present_fraction": round(float(present[:n_t].float().mean().item()), 4),
             "expected_present_fraction": round(cap / n_t + f * (1 - cap / n_t), 4),
             "avg_launch_us": round(k_cap * 1e6, 1), "gpu_vs_oracle": chk}
+    # HBM traffic of the test launches from the committed single-size PMC passes (tools/cfg1_run.py under rocprofv3,
+    # profiles/pmc_traffic_cfg1.json), reported only for the kernel code they measured (tools/kernel_hash.py)
+    traffic_file = os.path.join(ROOT, "profiles", "pmc_traffic_cfg1.json")
+    if os.path.isfile(traffic_file):
+        from tools.kernel_hash import kernel_sha
+        with open(traffic_file) as f:
+            recs = json.load(f)
+        lib_path = os.environ.get("DSY_LIB_PATH") or _native.LIB_PATH
+        for name in ("md5", "sha1"):
+            rec, rt = recs.get(name), out.get(name, {}).get("roofline_test")
+            if not rec or rt is None:
+                continue
+            now = kernel_sha(lib_path, rec["symbol"])
+            alg = int(lengths.sum().item()) + 17 * N
+            if now is not None and now == rec.get("kernel_sha") and int(rec.get("keys", -1)) == N:
+                rt["traffic"] = rec["hbm_bytes_per_launch"]
+                rt["traffic_over_algorithmic"] = round(rec["hbm_bytes_per_launch"] / alg, 3)
+                rt["traffic_source"] = "profiles/pmc_traffic_cfg1.json (%s; same kernel code, sha256 %s)" % (
+                    rec.get("round"), now[:16])
+            else:
+                rt["traffic"] = None
+                rt["traffic_source"] = "not reported: profiles/pmc_traffic_cfg1.json measured another build or size"
     if rank == 0 and world == 1:
         out["cpu_baseline"] = single_filter_cpu(blob, offsets)
     return out

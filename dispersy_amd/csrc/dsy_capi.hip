@@ -179,6 +179,10 @@ struct dsy_ctx {
     // upload per append; the next append synchronises the stream before it writes here again
     uint8_t* in_stage = nullptr;
     size_t in_stage_bytes = 0;
+    // pinned staging of store_flush's small table (metas, segments, slack, starts, counts): an asynchronous upload; every
+    // flush synchronises before it returns, so the next one may rewrite it
+    uint8_t* flush_pin = nullptr;
+    size_t flush_pin_bytes = 0;
     // the simulator's device-side counters (work of build / respond, pairs tested, response overflow): the calls
     // enqueue without reading them back; the synchronising accessors fold them (sim_collect)
     void* sim_acc = nullptr;
@@ -447,7 +451,7 @@ int run_bloom(dsy_ctx* c, BloomOp op, const dsy_bloom_params* p, const uint8_t* 
     if (op != BloomOp::Indices && n >= kLenSortMin) {
         void *bins, *tasks;
         int rc2;
-        if ((rc2 = ws_get(c, "len_bins", 1024 * 4, &bins))) return rc2;
+        if ((rc2 = ws_get(c, "len_bins", kLenSortBins * 4, &bins))) return rc2;
         if ((rc2 = ws_get(c, "len_tasks", n * sizeof(PairTask), &tasks))) return rc2;
         const bool wide = p->hash_kind >= DSY_SHA384;
         LenSort ls{p->prefix_len, wide ? 128u : 64u, wide ? 16u : 8u};
@@ -578,6 +582,7 @@ int dsy_ctx_destroy(dsy_ctx* c) {
         if (c->out_pin) hipHostFree(c->out_pin);
         if (c->pinned) hipHostFree(c->pinned);
         if (c->in_stage) hipHostFree(c->in_stage);
+        if (c->flush_pin) hipHostFree(c->flush_pin);
         hipStreamDestroy(c->stream);
     }
     delete c;
@@ -1248,13 +1253,9 @@ static int store_flush(dsy_ctx* c, const dsy_store* cs) {
         gap_before.push_back(gaps);
         gaps += extra.back();
     }
-    // the in-place tails need the first ranks; when they would move more than one whole merge does, the whole merge
-    // runs instead (its rows are ordered again, with the slack entries placed)
-    bool tried_fast = false;
-again:
-    const uint64_t total = fast ? P : P + gaps;
-    // 256-byte aligned parts: the metas | segments | gap_before | starts | counts | first ranks | the ordered rows | the
-    // sort's scratch
+    // 256-byte aligned parts: the metas | segments | gap_before | starts | counts | first ranks | the ordered rows (with
+    // room for the whole merge's slack entries) | the sort's scratch
+    const uint64_t total = P + gaps;
     const size_t b_m = ((size_t)nm * 4 + 255) / 256 * 256, b_u = ((size_t)nm * 8 + 255) / 256 * 256;
     const size_t b_tab = b_m + 2 * b_u + 4 * b_u;
     const size_t b_scr = pend_order_scratch(P), b_rows = ((size_t)total * sizeof(IngestRow) + 255) / 256 * 256;
@@ -1268,21 +1269,43 @@ again:
     uint64_t* d_cnt = (uint64_t*)(tab + b_m + 4 * b_u);
     uint64_t* d_first = (uint64_t*)(tab + b_m + 5 * b_u);
     IngestRow* d_rows = (IngestRow*)(tab + b_tab);
-    {  // one upload of the table (the first ranks are written on the device)
-        std::vector<uint8_t> h(b_m + 5 * b_u);
-        std::memcpy(h.data(), metas.data(), (size_t)nm * 4);
-        std::memcpy(h.data() + b_m, segs.data(), (size_t)nm * 16);
-        std::memcpy(h.data() + b_m + 2 * b_u, gap_before.data(), (size_t)nm * 8);
-        std::memcpy(h.data() + b_m + 3 * b_u, starts.data(), (size_t)nm * 8);
-        std::memcpy(h.data() + b_m + 4 * b_u, cnt.data(), (size_t)nm * 8);
-        HIP_TRY(hipMemcpyAsync(tab, h.data(), h.size(), hipMemcpyHostToDevice, c->stream));
+    {  // one asynchronous upload of the table through pinned staging (the first ranks are written on the device)
+        const size_t hb = b_m + 5 * b_u;
+        if (c->flush_pin_bytes < hb) {
+            if (c->flush_pin) hipHostFree(c->flush_pin);
+            c->flush_pin = nullptr;
+            c->flush_pin_bytes = 0;
+            if (hipHostMalloc((void**)&c->flush_pin, std::max<size_t>(hb, 4096), hipHostMallocDefault) != hipSuccess) {
+                c->flush_pin = nullptr;
+                return fail(DSY_ENOMEM, "hipHostMalloc for the index flush table failed");
+            }
+            c->flush_pin_bytes = std::max<size_t>(hb, 4096);
+        }
+        uint8_t* h = c->flush_pin;
+        std::memcpy(h, metas.data(), (size_t)nm * 4);
+        std::memcpy(h + b_m, segs.data(), (size_t)nm * 16);
+        std::memcpy(h + b_m + 2 * b_u, gap_before.data(), (size_t)nm * 8);
+        std::memcpy(h + b_m + 3 * b_u, starts.data(), (size_t)nm * 8);
+        std::memcpy(h + b_m + 4 * b_u, cnt.data(), (size_t)nm * 8);
+        HIP_TRY(hipMemcpyAsync(tab, h, hb, hipMemcpyHostToDevice, c->stream));
     }
     fc.mark("table");
-    HIP_TRY(launch_pend_order(s->d_pend_meta, s->d_pend_gt, P, s->pend_glo, s->pend_ghi, (const uint32_t*)tab, d_segs,
-                              fast ? nullptr : d_gapb, nm, s->pend_base, (uint8_t*)d_rows + b_rows, b_scr, d_rows,
-                              c->stream));
-    fc.mark("order");
+    // the pending entries in index order (with_gaps: laid out for the whole merge, each meta's rows after the slack
+    // of the metas before it) and, for the in-place path, each meta's first new entry's place (first).  (A one-workgroup
+    // bitonic sort in LDS for batches of <= 16 K entries was measured and dropped: 176-184 us per 10 k-entry flush
+    // against 42 us for the radix sorts, gpurun_out r6c1d)
+    auto order = [&](bool with_gaps, uint64_t* first) -> int {
+        HIP_TRY(launch_pend_order(s->d_pend_meta, s->d_pend_gt, P, s->pend_glo, s->pend_ghi, (const uint32_t*)tab,
+                                  d_segs, with_gaps ? d_gapb : nullptr, nm, s->pend_base, (uint8_t*)d_rows + b_rows,
+                                  b_scr, d_rows, c->stream));
+        if (first) HIP_TRY(launch_first_rank(s->d_live_gt, s->d_live_row, d_rows, d_starts, d_cnt, nm, first, c->stream));
+        return DSY_OK;
+    };
+    bool ordered_whole = false;  // d_rows hold the whole merge's layout already
+whole:
     if (!fast) {
+        if (!ordered_whole && (rc = order(true, nullptr))) return rc;
+        fc.mark("order");
         std::map<uint32_t, std::pair<uint64_t, uint64_t>> cm;
         for (uint32_t r = 0; r < nm; ++r) {
             HIP_TRY(launch_gap_rows(d_rows + starts[r] + cnt[r] + gap_before[r], extra[r], ends[r], c->stream));
@@ -1298,7 +1321,8 @@ again:
     // in place: each meta's tail [p, b) -- p: its first new entry's position -- is copied aside and merged with the
     // meta's new entries back into [p, b + k), inside the region's slack
     std::vector<uint64_t> first(nm);
-    HIP_TRY(launch_first_rank(s->d_live_gt, s->d_live_row, d_rows, d_starts, d_cnt, nm, d_first, c->stream));
+    if ((rc = order(false, d_first))) return rc;
+    fc.mark("order");
     HIP_TRY(hipMemcpyAsync(first.data(), d_first, (size_t)nm * 8, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     fc.mark("first_rank");
@@ -1308,10 +1332,12 @@ again:
             tail_max = std::max(tail_max, segs[2 * r + 1] - first[r]);
             tail_sum += segs[2 * r + 1] - first[r];
         }
-    if (!tried_fast && 64 * tail_sum > 32 * s->n_phys) {  // 64 B per tail entry (copied out and back) vs 32
-        tried_fast = true;
+    if (64 * tail_sum > 32 * s->n_phys) {  // 64 B per tail entry (copied out and back) vs 32: the whole merge instead
         fast = false;
-        goto again;
+        // (with no slack before any meta's rows the in-place order is the whole merge's layout already)
+        ordered_whole = true;
+        for (uint32_t r = 0; r < nm; ++r) ordered_whole = ordered_whole && gap_before[r] == 0;
+        goto whole;
     }
     void* d_tmp;
     if ((rc = ws_get(c, "live_merge", P * 8 + 64 + tail_max * 16, &d_tmp))) return rc;

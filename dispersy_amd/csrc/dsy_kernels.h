@@ -104,7 +104,8 @@ struct LenSort {
     uint32_t base_lo = 0;    // the blob's address mod 128 (line_mode)
 };
 hipError_t launch_len_sort(const LenSort& s, const uint64_t* offsets, const uint64_t* rows, const RowRec* rec, uint64_t n,
-                           uint32_t* d_bins /* 1024 */, PairTask* d_tasks, uint32_t max_grid, hipStream_t stream);
+                           uint32_t* d_bins /* kLenSortBins */, PairTask* d_tasks, uint32_t max_grid, hipStream_t stream);
+static constexpr uint32_t kLenSortBins = 4096;  // bins of the length sort (dsy_bloom_kernels.hip kLenBins)
 
 // ------------------------------------------------------------------------------------------ responder
 // One hashing wave-task as DSY_PAIR_TRACE records it: where it ran (HW_ID, XCC_ID), when (s_memrealtime, 100 MHz)
@@ -391,7 +392,6 @@ hipError_t launch_first_rank(const uint64_t* live_gt, const uint64_t* live_row, 
                              const uint64_t* starts, const uint64_t* counts, uint32_t nm, uint64_t* out,
                              hipStream_t stream);
 hipError_t launch_rows_seg(IngestRow* rows, uint64_t k, uint64_t sa, uint64_t sb, hipStream_t stream);
-
 // ---------------------------------------------------------------------------------------- simulator
 static constexpr uint32_t kSimFilterWordsMax = 2048;  // m <= 65536 bits
 static constexpr uint32_t kSimRespMax = DSY_SIM_RESP_MAX;
