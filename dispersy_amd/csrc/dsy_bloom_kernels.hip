@@ -29,38 +29,26 @@ namespace dsy {
 //   1 <= a <= 64 lag 1, shift 0: e0 = a, stage s hashes blocks 2s - 1, 2s (stage 0's first slot is empty)
 //   a > 64       lag 0, shift 1: e0 = a - 64; stage 0 stages line 1 and, as its carry, line 0's last 64 bytes (the
 //                message starts there), so stage s hashes blocks 2s, 2s + 1
-// A key takes line_stages(nb, a) = ceil((nb + lag) / 2) stages.  The length sort (k_len_*, LenSort::line_mode) orders
-// keys by (block slots, lag, e0), so a wave's lanes run the same slots and -- for keys of up to ~1.9 KB -- read their
-// window at the same row offset (a wave whose keys differ in e0 -- longer keys share the sort's last bin, small
-// unsorted batches -- still hashes right, with more LDS bank conflicts).  The window is read with ds_read_b128 at its
-// dword-aligned start (lds_read33: HSA runs the LDS in unaligned mode, tools/lds_unaligned_probe.hip), then one
-// alignbyte per word.  Rows are 208 bytes (13 16-byte slots, the last one unused): an odd slot
-// stride puts the 16 lanes of an aligned 16-byte access in 16 distinct bank groups (192-byte rows put four lanes in
-// each -- 4-way conflicts on every carry copy and window read, measured 345 M conflict cycles per 10 M-key launch).
+// A key takes line_stages(nb, a) = ceil((nb + lag) / 2) stages; the length sort (k_len_*, LenSort::line_mode) orders
+// keys by that count, so a wave's lanes run the same number of stages.
 struct LineStaging {
-    static constexpr int kRowBytes = 208;                      // [carry 64 B][line 128 B][unused 16 B] per key
-    static constexpr int kInsts = 64 * kRowBytes / 1024;       // 13 DMA wave-instructions cover the wave's rows
-    static constexpr int kWaveBytes = 64 * kRowBytes;          // 13 KiB per wave
-    static constexpr uint32_t kSlots = kRowBytes / 16;
+    static constexpr int kRowBytes = 192;                      // [carry 64 B][line 128 B] per key
+    static constexpr int kInsts = 64 * kRowBytes / 1024;       // 12 DMA wave-instructions cover the wave's rows
+    static constexpr int kWaveBytes = 64 * kRowBytes;          // 12 KiB per wave
 };
 
 __host__ __device__ __forceinline__ uint32_t line_lag(uint32_t a) { return (a >= 1u && a <= 64u) ? 1u : 0u; }
 __host__ __device__ __forceinline__ uint32_t line_stages(uint32_t nb, uint32_t a) { return (nb + line_lag(a) + 1u) / 2u; }
-// where in its row a key's stage window starts (1..64): see the table above
-__host__ __device__ __forceinline__ uint32_t line_e0(uint32_t a) {
-    return a + 64u - 64u * line_lag(a) - (a > 64u ? 128u : 0u);
-}
 
 // The pieces one lane moves for its wave's 64 keys.  DMA wave-instruction i writes LDS bytes [1024 i, +1024) of the
-// wave's buffer, lane t the 16 bytes at 1024 i + 16 t: 16-byte slot g = 64 i + t is piece g % 13 of key g / 13's row
-// (pieces 0-3 the carry, 4-11 the line, 12 unused).  Per piece: idx = its stage-0 address in 16-byte units from the
-// wave-uniform base (stage s: + 8 s); nls: stage s >= 1 is live while s < nls (16 bits each, two per register: keys
-// under 8 MiB, hash_key_dma_packed checks); m0: bit i = piece i is live at stage 0 (the first line's pieces before the
-// message, and the carry pieces of keys with shift 1).  21 VGPRs.
+// wave's buffer, lane t the 16 bytes at 1024 i + 16 t: 16-byte slot g = 64 i + t is piece g % 12 of key g / 12's row
+// (pieces 0-3 the carry, 4-11 the line).  Per piece: idx = its stage-0 address in 16-byte units from the wave-uniform
+// base (stage s: + 8 s); lim: stage s >= 1 is live while 128 s < lim; m0: bit i = piece i is live at stage 0 (the
+// first line's pieces before the message, and the carry pieces of keys with shift 1).  25 VGPRs.
 struct DmaPackedPieces {
     using G = LineStaging;
     uint32_t idx[G::kInsts];
-    uint32_t nls2[(G::kInsts + 1) / 2];
+    uint32_t lim[G::kInsts];
     uint32_t m0;
     // line: the key's first line (from the wave base, < 2^28); lo / hi: the bytes to load, [lo, hi) from that line's
     // start (the prefix bytes are merged in registers, not loaded)
@@ -70,30 +58,23 @@ struct DmaPackedPieces {
         xs[lane] = make_uint4(line, shift, lo, hi);
         m0 = 0;
 #pragma unroll
-        for (int i = 0; i < (G::kInsts + 1) / 2; ++i) nls2[i] = 0;
-#pragma unroll
         for (int i = 0; i < G::kInsts; ++i) {
             const uint32_t g = 64u * i + lane;
-            const uint32_t p = g / G::kSlots, k = g % G::kSlots;
+            const uint32_t p = g / 12u, k = g % 12u;
             const uint4 v = xs[p];
             uint32_t start0, live0;  // the piece's stage-0 byte range [start0, +16) from the key's first line
-            uint32_t nls = 0u;
-            if (k == 12) {           // the row's unused slot
-                start0 = 0u;
-                idx[i] = 0u;
-                live0 = 0u;
-            } else if (k < 4) {      // carry piece: line 0's bytes 64 + 16 k, staged only at stage 0 (shift 1)
+            if (k < 4) {             // carry piece: line 0's bytes 64 + 16 k, staged only at stage 0 (shift 1)
                 start0 = 64u + 16u * k;
                 idx[i] = 8u * v.x + 4u + k;
+                lim[i] = 0u;
                 live0 = v.y;
             } else {
                 const uint32_t c = k - 4u;
                 start0 = 128u * v.y + 16u * c;
                 idx[i] = 8u * (v.x + v.y) + c;
-                nls = v.w > start0 ? (v.w - start0 + 127u) >> 7 : 0u;  // stages s with 128 s < v.w - start0
+                lim[i] = v.w > start0 ? v.w - start0 : 0u;
                 live0 = 1u;
             }
-            nls2[i / 2] |= nls << (16 * (i & 1));
             live0 &= (start0 < v.w) & (start0 + 16u > v.z);
             m0 |= live0 << i;
         }
@@ -105,8 +86,7 @@ struct DmaPackedPieces {
         if constexpr (SKIP) return;
 #pragma unroll
         for (int i = 0; i < G::kInsts; ++i) {
-            const uint32_t nls = (i & 1) ? nls2[i / 2] >> 16 : nls2[i / 2] & 0xffffu;
-            const bool live = s ? s < nls : ((m0 >> i) & 1u) != 0u;
+            const bool live = s ? 128u * s < lim[i] : ((m0 >> i) & 1u) != 0u;
             if (live)
                 __builtin_amdgcn_global_load_lds((const void*)(base + ((uint64_t)(idx[i] + (s << 3)) << 4)),
                                                  (__attribute__((address_space(3))) void*)(uintptr_t)(lds + i * 1024),
@@ -114,39 +94,6 @@ struct DmaPackedPieces {
         }
     }
 };
-
-// 33 consecutive dwords from LDS byte address `addr` (4-byte aligned) -- eight ds_read_b128 and a ds_read_b32 -- and
-// the row's line tail (the next stage's carry: four aligned ds_read_b128 at `tail`), in one block that also waits for
-// them (the compiler cannot count asm loads): one LDS round trip per stage
-__device__ __forceinline__ void lds_read33(uint32_t addr, uint32_t tail, uint32_t* d, uint4* t) {
-    uint4 a0, a1, a2, a3, a4, a5, a6, a7;
-    uint32_t a8;
-    asm volatile(
-        "ds_read_b128 %0, %13\n\t"
-        "ds_read_b128 %1, %13 offset:16\n\t"
-        "ds_read_b128 %2, %13 offset:32\n\t"
-        "ds_read_b128 %3, %13 offset:48\n\t"
-        "ds_read_b128 %4, %13 offset:64\n\t"
-        "ds_read_b128 %5, %13 offset:80\n\t"
-        "ds_read_b128 %6, %13 offset:96\n\t"
-        "ds_read_b128 %7, %13 offset:112\n\t"
-        "ds_read_b32 %8, %13 offset:128\n\t"
-        "ds_read_b128 %9, %14\n\t"
-        "ds_read_b128 %10, %14 offset:16\n\t"
-        "ds_read_b128 %11, %14 offset:32\n\t"
-        "ds_read_b128 %12, %14 offset:48\n\t"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(a3), "=&v"(a4), "=&v"(a5), "=&v"(a6), "=&v"(a7), "=&v"(a8),
-          "=&v"(t[0]), "=&v"(t[1]), "=&v"(t[2]), "=&v"(t[3])
-        : "v"(addr), "v"(tail)
-        : "memory");
-    const uint4 a[8] = {a0, a1, a2, a3, a4, a5, a6, a7};
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        d[4 * k] = a[k].x; d[4 * k + 1] = a[k].y; d[4 * k + 2] = a[k].z; d[4 * k + 3] = a[k].w;
-    }
-    d[32] = a8;
-}
 
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 #pragma unroll
@@ -173,20 +120,14 @@ __device__ __forceinline__ void hash_key_dma_packed(const KeyView& kv, H& st, ui
     const uint64_t base = (uint64_t)(uintptr_t)kv.key - r;
     const uint64_t wline = wave_min_u64(base >> 7);  // the wave's lowest line: piece offsets are 32-bit from there
     const uint64_t span = (base >> 7) - wline;
-    // (and keys of 8 MiB or more: the pieces' 16-bit stage counts)
-    if (__builtin_amdgcn_readfirstlane((uint32_t)(__ballot(span >= (1ull << 28) || total >= (1u << 23)) != 0))) {
+    if (__builtin_amdgcn_readfirstlane((uint32_t)(__ballot(span >= (1ull << 28)) != 0))) {
         hash_key<H>(kv, st);
         return;
     }
     const uint8_t* wbase = (const uint8_t*)(uintptr_t)(wline << 7);
-    const uint32_t a0 = (uint32_t)base & 127u;
-    // the wave-uniform window: the first lane with key bytes sets it; lanes without any (idle lanes, empty keys: their
-    // message is the prefix, merged in registers) take it too, whatever their address
-    const uint64_t has = __ballot(kv.len > 0);
-    const uint32_t a_w = (uint32_t)__shfl((int)a0, has ? (int)__builtin_ctzll(has) : 0, 64);
-    const uint32_t a = kv.len > 0 ? a0 : a_w;
+    const uint32_t a = (uint32_t)base & 127u;
     const uint32_t lag = line_lag(a), shift = a > 64u ? 1u : 0u;
-    const uint32_t e0 = line_e0(a);  // 1..64
+    const uint32_t e0 = a + 64u - 64u * lag - 128u * shift;  // 1..64
     const uint32_t nst = wave_max_uniform(line_stages(nb, a));
     const uint32_t tmin = wave_min_uniform(total);
     const uint32_t lag_min = wave_min_uniform(lag);  // the slot's highest block is 2 s + bb - lag_min
@@ -195,20 +136,25 @@ __device__ __forceinline__ void hash_key_dma_packed(const KeyView& kv, H& st, ui
     st.init();
     const uint32_t lds = lds_local(lds_wave);
     const uint8_t* row = lds_wave + lane * G::kRowBytes;
-    const uint32_t win = lds + lane * G::kRowBytes + (e0 & ~3u);  // the window's first dword (LDS address)
+    const uint32_t* win = (const uint32_t*)(row + (e0 & ~3u));
     const uint32_t sh = e0 & 3u;
     if (nst) dl.template issue<MODE == 1>(0, wbase, lds);
     for (uint32_t s = 0; s < nst; ++s) {
         __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): stage s has landed
         __builtin_amdgcn_wave_barrier();
         uint32_t d[33];
-        uint4 t[4];  // the line's last 64 bytes: the next stage's carry
-        lds_read33(win, lds + lane * G::kRowBytes + 128, d, t);  // (waited: the line slots are free again)
+#pragma unroll
+        for (int i = 0; i < 33; ++i) d[i] = win[i];
+        // the line's last 64 bytes: the next stage's carry (four named registers: an array of them was kept in
+        // scratch by the compiler)
+        const uint4 t0 = *(const uint4*)(row + 128), t1 = *(const uint4*)(row + 144);
+        const uint4 t2 = *(const uint4*)(row + 160), t3 = *(const uint4*)(row + 176);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the line slots are free again
         __builtin_amdgcn_wave_barrier();
-        *(uint4*)(row) = t[0];  // (the DMA below writes only the line slots)
-        *(uint4*)(row + 16) = t[1];
-        *(uint4*)(row + 32) = t[2];
-        *(uint4*)(row + 48) = t[3];
+        *(uint4*)(row) = t0;  // (the DMA below writes only the line slots)
+        *(uint4*)(row + 16) = t1;
+        *(uint4*)(row + 32) = t2;
+        *(uint4*)(row + 48) = t3;
         if (s + 1 < nst) dl.template issue<MODE == 1>(s + 1, wbase, lds);
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb) {
@@ -239,9 +185,9 @@ static constexpr size_t kLineWaveBytes = LineStaging::kWaveBytes;
 // first one of a lag-1 wave, the last one of an odd count) is skipped as a whole instead of hashed for a few lanes
 __device__ __forceinline__ uint32_t len_bin(uint64_t off, uint64_t len, const LenSort& s) {
     uint32_t units = n_blocks(s.plen + (uint32_t)len, s.blk, s.lenb);
-    if (s.line_mode) {  // (slots, lag, e0): 64 bins per slot count and lag
-        const uint32_t a = (s.base_lo + (uint32_t)off - s.plen) & 127u, lag = line_lag(a);
-        units = (2u * (units + lag) + lag) * 64u + (line_e0(a) - 1u);
+    if (s.line_mode) {
+        const uint32_t lag = line_lag((s.base_lo + (uint32_t)off - s.plen) & 127u);
+        units = 2u * (units + lag) + lag;
     }
     return kLenBins - 1u - min(units, kLenBins - 1u);
 }
@@ -280,31 +226,20 @@ __global__ void __launch_bounds__(256) k_len_hist(LenSort s, const uint64_t* __r
         if (h[i]) atomicAdd(&hist[i], h[i]);
 }
 
-// pass 2: exclusive scan of the bins (one workgroup of 1024 threads, kLenBins / 1024 consecutive bins each)
-static constexpr uint32_t kScanThreads = 1024, kScanPer = kLenBins / kScanThreads;
-__global__ void __launch_bounds__(kScanThreads) k_len_scan(uint32_t* __restrict__ hist) {
-    __shared__ uint32_t part[kScanThreads];
+// pass 2: exclusive scan of the bins (one workgroup of kLenBins threads)
+__global__ void __launch_bounds__(kLenBins) k_len_scan(uint32_t* __restrict__ hist) {
+    __shared__ uint32_t part[kLenBins];
     const uint32_t t = threadIdx.x;
-    uint32_t v[kScanPer], sum = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < kScanPer; ++j) {
-        v[j] = hist[t * kScanPer + j];
-        sum += v[j];
-    }
-    part[t] = sum;
+    const uint32_t v = hist[t];
+    part[t] = v;
     __syncthreads();
-    for (uint32_t d = 1; d < kScanThreads; d <<= 1) {
+    for (uint32_t d = 1; d < kLenBins; d <<= 1) {
         const uint32_t add = t >= d ? part[t - d] : 0u;
         __syncthreads();
         part[t] += add;
         __syncthreads();
     }
-    uint32_t run = part[t] - sum;
-#pragma unroll
-    for (uint32_t j = 0; j < kScanPer; ++j) {
-        hist[t * kScanPer + j] = run;
-        run += v[j];
-    }
+    hist[t] = part[t] - v;
 }
 
 // pass 3: scatter task records; each workgroup reserves its bins' ranges with one global atomic per bin
@@ -482,12 +417,12 @@ hipError_t launch_or_reduce(const uint32_t* parts, uint32_t n_parts, uint64_t wo
 // ------------------------------------------------------------------------------------------ dispatch
 hipError_t launch_len_sort(const LenSort& s, const uint64_t* offsets, const uint64_t* rows, const RowRec* rec, uint64_t n,
                            uint32_t* d_bins, PairTask* d_tasks, uint32_t max_grid, hipStream_t stream) {
-    hipError_t e = hipMemsetAsync(d_bins, 0, kLenBins * 4, stream);  // (d_bins: kLenBins entries)
+    hipError_t e = hipMemsetAsync(d_bins, 0, kLenBins * 4, stream);
     if (e != hipSuccess) return e;
     const uint64_t want = (n + 255) / 256;
     const uint32_t grid = (uint32_t)(want < max_grid ? (want ? want : 1) : max_grid);
     hipLaunchKernelGGL(k_len_hist, dim3(grid), dim3(256), 0, stream, s, offsets, rows, rec, n, d_bins);
-    hipLaunchKernelGGL(k_len_scan, dim3(1), dim3(kScanThreads), 0, stream, d_bins);
+    hipLaunchKernelGGL(k_len_scan, dim3(1), dim3(kLenBins), 0, stream, d_bins);
     const uint64_t chunks = (n + kScatterChunk - 1) / kScatterChunk;
     const uint32_t sgrid = (uint32_t)(chunks < max_grid ? (chunks ? chunks : 1) : max_grid);
     hipLaunchKernelGGL(k_len_scatter, dim3(sgrid), dim3(256), 0, stream, s, offsets, rows, rec, n, d_bins, d_tasks);
@@ -502,8 +437,7 @@ hipError_t launch_len_sort(const LenSort& s, const uint64_t* offsets, const uint
 int bloom_staging(const BloomLaunch& L) {
     if (!(L.kind == DSY_MD5 || L.kind == DSY_SHA1) || L.prm_prefix_len > 4) return 0;
     const uint64_t fbytes = L.use_lds ? (uint64_t)L.nwords * 4 : 0;
-    // (3 x (4 x 13 KiB + filter) <= 160 KiB: filters of <= 1301 bytes; the MTU filter takes 1272)
-    if (((L.line_kinds >> L.kind) & 1u) && 3 * (4 * (uint64_t)kLineWaveBytes + fbytes) <= 160 * 1024) return 2;
+    if (((L.line_kinds >> L.kind) & 1u) && fbytes <= 5 * 1024) return 2;
     return fbytes <= 16 * 1024 ? 1 : 0;
 }
 

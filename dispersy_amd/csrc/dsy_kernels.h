@@ -105,7 +105,7 @@ struct LenSort {
 };
 hipError_t launch_len_sort(const LenSort& s, const uint64_t* offsets, const uint64_t* rows, const RowRec* rec, uint64_t n,
                            uint32_t* d_bins /* kLenSortBins */, PairTask* d_tasks, uint32_t max_grid, hipStream_t stream);
-static constexpr uint32_t kLenSortBins = 4096;  // bins of the length sort (dsy_bloom_kernels.hip kLenBins)
+static constexpr uint32_t kLenSortBins = 1024;  // bins of the length sort (dsy_bloom_kernels.hip kLenBins)
 
 // ------------------------------------------------------------------------------------------ responder
 // One hashing wave-task as DSY_PAIR_TRACE records it: where it ran (HW_ID, XCC_ID), when (s_memrealtime, 100 MHz)

@@ -231,3 +231,32 @@ def test_filter_build_or_modes(monkeypatch, or_mode, m, f, prefix, n):
         assert got[:len(bf.bytes)] == ref.to_bytes()
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("lines", [0, 3], ids=["windows", "lines"])
+@pytest.mark.parametrize("m,f,prefix,n_add", [(10160, 0.01, b"\x00\x01\x02\x03", 1500), (4096, 0.001, b"x", 300),
+                                              (10160, 0.01, b"", 1500), (10160, 0.01, b"\x05" * 5, 1500)],
+                         ids=["md5-p4", "sha1-p1", "md5-p0", "md5-p5"])
+def test_single_filter_staging_variants(monkeypatch, lines, m, f, prefix, n_add):
+    """Single-filter membership over >= kLenSortMin keys (length-sorted, LDS-DMA staged k_bloom) under both staging
+    variants (DSY_BLOOM_LINES: 0 = each key's own window, 3 = whole 128-byte lines for MD5 and SHA-1, with the 5-byte
+    prefix falling back to windows) against the oracle: unaligned packed keys of 1..1500 bytes, a filter that is not
+    saturated, so membership tells keys apart."""
+    monkeypatch.setenv("DSY_BLOOM_LINES", str(lines))
+    ctx = _native.Context(0)
+    try:
+        n = 40_000
+        blob, off = random_packets(9000 + n_add + lines, n, 1, 1500)
+        bf = BloomFilter(m, f, prefix)
+        filt = ctx.bloom_add(bf.params, blob, off[:n_add + 1], b"\x00" * (len(bf.bytes) + (-len(bf.bytes)) % 4))
+        ref = OracleBloom.from_m_f(m, f, prefix)
+        keys = [blob[int(off[i]):int(off[i + 1])] for i in range(n)]
+        ref.add_keys(keys[:n_add])
+        assert filt[:len(bf.bytes)] == ref.to_bytes()
+        got = ctx.bloom_test(bf.params, blob, off, filt)
+        want = np.array([k in ref for k in keys], dtype=np.uint8)
+        assert got[:n_add].all()
+        assert 0 < int(want[n_add:].sum()) < n - n_add
+        assert (got.astype(np.uint8) == want).all()
+    finally:
+        ctx.close()
