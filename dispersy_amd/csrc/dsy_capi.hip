@@ -181,8 +181,9 @@ struct dsy_ctx {
     // upload per append; the next append synchronises the stream before it writes here again
     uint8_t* in_stage = nullptr;
     size_t in_stage_bytes = 0;
-    // pinned staging of store_flush's small table (metas, segments, slack, starts, counts): an asynchronous upload; every
-    // flush synchronises before it returns, so the next one may rewrite it
+    // pinned staging of store_flush's small table (metas, segments, slack, starts, counts): an asynchronous upload; a
+    // flush only has work after an append, and every append synchronises the stream first, so the next flush may
+    // rewrite it
     uint8_t* flush_pin = nullptr;
     size_t flush_pin_bytes = 0;
     // the simulator's device-side counters (work of build / respond, pairs tested, response overflow): the calls
@@ -1081,6 +1082,8 @@ static std::pair<uint64_t, uint64_t> seg_or_place(const dsy_store* s, uint32_t m
 
 static int spare_reserve(dsy_store* s, uint64_t need, uint64_t have) {
     if (s->spare_cap >= need) return DSY_OK;
+    // (merges do not wait on the host: an earlier one may still read the buffer pair being replaced)
+    if (s->spare_gt || s->spare_row) HIP_TRY(hipStreamSynchronize(s->ctx->stream));
     store_release(s, s->spare_gt);
     store_release(s, s->spare_row);
     s->spare_gt = s->spare_row = nullptr;
@@ -1135,8 +1138,10 @@ static int live_merge(dsy_ctx* c, dsy_store* s, const IngestRow* d_rows, uint64_
     HIP_TRY(launch_ingest_merge(s->d_live_gt, s->d_live_row, s->n_phys, d_rows, a, d_rank, s->spare_gt, s->spare_row,
                                 check_present ? d_present : nullptr, c->max_grid, c->stream));
     unsigned int present = 0;
-    if (check_present) HIP_TRY(hipMemcpyAsync(&present, d_present, 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (check_present) {  // (otherwise no host wait: the index's next reader is stream-ordered behind the merge)
+        HIP_TRY(hipMemcpyAsync(&present, d_present, 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
     if (present) return fail(DSY_EINVAL, "a row to insert is in the live index already");
     spare_swap(s);
     // segments: a meta's segment moves by every entry of the smaller metas and grows by its own live ones; a meta new
@@ -1363,7 +1368,7 @@ whole:
         moved += L;
         s->segs[metas[r]].second += cnt[r];
     }
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    // (no host wait: the index's next reader is stream-ordered behind the merges)
     fc.mark("tail_merge");
     fc.done(P, "in_place");
     s->n_live += P;

@@ -31,25 +31,26 @@ def pooled_ctx(request, monkeypatch):
     ctx.close()
 
 
-@pytest.mark.parametrize("one_byte", [False, True], ids=["prefixes0-5", "prefix1"])
-@pytest.mark.parametrize("window", [0, 256, 16384])
-@pytest.mark.parametrize("skew", [False, "dense"])
-def test_pooled_families_vs_oracle(pooled_ctx, skew, window, one_byte):
-    """one_byte: every claim's prefix is 1 byte (every reference claim), so the pooled MD5 / SHA-1 families hash the
-    line copy's padded messages (k_pair_test<..., POOL, PADDED>)."""
+_WORLD = {}  # (skew, one_byte) -> the rows, the sqlite oracle and the claims: the same for every mode and window
+
+
+def _world(skew, one_byte):
+    """The store's rows and its sqlite copy, 72 claims (filters built on the device and by the oracle) and the
+    oracle's answers -- none depends on the pooling mode or the window, so every (mode, window) case of one
+    (skew, one_byte) shares them (the Python oracle's filter builds and sqlite walks are most of the test's time)."""
+    key = (skew, one_byte)
+    if key in _WORLD:
+        return _WORLD[key]
     seed = 3 if skew is False else 4
     rows, conn = build(seed, 30_000, 120_000 if skew is False else 5_000, skew)
-    store = SyncStore.from_rows(rows, ctx=pooled_ctx)
     gt_now = 120_100 if skew is False else 30_100
     chosen = [m for m in METAS if m[0] in ("a", "d")]
-    served = [MetaMessage(n, i, SyncDistribution(d, p, None)) for n, i, d, p, _ in chosen]
     served_oracle = [dict(name=n, id=i, direction=d, priority=p, pruning=None) for n, i, d, p, _ in chosen]
-    com = SyncCommunity(store, served, global_time=gt_now)
     rng = np.random.Generator(np.random.PCG64(91 + seed))
     packets = {r[0]: r[4] for r in rows}
     # SHA-1 / MD5 / SHA-256 (pooled) and SHA-512 (never pooled) claims in one call
     shapes = [(4096, 0.001), (10160, 0.01), (1 << 15, 0.01), (1 << 16, 0.0001)]
-    reqs, oracle_blooms = [], []
+    reqs, want = [], {}
     for q in range(72):
         modulo = int(rng.choice([1, 1, 7, 331]))
         offset = int(rng.integers(0, modulo))
@@ -62,15 +63,30 @@ def test_pooled_families_vs_oracle(pooled_ctx, skew, window, one_byte):
         bf.add_keys(known)
         ob.add_keys(known)
         reqs.append(ClaimRequest(lo, hi, modulo, offset, bf))
-        oracle_blooms.append(ob)
+        for limit in (5120, 1 << 40):
+            want[q, limit] = sync_ref.respond_lists(conn, served_oracle, (lo, hi, offset, modulo), ob, gt_now, limit,
+                                                    False)
     assert {bf.hash_name for bf in (r.bloom_filter for r in reqs)} == {"md5", "sha1", "sha256", "sha512"}
+    conn.close()
+    _WORLD[key] = (rows, chosen, gt_now, reqs, want)
+    return _WORLD[key]
+
+
+@pytest.mark.parametrize("one_byte", [False, True], ids=["prefixes0-5", "prefix1"])
+@pytest.mark.parametrize("window", [0, 256, 16384])
+@pytest.mark.parametrize("skew", [False, "dense"])
+def test_pooled_families_vs_oracle(pooled_ctx, skew, window, one_byte):
+    """one_byte: every claim's prefix is 1 byte (every reference claim), so the pooled MD5 / SHA-1 families hash the
+    line copy's padded messages (k_pair_test<..., POOL, PADDED>)."""
+    rows, chosen, gt_now, reqs, want = _world(skew, one_byte)
+    store = SyncStore.from_rows(rows, ctx=pooled_ctx)
+    served = [MetaMessage(n, i, SyncDistribution(d, p, None)) for n, i, d, p, _ in chosen]
+    com = SyncCommunity(store, served, global_time=gt_now)
     store.ctx.set_window(window)
     try:
         results = [(limit, com.respond(reqs, byte_limit=limit)) for limit in (5120, 1 << 40)]
     finally:
         store.ctx.set_window(0)
     for limit, got in results:
-        for q, ob, g in zip(reqs, oracle_blooms, got):
-            want = sync_ref.respond_lists(conn, served_oracle, (q.time_low, q.time_high, q.offset, q.modulo), ob,
-                                          gt_now, limit, False)
-            assert store.rowid[g].tolist() == want, (q.time_low, q.time_high, q.modulo, q.offset, limit)
+        for i, (q, g) in enumerate(zip(reqs, got)):
+            assert store.rowid[g].tolist() == want[i, limit], (q.time_low, q.time_high, q.modulo, q.offset, limit)

@@ -53,11 +53,13 @@ def oracle_metas():
     return [dict(name=n, id=i, direction=d, priority=p, pruning=pr) for n, i, d, p, pr in METAS]
 
 
-@pytest.mark.parametrize("window", [0, 256, 4160])
-@pytest.mark.parametrize("skew", [False, True, "dense"])
-def test_respond_vs_oracle(skew, window):
-    """window caps the responder's window (dsy_ctx_set_window): 0 is the default growing window; 256 and 4160 force
-    claims across many windows, so the resumable (meta, candidate, sub-row) cursor is exercised in every direction."""
+_SCALE = {}  # skew -> the store, its sqlite copy and the 96 claims: shared by the three windows of one skew
+
+
+def _scale_world(skew):
+    """(the Python oracle's filter builds are most of a case's time, and nothing here depends on the window)"""
+    if skew in _SCALE:
+        return _SCALE[skew]
     seed = {False: 0, True: 1, "dense": 2}[skew]
     rows, conn = build(11 + seed, 60_000, 200_000 if skew is False else 5_000, skew)
     store = SyncStore.from_rows(rows)
@@ -83,6 +85,16 @@ def test_respond_vs_oracle(skew, window):
         assert bf.bytes == ob.to_bytes()
         reqs.append(ClaimRequest(lo, hi, modulo, offset, bf))
         oracle_blooms.append(ob)
+    _SCALE[skew] = (conn, store, com, gt_now, reqs, oracle_blooms)
+    return _SCALE[skew]
+
+
+@pytest.mark.parametrize("skew", [False, True, "dense"])
+@pytest.mark.parametrize("window", [0, 256, 4160])
+def test_respond_vs_oracle(skew, window):
+    """window caps the responder's window (dsy_ctx_set_window): 0 is the default growing window; 256 and 4160 force
+    claims across many windows, so the resumable (meta, candidate, sub-row) cursor is exercised in every direction."""
+    conn, store, com, gt_now, reqs, oracle_blooms = _scale_world(skew)
     store.ctx.set_window(window)
     try:
         results = [(inc, limit, com.respond(reqs, include_inactive=inc, byte_limit=limit))
