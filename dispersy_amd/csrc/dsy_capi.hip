@@ -82,6 +82,8 @@ struct RespondJob {
     uint8_t* h_in = nullptr;   // pinned staging (upload region, then host-mapped status)
     uint8_t* h_io = nullptr;
     uint32_t* h_act0 = nullptr;
+    uint32_t* h_act_next = nullptr;  // pinned: a later window's active list (never the staged upload k_fill_first reads)
+    uint64_t windows = 0;            // windows enqueued; the pack kernel numbers each in the status (kStatusSeq)
     bool act0_identity = true;  // h_act0[a] == a (k_fill_first may then map slot a to claim a without the list)
     const uint32_t* d_slots = nullptr;
     uint32_t* d_act = nullptr;
@@ -2087,7 +2089,7 @@ static int job_window(dsy_ctx* c, RespondSlot& sl) {
     }
     L.n_act = (uint32_t)n_act;
     if (!jb.first) {  // the first window's list went up with the claims
-        uint32_t* h_act = (uint32_t*)jb.h_in;  // the staged claims are on the device already: reuse the space
+        uint32_t* h_act = jb.h_act_next;
         size_t a = 0;
         for (auto& fa : jb.fam_active)
             for (uint32_t r : fa) h_act[a++] = r;
@@ -2239,6 +2241,7 @@ static int job_window(dsy_ctx* c, RespondSlot& sl) {
     // up and reads the status
     static const bool ev_marker = getenv("DSY_EVENT_MARKER") != nullptr;  // A/B: the event as a separate record
     HIP_TRY(launch_pack(L, (uint64_t*)jb.d_packed, (uint64_t*)jb.d_packed_off, nullptr, ev_marker ? nullptr : sl.ev_done));
+    ++jb.windows;
     if (ev_marker) HIP_TRY(hipEventRecord(sl.ev_done, st));
     if (g_host_profile && !jb.hp[2]) jb.hp[2] = host_us();  // first window enqueued
     return DSY_OK;
@@ -2373,12 +2376,14 @@ static int job_start(dsy_ctx* c, RespondSlot& sl, const dsy_store* s, const Clai
         HIP_TRY(hipMemsetAsync(d_pool_counts, 0, sizeof(PoolCounts), st));
     }
     uint8_t* h_in;
-    if ((rc = stage_get(w, in_b + kHostHead + act_done_b, &h_in))) return rc;
+    if ((rc = stage_get(w, in_b + kHostHead + act_done_b + (size_t)R * 4, &h_in))) return rc;
     jb.h_in = h_in;
     jb.d_in = d_in;
     jb.d_io = d_io;
     uint8_t* h_io = h_in + in_b;  // host-mapped status
     jb.h_io = h_io;
+    jb.h_act_next = (uint32_t*)(h_io + kHostHead + act_done_b);
+    jb.windows = 0;
     std::memset(h_io, 0, kHostHead);  // totals stay zero if no window runs (R == 0)
     {
         DevRequest* dq = (DevRequest*)h_in;
@@ -2570,6 +2575,70 @@ static int job_status(const RespondJob& jb) {
     return DSY_OK;
 }
 
+// A window's status check failed: when k_pair_test's task-record check tripped, audit the window's task records
+// (k_task_audit: the window's state and records are intact until the next window) and name the first bad one.
+static int job_status_audit(dsy_ctx* c, RespondSlot& sl, int rc) {
+    const RespondJob& jb = sl.job;
+    const uint64_t g = ((const volatile uint64_t*)jb.h_io)[kStatusGuard];
+    if (!((g >> (8 * kGuardTask)) & 0xff)) return rc;
+    const std::string first = dsy_last_error();
+    void* d_out;
+    if (ws_get(sl.w, "task_audit", 128, &d_out)) return rc;
+    unsigned long long h[10] = {};
+    if (hipMemsetAsync(d_out, 0, 80, c->stream) != hipSuccess || launch_task_audit(jb.L, (unsigned long long*)d_out) ||
+        hipMemcpyAsync(h, d_out, 80, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return rc;
+    // that claim's records and state on the host: which slots are missing, which are placed twice, and the window's
+    // path (split part / slice / one workgroup) from its cursor and plan
+    std::string more;
+    const uint64_t a = h[1], r = h[2], n = h[4], W = h[8];
+    if (h[0] && n && n <= (1ull << 22)) {
+        std::vector<PairTask> tk(n);
+        ReqState S{};
+        Plan P{};
+        if (hipMemcpyAsync(tk.data(), jb.L.task + a * W, n * sizeof(PairTask), hipMemcpyDeviceToHost, c->stream) ==
+                hipSuccess &&
+            hipMemcpyAsync(&S, jb.L.state + r, sizeof S, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+            hipStreamSynchronize(c->stream) == hipSuccess) {
+            if (S.win_meta < jb.J)
+                (void)hipMemcpy(&P, jb.L.plans + r * jb.J + S.win_meta, sizeof P, hipMemcpyDeviceToHost);
+            std::vector<uint32_t> seen(n, 0);
+            uint64_t stale = 0, dup = 0, first_stale = ~0ull, last_stale = 0;
+            for (uint64_t i = 0; i < n; ++i) {
+                if (tk[i].slot >= n) {
+                    ++stale;
+                    first_stale = std::min(first_stale, i);
+                    last_stale = i;
+                } else if (seen[tk[i].slot]++) {
+                    ++dup;
+                }
+            }
+            uint64_t missing = 0, first_missing = ~0ull;
+            for (uint64_t t = 0; t < n; ++t)
+                if (!seen[t]) {
+                    ++missing;
+                    first_missing = std::min(first_missing, t);
+                }
+            char buf[512];
+            snprintf(buf, sizeof buf, "; claim %llu: %llu stale positions [%llu..%llu], %llu slots placed twice, %llu "
+                     "missing (first %llu); state meta %u cand %llu sub %llu win %u/%llu/%llu exhausted %u done %u; plan "
+                     "mode %u dir %u ncand %llu dense %u span %llu..%llu",
+                     (unsigned long long)r, (unsigned long long)stale, (unsigned long long)first_stale,
+                     (unsigned long long)last_stale, (unsigned long long)dup, (unsigned long long)missing,
+                     (unsigned long long)first_missing, S.meta, (unsigned long long)S.cand, (unsigned long long)S.sub,
+                     S.win_meta, (unsigned long long)S.win_cand, (unsigned long long)S.win_sub, S.exhausted, S.done,
+                     P.mode, P.dir, (unsigned long long)P.ncand, P.dense, (unsigned long long)P.a, (unsigned long long)P.b);
+            more = buf;
+        }
+    }
+    return fail(DSY_EINTERNAL, "%s; audit: %llu bad task records in %llu claims, e.g. window slot %llu (claim %llu) "
+                "record %llu of n_window %llu: off %llu len %llu slot %llu (W %llu, line copy %llu B, call R %u J %u, "
+                "window %llu)%s",
+                first.c_str(), h[0], h[9], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8],
+                (unsigned long long)jb.L.st.lines_bytes, jb.R, jb.J, (unsigned long long)jb.windows, more.c_str());
+}
+
 // Wait for the job's windows, run the further windows its unfinished claims need, and return its results.
 static int job_finish(dsy_ctx* c, RespondSlot& sl, uint64_t** d_packed, uint64_t** d_packed_off, uint64_t* total_pairs) {
     RespondJob& jb = sl.job;
@@ -2583,8 +2652,23 @@ static int job_finish(dsy_ctx* c, RespondSlot& sl, uint64_t** d_packed, uint64_t
         const double w0 = g_host_profile ? host_us() : 0.0;
         HIP_TRY(hipEventSynchronize(sl.ev_done));  // this job's window, not what later batches queued behind it
         if (g_host_profile) jb.hp_wait += host_us() - w0;
+        // the window's status must be the one its pack kernel numbered: a status read before it is visible would
+        // steer the next window (its claims, and the host's reuse of the staging) from the previous window's state
+        if (((const volatile uint64_t*)jb.h_io)[kStatusSeq] != jb.windows) {
+            HIP_TRY(hipStreamSynchronize(st));
+            const uint64_t seq = ((const volatile uint64_t*)jb.h_io)[kStatusSeq];
+            static bool noted = false;
+            if (!noted) {
+                noted = true;
+                fprintf(stderr, "dsybloom: window %llu's status was not visible at its completion event (seq %llu); "
+                        "synchronised the stream\n", (unsigned long long)jb.windows, (unsigned long long)seq);
+            }
+            if (seq != jb.windows)
+                return fail(DSY_EINTERNAL, "internal: window %llu's status not visible after a stream synchronise "
+                            "(seq %llu)", (unsigned long long)jb.windows, (unsigned long long)seq);
+        }
         // capacity overflow can only come from a wrong min_len bound; report it loudly
-        if (int rc = job_status(jb)) return rc;
+        if (int rc = job_status(jb)) return job_status_audit(c, sl, rc);
         const volatile uint8_t* done = jb.h_io + kHostHead;
         size_t a = 0, left = 0;
         for (auto& fa : jb.fam_active) {

@@ -155,7 +155,10 @@ enum { kCntPairs = 0, kCntBlocks = 1, kCntBytes = 2, kCntUseful = 3, kCntSlots =
 // host-mapped status words after the kCntN totals: [kStatusOverflow] a claim overflowed its output capacity
 // (k_compact); [kStatusGuard] one byte per device-side bounds check that tripped (kGuard*): an index the responder
 // computed fell outside the buffer it addresses -- the access is skipped and the call fails with DSY_EINTERNAL
-enum { kStatusOverflow = kCntN, kStatusGuard = kCntN + 1 };
+enum { kStatusOverflow = kCntN, kStatusGuard = kCntN + 1, kStatusSeq = kCntN + 2 };
+// [kStatusSeq] the number of the window whose pack kernel folded the status (counter slot kCntSeq keeps the count on
+// the device): the host checks it after the window's completion event
+static constexpr uint32_t kCntSeq = kCntN - 1;
 enum { kGuardSortPos = 0, kGuardTask = 1, kGuardPack = 2, kGuardWindow = 3 };
 __device__ __forceinline__ void guard_trip(uint64_t* h_status, int which) {
     ((volatile uint8_t*)&h_status[kStatusGuard])[which] = 1;
@@ -295,6 +298,8 @@ hipError_t launch_pair_test_list(const RespondLaunch& L, int kind, uint32_t chun
 hipError_t launch_pair_test_pooled(const RespondLaunch& L, int kind, uint32_t chunk, bool long_prefix, bool padded,
                                    uint32_t fam, const uint32_t* d_list, uint32_t n);
 hipError_t launch_compact(const RespondLaunch& L);
+// diagnostics after a kGuardTask trip (k_task_audit): out[10] u64, zeroed by the caller
+hipError_t launch_task_audit(const RespondLaunch& L, unsigned long long* out);
 // done (optional): an event the last pack kernel's dispatch records when it completes
 hipError_t launch_pack(const RespondLaunch& L, uint64_t* packed, uint64_t* packed_offsets, uint64_t* d_scan_tmp,
                        hipEvent_t done = nullptr);

@@ -1568,6 +1568,11 @@ __device__ __forceinline__ void fold_status(const RespondLaunch& L) {
         for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
         if (lane == 0) L.h_status[k] = v;
     }
+    if (lane == 0) {  // this window's number (copy 0's spare counter slot), after its totals
+        const uint64_t seq = L.counters[kCntSeq] + 1;
+        L.counters[kCntSeq] = seq;
+        L.h_status[kStatusSeq] = seq;
+    }
 }
 
 // position of the k-th set bit of w (k < popcount(w))
@@ -1851,6 +1856,42 @@ hipError_t launch_fill_first(const RespondLaunch& L, const void* h_src, void* d_
     hipLaunchKernelGGL(k_fill_first, dim3(L.n_act), dim3(kFillThreads), 0, L.stream, L, (const uint4*)h_src,
                        (uint4*)d_dst, (uint32_t)(in_bytes / 16), (uint4*)d_counters, (uint32_t)(counter_bytes / 16),
                        per_claim_cap, h_act);
+    return hipGetLastError();
+}
+
+// Diagnostics, run only after a window whose k_pair_test tripped kGuardTask: every listed claim's task records
+// [0, n_window) checked as k_pair_test checks them.  out[0]: bad records; out[1..8]: one of them (a_slot, claim, index,
+// n_window, off, len, slot, W); out[9]: claims with a bad record.
+__global__ void __launch_bounds__(256) k_task_audit(RespondLaunch L, unsigned long long* __restrict__ out) {
+    __shared__ uint32_t bad_here;
+    const uint32_t a_slot = blockIdx.x;
+    const uint32_t r = L.act[a_slot];
+    const uint64_t n = L.state[r].n_window, W = L.window;
+    if (threadIdx.x == 0) bad_here = 0;
+    __syncthreads();
+    for (uint64_t i = threadIdx.x; i < n && i < W; i += blockDim.x) {
+        const PairTask tk = L.task[(uint64_t)a_slot * W + i];
+        if (!packet_in_lines(tk.off, tk.len, L.st.lines_bytes) || tk.slot >= n) {
+            atomicAdd(&bad_here, 1u);
+            if (atomicAdd(&out[0], 1ull) == 0) {
+                out[1] = a_slot;
+                out[2] = r;
+                out[3] = i;
+                out[4] = n;
+                out[5] = tk.off;
+                out[6] = tk.len;
+                out[7] = tk.slot;
+                out[8] = W;
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && bad_here) atomicAdd(&out[9], 1ull);
+}
+
+hipError_t launch_task_audit(const RespondLaunch& L, unsigned long long* out) {
+    if (!L.n_act) return hipSuccess;
+    hipLaunchKernelGGL(k_task_audit, dim3(L.n_act), dim3(256), 0, L.stream, L, out);
     return hipGetLastError();
 }
 

@@ -3,6 +3,7 @@
 the same kernel as the headline's).  Prints the leg's JSON record.
 
 usage: python tools/leg_run.py 5 [bench.py options]     (config 5, the heavy-tailed store; --cpu-claims 0 implied)
+       DSY_LEG_RANK=r: the claims rank r of a multi-GPU run draws (its seed), in this one process
 """
 import json
 import os
@@ -23,7 +24,7 @@ def main():
     dev = torch.device("cuda", 0)
     ctx = _native.Context(0)
     if leg == "5":
-        out = bench.heavy_tail(args, ctx, ctx.lib, dev, 0, 1, None)
+        out = bench.heavy_tail(args, ctx, ctx.lib, dev, int(os.environ.get("DSY_LEG_RANK", "0")), 1, None)
     else:
         raise SystemExit("unknown leg %r" % leg)
     print(json.dumps(out))
