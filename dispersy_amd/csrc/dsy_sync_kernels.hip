@@ -1178,7 +1178,19 @@ __global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_waves_per_
         if (part > 0) return;
     }
     // (k_fill_sort runs after this launch whenever it has parts: a big window may leave its placement to it)
-    fill_claim(L, a_slot, r, L.reqs[r], S, S->meta, S->cand, S->sub, [&](uint32_t j) { return plans[j]; }, clk0, clk0,
+    // The window's start cursor, read once for the workgroup: fill_claim's thread 0 writes the next cursor into S when
+    // its selection ends, and a wave that read S only after that (waves of a workgroup start at different times; one
+    // scheduled late under a busy GPU did) would select nothing -- its pairs then missing from the window's sort,
+    // their task records left from an earlier window (k_pair_test's kGuardTask check caught it; tools/r6_cfg5_audit.sh)
+    __shared__ uint32_t c_meta;
+    __shared__ uint64_t c_cand, c_sub;
+    if (threadIdx.x == 0) {
+        c_meta = S->meta;
+        c_cand = S->cand;
+        c_sub = S->sub;
+    }
+    __syncthreads();
+    fill_claim(L, a_slot, r, L.reqs[r], S, c_meta, c_cand, c_sub, [&](uint32_t j) { return plans[j]; }, clk0, clk0,
                gridDim.y > 1);
 }
 
