@@ -558,6 +558,10 @@ int dsy_ctx_create(int device, dsy_ctx** out) {
     if (const char* v = getenv("DSY_POOL")) c->pool_kinds = (uint32_t)strtoul(v, nullptr, 0);
     if (const char* v = getenv("DSY_POOL_QUEUE")) c->pool_queue = atoi(v);
     if (const char* v = getenv("DSY_POOL_DEAL")) c->pool_deal = atoi(v);
+    {  // diagnostics, process-wide: every ctx creation sets it (0 without the variable)
+        const char* v = getenv("DSY_FILL_SKEW");
+        set_fill_skew(v ? (uint32_t)strtoul(v, nullptr, 0) : 0u);
+    }
     if (const char* v = getenv("DSY_POOL_SCAN")) c->pool_scan = atoi(v);
     if (const char* v = getenv("DSY_PAIR_PRIO")) c->pair_prio = atoi(v);
     if (const char* v = getenv("DSY_BULK_ZERO")) c->bulk_zero = atoi(v);

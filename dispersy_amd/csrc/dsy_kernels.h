@@ -284,6 +284,10 @@ hipError_t launch_setup(const RespondLaunch& L, const void* h_src, void* d_dst, 
                         size_t zero_bytes, uint64_t per_claim_cap);
 static constexpr uint32_t kPackFusedMax = 8192;  // claims packed by one launch (k_pack_fused)
 hipError_t launch_fill(const RespondLaunch& L);
+// diagnostics (DSY_FILL_SKEW, read when a ctx is created; process-wide): k_fill holds back waves 1-3 of a claim's
+// one-workgroup fill by `sleeps` x s_sleep(127) before they read the window's cursor -- a wave scheduled late, on
+// purpose (tests/test_fill_skew_gpu.py)
+hipError_t set_fill_skew(uint32_t sleeps);
 // first window of a one-meta call with device-side capacities: k_setup fused into k_fill (every claim's plan, state and
 // window in one launch); h_act: the first active list in pinned host memory, or nullptr when window slot a is claim a
 hipError_t launch_fill_first(const RespondLaunch& L, const void* h_src, void* d_dst, size_t in_bytes, void* d_counters,

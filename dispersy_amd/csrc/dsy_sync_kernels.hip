@@ -1143,6 +1143,10 @@ __global__ void __launch_bounds__(256) k_pool_scatter(RespondLaunch L, const uin
     }
 }
 
+__device__ uint32_t g_fill_skew = 0;  // set_fill_skew (diagnostics)
+
+hipError_t set_fill_skew(uint32_t sleeps) { return hipMemcpyToSymbol(HIP_SYMBOL(g_fill_skew), &sleeps, sizeof sleeps); }
+
 __global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) k_fill(RespondLaunch L) {
     const uint32_t a_slot = blockIdx.x, part = blockIdx.y;
     const uint64_t clk0 = L.fill_clock ? __builtin_amdgcn_s_memtime() : 0;
@@ -1184,6 +1188,8 @@ __global__ void __launch_bounds__(kFillThreads) __attribute__((amdgpu_waves_per_
     // their task records left from an earlier window (k_pair_test's kGuardTask check caught it; tools/r6_cfg5_audit.sh)
     __shared__ uint32_t c_meta;
     __shared__ uint64_t c_cand, c_sub;
+    if (const uint32_t skew = g_fill_skew; skew && threadIdx.x >= 64)
+        for (uint32_t i = 0; i < skew; ++i) __builtin_amdgcn_s_sleep(127);
     if (threadIdx.x == 0) {
         c_meta = S->meta;
         c_cand = S->cand;
