@@ -146,7 +146,7 @@ struct dsy_ctx {
     // DSY_BLOOM_LINES at creation: bit k = hash kind k's single-filter hashing (k_bloom) stages whole lines
     // (hash_key_dma_packed); otherwise LDS-DMA windows at each key's own alignment (hash_key_dma_reg).  Same box,
     // config 1's 10 M-key test (profiles/cfg1_ab_r6.json): MD5 2248 us with lines vs 2294 us with windows; SHA-1
-    // (VALU-bound) 3101 vs 3071 us, kept on lines for 1.17x instead of 1.51x the algorithmic HBM bytes
+    // (VALU-bound) 3101 vs 3071 us, kept on lines for 1.18x instead of 1.51x the algorithmic HBM bytes
     uint32_t bloom_lines = (1u << DSY_MD5) | (1u << DSY_SHA1);
     // DSY_POOL at creation: bit k = hash kind k's responder pairs are pooled across claims (k_pool_scatter) -- MD5,
     // SHA-1 and SHA-256 only; DSY_POOL_QUEUE: the pooled hashing takes its wave-tasks from a queue.  Off by default:
