@@ -32,6 +32,28 @@ def test_gpu_engine_matches_oracle_engine():
     assert sg.tested >= so.tested
 
 
+def test_gpu_engine_matches_oracle_at_bench_shape():
+    """The bench's gossip configuration (universe 10 000 packets, 100 initial per peer, MTU filters, 5 KiB budget) at
+    20 000 peers -- 13x the peers above, where every peer's store is near the filter's capacity by the second round --
+    against the oracle engine, peer by peer, for two rounds (the 1 M-peer bench run is checked by its store checksum
+    only; the oracle takes ~18 s per round here)."""
+    p, u, initial = 20_000, 10_000, 100
+    blob, offs = make_universe(u, seed=5)
+    dev = torch.device("cuda", 0)
+    cg = make_config(p, u, 0, 1, seed=21)
+    co = make_config(p, u, 0, 1, seed=21)
+    g, o = GpuEngine(cg, blob, offs, dev), OracleEngine(co, blob, offs)
+    g.seed(initial)
+    o.seed(initial)
+    sg, so = EpidemicSim(g, cg, device=dev), EpidemicSim(o, co)
+    for r in range(2):
+        sg.round(r)
+        so.round(r)
+        assert sg.global_stats() == so.global_stats(), r
+    gb = g.bits.cpu().numpy().view(np.uint32).reshape(p, cg.words)
+    assert (gb == o.bitsets()).all()
+
+
 def test_two_rank_routing_in_one_process():
     """Two GpuEngines own halves of the peers; their records are exchanged by slicing, as all_to_all_single does."""
     blob, offs = make_universe(U, seed=4)
